@@ -1,0 +1,199 @@
+/* libvqa_hip — MI355X (gfx950) kernels for the ResNet+T5+SGA VQA training step.
+ *
+ * Drop-in boundary.  The reference
+ * (shiv-vignesh/T5-Resnet-VQA) has no FFI: its hot path is PyTorch eager
+ * ops under `ResnetVQAModel.forward` (model/resnet_vqa_model.py:101-165),
+ * `SGA.forward` (model/multi_head_vision_text_attn.py:145-158) and
+ * `train_one_step` (trainer/faster_rcnn_vqa_trainer.py:391-406).  Each export
+ * below replaces the ATen/cuDNN/cuBLAS calls of one op of that path (cited per
+ * function).  Conventions:
+ *   - plain C ABI: raw device pointers, sizes, an explicit hipStream_t;
+ *   - every call returns 0 on success, else a VQA_ERR_* / hipError_t code; the
+ *     message is in vqa_last_error() (thread-local); nothing throws;
+ *   - the caller owns every buffer; the library allocates nothing per call,
+ *     so every call is safe inside hipStream capture (hipGraph);
+ *   - bf16 tensors are passed as void* (raw bfloat16 bits), fp32 as float*.
+ */
+#ifndef VQA_HIP_H
+#define VQA_HIP_H
+
+#include <hip/hip_runtime.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VQA_ABI_VERSION 1
+#define VQA_OK 0
+#define VQA_ERR_INVALID 1000
+
+int vqa_abi_version(void);
+const char* vqa_last_error(void);
+
+/* ------------------------------------------------------------------ GEMM ---
+ * C[m,n] = epilogue( alpha * sum_k A(m,k) * B(k,n) ), bf16 operands, fp32 MFMA
+ * accumulation (v_mfma_f32_32x32x16_bf16).  Replaces every nn.Linear
+ * (multi_head_vision_text_attn.py:31-34, 92-93; TF t5 q/k/v/o/wi/wo;
+ * resnet_vqa_model.py:19, 85) forward, input-grad and weight-grad, and the
+ * implicit-GEMM convolutions (torchvision conv layers, ConvTranspose2d
+ * resnet_vqa_model.py:72-78).
+ *   a_trans = 0: A(m,k) = a[m*lda + k]   a_trans = 1: A(m,k) = a[k*lda + m]
+ *   b_trans = 0: B(k,n) = b[n*ldb + k]   b_trans = 1: B(k,n) = b[k*ldb + n]
+ * a_conv: A(m,k) is the implicit im2col of an NHWC bf16 activation
+ *   (m = output pixel (img,oh,ow), k = (kh,kw,c)); requires a_trans = 0.
+ * b_conv: B(k,n) is the implicit im2col with k = output pixel, n = (kh,kw,c);
+ *   requires b_trans = 1 (weight-gradient of a convolution).
+ * Epilogue order: v = alpha*acc; +bias[n]; +res(m,n); relu; *(mask(m,n) > 0);
+ *   c32 = v + beta*c32 (c32 may be NULL); c16 = bf16(v) (may be NULL).
+ * batch > 1 offsets a, b, c32, c16 by their strides and res/mask by stride_res. */
+typedef struct vqa_conv_geom {
+  int n, h, w, c;          /* NHWC input */
+  int oh, ow;              /* output spatial size */
+  int kh, kw, stride, pad;
+} vqa_conv_geom;
+
+typedef struct vqa_gemm_desc {
+  const void* a; long long lda; int a_trans;
+  const void* b; long long ldb; int b_trans;
+  int m, n, k;
+  float* c32; long long ldc32;
+  void* c16; long long ldc16;
+  const float* bias;
+  const float* res32; const void* res16; long long ldres;
+  const void* mask16; long long ldmask;
+  float alpha, beta; int relu;
+  int a_conv; vqa_conv_geom ga;
+  int b_conv; vqa_conv_geom gb;
+  int batch; long long stride_a, stride_b, stride_c32, stride_c16, stride_res;
+} vqa_gemm_desc;
+
+int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
+
+/* ------------------------------------------------------------- attention ---
+ * Multi-head attention core for Lq, Lk <= 64 (one workgroup per (b, head)):
+ *   S = scale * Q K^T (+ bias[h,i,j]) (+ finfo(f32).min where key_mask[b,j]==0)
+ *   P = softmax_j(S), O = P V.
+ * Replaces MHAtt.att (multi_head_vision_text_attn.py:73-86; scale 1/sqrt(96),
+ * 8 heads, no mask) and T5 eager attention (TF modeling_t5.py:144-173; scale 1,
+ * 12 heads, relative bias, key mask).  Element (b, i, h, e) of Q lives at
+ * q[(b*lq + i)*ldq + h*dh + e] (likewise K, V, O, dO, dQ, dK, dV), so Q/K/V are
+ * read in place from fused projection outputs.  p: saved P [B, H, Lq, Lk].
+ * Backward: dS = P (dP - rowsum(P dP)), dQ = scale dS K, dK = scale dS^T Q,
+ * dV = P^T dO; dbias[h,i,j] += sum_b dS (atomic) when dbias != NULL. */
+typedef struct vqa_attn_desc {
+  const void* q; long long ldq;
+  const void* k; long long ldk;
+  const void* v; long long ldv;
+  void* o; long long ldo;
+  float* p;
+  const float* bias;
+  const long long* key_mask;
+  int batch, heads, lq, lk, dh;
+  float scale;
+  const void* dout; long long lddo;
+  void* dq; long long lddq;
+  void* dk; long long lddk;
+  void* dv; long long lddv;
+  float* dbias;
+} vqa_attn_desc;
+
+int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t stream);
+int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t stream);
+
+/* ----------------------------------------------------------------- norms ---
+ * Rows of width d (d % 256 == 0, d <= 1024), fp32 in, fp32 and/or bf16 out.
+ * RMS: T5LayerNorm (TF modeling_t5.py:50-72): y = w * x * rsqrt(mean(x^2)+eps).
+ * LN:  nn.LayerNorm (multi_head_vision_text_attn.py:120-126), post-LN of SGA.
+ * Backward adds the residual gradient dres (may be NULL) into dx and reduces
+ * the weight gradients deterministically through ws
+ * (vqa_norm_bwd_workspace_floats(rows, d) floats). */
+int vqa_rmsnorm_fwd(const float* x, const float* w, float* y32, void* y16, float* rstd, int rows, int d, float eps,
+                    hipStream_t stream);
+int vqa_rmsnorm_bwd(const float* dy, const float* x, const float* rstd, const float* w, const float* dres,
+                    float* dx32, void* dx16, float* dw, float dw_beta, float* ws, int rows, int d,
+                    hipStream_t stream);
+int vqa_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y32, void* y16, float* mean,
+                      float* rstd, int rows, int d, float eps, hipStream_t stream);
+int vqa_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
+                      const float* dres, float* dx32, void* dx16, float* dgamma, float* dbeta, float* ws, int rows,
+                      int d, hipStream_t stream);
+int vqa_norm_bwd_workspace_floats(int rows, int d);
+/* out[c] = beta*out[c] + sum_p ws[p*stride + c] (fixed order) */
+int vqa_colsum_partials(const float* ws, int parts, long long stride, int cols, float* out, float beta,
+                        hipStream_t stream);
+
+/* ---------------------------------------------------------- elementwise ---
+ * vqa_image_to_nhwc8: NCHW fp32 [N,3,H,W] (collate ToTensor,
+ *   resnet_vqa_daquar_dataset.py:131-137) -> NHWC bf16 [N,H,W,8], ch 3..7 = 0.
+ * vqa_maxpool3x3s2_nhwc: torchvision ResNet maxpool (3, 2, pad 1), bf16 NHWC.
+ * vqa_colsum: out[c] = beta*out[c] + sum_r x[r*ld + c] (bias gradients of
+ *   every nn.Linear / ConvTranspose2d), ws = vqa_colsum_workspace_floats().
+ * vqa_embedding_fwd/bwd: T5 embed_tokens gather (TF modeling_t5.py:678) and
+ *   its dense scatter-add gradient (dtable must be zeroed by the caller).
+ * vqa_t5_relbias_fwd/bwd: compute_bias gather of the [buckets, H] table by a
+ *   precomputed bucket map [Lq*Lk] (TF modeling_t5.py:217-279) and its
+ *   scatter-add gradient (dtable zeroed by the caller). */
+int vqa_image_to_nhwc8(const float* img, void* out, int n, int h, int w, hipStream_t stream);
+int vqa_maxpool3x3s2_nhwc(const void* x, void* y, int n, int h, int w, int c, int oh, int ow, hipStream_t stream);
+int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long long ld, float* out, float beta, float* ws,
+               hipStream_t stream);
+int vqa_colsum_workspace_floats(int rows, int cols);
+int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int tokens, int d, int vocab,
+                      hipStream_t stream);
+int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab,
+                      hipStream_t stream);
+int vqa_t5_relbias_fwd(const float* table, const int* bucket, float* out, int heads, int lq, int lk,
+                       hipStream_t stream);
+int vqa_t5_relbias_bwd(const float* dbias, const int* bucket, float* dtable, int heads, int lq, int lk,
+                       hipStream_t stream);
+int vqa_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t stream);
+int vqa_zero(void* p, long long bytes, hipStream_t stream);
+
+/* ------------------------------------------------------------------ head ---
+ * AttentionPooler (resnet_vqa_model.py:14-26) + classification_layer +
+ * log_softmax + NLLLoss mean (:152-160).  fp32.  targets may be NULL in
+ * forward (loss is then not computed, like annotation_ids=None).
+ * ws = vqa_head_workspace_floats(batch, seq, d, answers) floats. */
+int vqa_head_fwd(const float* x, const float* wp, const float* bp, const float* wc, const float* bc,
+                 const long long* targets, float* att, float* pooled, float* logp, float* nll, float* loss,
+                 int batch, int seq, int d, int answers, hipStream_t stream);
+int vqa_head_bwd(const float* x, const float* att, const float* pooled, const float* logp, const long long* targets,
+                 const float* wp, const float* wc, float* dx32, void* dx16, float* dwp, float* dbp, float* dwc,
+                 float* dbc, float* ws, int batch, int seq, int d, int answers, hipStream_t stream);
+int vqa_head_workspace_floats(int batch, int seq, int d, int answers);
+
+/* ------------------------------------------------------------- optimiser ---
+ * clip_grad_norm_(1.0) + AdamW(amsgrad) + linear warmup/decay schedule
+ * (faster_rcnn_vqa_trainer.py:399-404, :231-287; TF optimization.py:101-107),
+ * device-resident so a whole step is graph-capturable.  `state` is a float[8]
+ * device block indexed by VQA_ST_*; vqa_optim_finalize reads STEP and writes
+ * the rest, then advances STEP. */
+#define VQA_MAX_GROUPS 8
+#define VQA_ST_STEP 0
+#define VQA_ST_GRAD_NORM 1
+#define VQA_ST_CLIP_COEF 2
+#define VQA_ST_LR_SCALE 3
+#define VQA_ST_BC1 4
+#define VQA_ST_BC2_SQRT 5
+
+typedef struct vqa_adamw_desc {
+  float* param; const float* grad;
+  float* exp_avg; float* exp_avg_sq; float* max_exp_avg_sq;
+  void* param16;                      /* bf16 shadow written after the update (may be NULL) */
+  long long n;
+  int ngroups;
+  long long group_end[VQA_MAX_GROUPS];/* exclusive end element of each contiguous group */
+  float group_lr[VQA_MAX_GROUPS];
+  float beta1, beta2, eps, weight_decay, grad_scale;
+  const float* state;
+} vqa_adamw_desc;
+
+int vqa_grad_sqnorm(const float* g, long long n, double* ws, int parts, hipStream_t stream);
+int vqa_optim_finalize(const double* ws, int parts, float grad_scale, float max_norm, int warmup, int total,
+                       float beta1, float beta2, float* state, hipStream_t stream);
+int vqa_adamw_amsgrad(const vqa_adamw_desc* d, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VQA_HIP_H */

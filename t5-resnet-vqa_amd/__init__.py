@@ -15,7 +15,7 @@ import importlib
 
 from . import synthetic  # noqa: F401  (numpy only)
 
-_LAZY = ("lib", "engine", "layout", "model", "trainer", "dp")
+_LAZY = ("lib", "ops", "engine", "layout", "model", "trainer", "dp")
 
 
 def __getattr__(name):

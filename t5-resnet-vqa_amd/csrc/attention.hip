@@ -1,0 +1,215 @@
+// Fused multi-head attention core, forward and backward, for the two short
+// attention shapes of the step (Lq, Lk <= 64):
+//   SGA  MHAtt.att   softmax(QK^T/sqrt(96)) V, 8 heads x 96     multi_head_vision_text_attn.py:73-86
+//   T5   attention   softmax(QK^T + relbias + mask) V, 12 x 64  TF/models/t5/modeling_t5.py:144-173
+// One workgroup per (batch, head).  Q/K/V/dO are staged in LDS as packed bf16
+// pairs ([rows][D/2+1] dwords, conflict-free for both the row-dot and the
+// column-axpy access), scores/probabilities in fp32, one wave per softmax row.
+// The whole (b,h) problem is at most 64x64x96, so everything stays on-chip; Q,
+// K and V are read straight out of the fused QKV projection output through
+// row strides (no head transposes in HBM).
+#include "common.h"
+
+namespace {
+
+constexpr float MASK_MIN = -3.4028234663852886e38f;     // torch.finfo(float32).min (additive key mask)
+
+struct AttnP {
+  const bf16_t *q, *k, *v; long ldq, ldk, ldv;
+  bf16_t* o; long ldo;
+  float* p;
+  const float* bias;
+  const long long* mask;
+  int heads, lq, lk, dh;
+  float scale;
+  const bf16_t* dout; long lddo;
+  bf16_t *dq, *dk, *dv; long lddq, lddk, lddv;
+  float* dbias;
+};
+
+__device__ __forceinline__ float2 unpack(uint32_t u) {
+  return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+}
+__device__ __forceinline__ uint32_t pack(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+// stage rows [n][dh] bf16 (row stride ld, head offset) into LDS [n][dh/2+1] dwords
+__device__ __forceinline__ void stage(uint32_t* dst, const bf16_t* src, long ld, int n, int dh) {
+  const int w2 = dh / 2, st = w2 + 1, c8 = dh / 8;
+  for (int idx = threadIdx.x; idx < n * c8; idx += blockDim.x) {
+    const int r = idx / c8, c = idx - r * c8;
+    const uint4 u = *reinterpret_cast<const uint4*>(src + (long)r * ld + c * 8);
+    uint32_t* d = dst + r * st + c * 4;
+    d[0] = u.x; d[1] = u.y; d[2] = u.z; d[3] = u.w;
+  }
+}
+
+__device__ __forceinline__ float rowdot(const uint32_t* a, const uint32_t* b, int w2) {
+  float s0 = 0.f, s1 = 0.f;
+  for (int e = 0; e < w2; ++e) {
+    const float2 x = unpack(a[e]), y = unpack(b[e]);
+    s0 = fmaf(x.x, y.x, s0);
+    s1 = fmaf(x.y, y.y, s1);
+  }
+  return s0 + s1;
+}
+
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnP P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  const int b = blockIdx.x / P.heads, h = blockIdx.x - b * P.heads;
+  const int lq = P.lq, lk = P.lk, dh = P.dh, w2 = dh / 2, st = w2 + 1, sst = lk + 1;
+  uint32_t* Qs = sm;
+  uint32_t* Ks = Qs + lq * st;
+  uint32_t* Vs = Ks + lk * st;
+  float* S = reinterpret_cast<float*>(Vs + lk * st);
+  stage(Qs, P.q + (long)b * lq * P.ldq + h * dh, P.ldq, lq, dh);
+  stage(Ks, P.k + (long)b * lk * P.ldk + h * dh, P.ldk, lk, dh);
+  stage(Vs, P.v + (long)b * lk * P.ldv + h * dh, P.ldv, lk, dh);
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < lq * lk; idx += blockDim.x) {
+    const int i = idx / lk, j = idx - i * lk;
+    float s = rowdot(Qs + i * st, Ks + j * st, w2) * P.scale;
+    if (P.bias) s += P.bias[((long)h * lq + i) * lk + j];
+    if (P.mask && P.mask[(long)b * lk + j] == 0) s += MASK_MIN;
+    S[i * sst + j] = s;
+  }
+  __syncthreads();
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int i = wv; i < lq; i += 4) {
+    const float s = l < lk ? S[i * sst + l] : -INFINITY;
+    const float m = wave_max(s);
+    const float e = l < lk ? __expf(s - m) : 0.f;
+    const float z = wave_sum(e);
+    const float pr = e / z;
+    if (l < lk) {
+      S[i * sst + l] = pr;
+      if (P.p) P.p[(((long)b * P.heads + h) * lq + i) * lk + l] = pr;
+    }
+  }
+  __syncthreads();
+  // O[i][2e..2e+1] = sum_j P[i][j] V[j][2e..2e+1]
+  for (int idx = threadIdx.x; idx < lq * w2; idx += blockDim.x) {
+    const int i = idx / w2, e = idx - i * w2;
+    float a0 = 0.f, a1 = 0.f;
+    for (int j = 0; j < lk; ++j) {
+      const float pr = S[i * sst + j];
+      const float2 v = unpack(Vs[j * st + e]);
+      a0 = fmaf(pr, v.x, a0);
+      a1 = fmaf(pr, v.y, a1);
+    }
+    reinterpret_cast<uint32_t*>(P.o + ((long)b * lq + i) * P.ldo + h * dh)[e] = pack(a0, a1);
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnP P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  const int b = blockIdx.x / P.heads, h = blockIdx.x - b * P.heads;
+  const int lq = P.lq, lk = P.lk, dh = P.dh, w2 = dh / 2, st = w2 + 1, sst = lk + 1;
+  uint32_t* Qs = sm;
+  uint32_t* Ks = Qs + lq * st;
+  uint32_t* Vs = Ks + lk * st;
+  uint32_t* Os = Vs + lk * st;                       // dO
+  float* Ps = reinterpret_cast<float*>(Os + lq * st);
+  float* dS = Ps + lq * sst;
+  stage(Qs, P.q + (long)b * lq * P.ldq + h * dh, P.ldq, lq, dh);
+  stage(Ks, P.k + (long)b * lk * P.ldk + h * dh, P.ldk, lk, dh);
+  stage(Vs, P.v + (long)b * lk * P.ldv + h * dh, P.ldv, lk, dh);
+  stage(Os, P.dout + (long)b * lq * P.lddo + h * dh, P.lddo, lq, dh);
+  const float* Pg = P.p + ((long)b * P.heads + h) * lq * lk;
+  for (int idx = threadIdx.x; idx < lq * lk; idx += blockDim.x) {
+    const int i = idx / lk, j = idx - i * lk;
+    Ps[i * sst + j] = Pg[idx];
+  }
+  __syncthreads();
+  // dP = dO V^T
+  for (int idx = threadIdx.x; idx < lq * lk; idx += blockDim.x) {
+    const int i = idx / lk, j = idx - i * lk;
+    dS[i * sst + j] = rowdot(Os + i * st, Vs + j * st, w2);
+  }
+  __syncthreads();
+  // dS = P (dP - sum_j P dP)
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int i = wv; i < lq; i += 4) {
+    const float pr = l < lk ? Ps[i * sst + l] : 0.f;
+    const float dp = l < lk ? dS[i * sst + l] : 0.f;
+    const float di = wave_sum(pr * dp);
+    if (l < lk) {
+      const float ds = pr * (dp - di);
+      dS[i * sst + l] = ds;
+      if (P.dbias) atomicAdd(P.dbias + ((long)h * lq + i) * lk + l, ds);
+    }
+  }
+  __syncthreads();
+  // dQ = scale * dS K
+  for (int idx = threadIdx.x; idx < lq * w2; idx += blockDim.x) {
+    const int i = idx / w2, e = idx - i * w2;
+    float a0 = 0.f, a1 = 0.f;
+    for (int j = 0; j < lk; ++j) {
+      const float d = dS[i * sst + j];
+      const float2 kv = unpack(Ks[j * st + e]);
+      a0 = fmaf(d, kv.x, a0);
+      a1 = fmaf(d, kv.y, a1);
+    }
+    reinterpret_cast<uint32_t*>(P.dq + ((long)b * lq + i) * P.lddq + h * dh)[e] = pack(a0 * P.scale, a1 * P.scale);
+  }
+  // dK = scale * dS^T Q ; dV = P^T dO
+  for (int idx = threadIdx.x; idx < lk * w2; idx += blockDim.x) {
+    const int j = idx / w2, e = idx - j * w2;
+    float k0 = 0.f, k1 = 0.f, v0 = 0.f, v1 = 0.f;
+    for (int i = 0; i < lq; ++i) {
+      const float d = dS[i * sst + j], pr = Ps[i * sst + j];
+      const float2 qv = unpack(Qs[i * st + e]);
+      const float2 ov = unpack(Os[i * st + e]);
+      k0 = fmaf(d, qv.x, k0);
+      k1 = fmaf(d, qv.y, k1);
+      v0 = fmaf(pr, ov.x, v0);
+      v1 = fmaf(pr, ov.y, v1);
+    }
+    reinterpret_cast<uint32_t*>(P.dk + ((long)b * lk + j) * P.lddk + h * dh)[e] = pack(k0 * P.scale, k1 * P.scale);
+    reinterpret_cast<uint32_t*>(P.dv + ((long)b * lk + j) * P.lddv + h * dh)[e] = pack(v0, v1);
+  }
+}
+
+size_t fwd_smem(int lq, int lk, int dh) { return 4ul * ((lq + 2 * lk) * (dh / 2 + 1) + lq * (lk + 1)); }
+size_t bwd_smem(int lq, int lk, int dh) {
+  return 4ul * ((2 * lq + 2 * lk) * (dh / 2 + 1) + 2 * lq * (lk + 1));
+}
+
+int fill(AttnP& P, const vqa_attn_desc* d) {
+  VQA_REQUIRE(d && d->q && d->k && d->v, "attention: null q/k/v");
+  VQA_REQUIRE(d->lq > 0 && d->lk > 0 && d->lq <= 64 && d->lk <= 64, "attention: lq, lk must be in [1, 64]");
+  VQA_REQUIRE(d->dh % 8 == 0 && d->dh <= 256, "attention: head dim must be a multiple of 8");
+  VQA_REQUIRE(d->ldq % 8 == 0 && d->ldk % 8 == 0 && d->ldv % 8 == 0, "attention: strides must be multiples of 8");
+  P.q = (const bf16_t*)d->q; P.k = (const bf16_t*)d->k; P.v = (const bf16_t*)d->v;
+  P.ldq = d->ldq; P.ldk = d->ldk; P.ldv = d->ldv;
+  P.o = (bf16_t*)d->o; P.ldo = d->ldo;
+  P.p = d->p; P.bias = d->bias; P.mask = d->key_mask;
+  P.heads = d->heads; P.lq = d->lq; P.lk = d->lk; P.dh = d->dh; P.scale = d->scale;
+  P.dout = (const bf16_t*)d->dout; P.lddo = d->lddo;
+  P.dq = (bf16_t*)d->dq; P.dk = (bf16_t*)d->dk; P.dv = (bf16_t*)d->dv;
+  P.lddq = d->lddq; P.lddk = d->lddk; P.lddv = d->lddv;
+  P.dbias = d->dbias;
+  return VQA_OK;
+}
+
+}  // namespace
+
+extern "C" int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t s) {
+  AttnP P;
+  if (int rc = fill(P, d)) return rc;
+  VQA_REQUIRE(d->o, "vqa_attn_fwd: null output");
+  const size_t sm = fwd_smem(d->lq, d->lk, d->dh);
+  VQA_REQUIRE(sm <= 65536, "vqa_attn_fwd: shape needs %zu B of LDS (> 64 KiB)", sm);
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(d->batch * d->heads), dim3(256), sm, s, P);
+  return vqa::check_launch("vqa_attn_fwd");
+}
+
+extern "C" int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t s) {
+  AttnP P;
+  if (int rc = fill(P, d)) return rc;
+  VQA_REQUIRE(d->p && d->dout && d->dq && d->dk && d->dv, "vqa_attn_bwd: null P / dO / dQ / dK / dV");
+  VQA_REQUIRE(d->lddo % 8 == 0, "vqa_attn_bwd: dO stride must be a multiple of 8");
+  const size_t sm = bwd_smem(d->lq, d->lk, d->dh);
+  VQA_REQUIRE(sm <= 65536, "vqa_attn_bwd: shape needs %zu B of LDS (> 64 KiB)", sm);
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(d->batch * d->heads), dim3(256), sm, s, P);
+  return vqa::check_launch("vqa_attn_bwd");
+}

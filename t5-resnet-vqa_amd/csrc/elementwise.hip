@@ -1,0 +1,238 @@
+// Memory-bound helpers of the step: image layout change, max-pool, column sums
+// (bias gradients), T5 embedding gather / scatter-add, T5 relative-position
+// bias gather / scatter, casts and zeroing.  All 16-B vectorised where the
+// layout allows (cdna_hip_programming.md Guideline 13).
+#include "common.h"
+
+namespace {
+
+// NCHW fp32 [N,3,H,W] in [0,1] (collate ToTensor, resnet_vqa_daquar_dataset.py:131-137)
+// -> NHWC bf16 [N,H,W,8], channels 3..7 zero (the stem conv's K = 7*7*8).
+__global__ __launch_bounds__(256) void image_to_nhwc8_kernel(const float* __restrict__ img, bf16_t* __restrict__ out,
+                                                             int n, int hw) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)n * hw) return;
+  const long b = i / hw, p = i - b * hw;
+  const float* src = img + b * 3 * hw + p;
+  uint4 u;
+  u.x = (uint32_t)f2bf(src[0]) | ((uint32_t)f2bf(src[hw]) << 16);
+  u.y = (uint32_t)f2bf(src[2 * hw]);
+  u.z = 0; u.w = 0;
+  reinterpret_cast<uint4*>(out)[i] = u;
+}
+
+// torchvision MaxPool2d(3, 2, 1) on NHWC bf16; 8 channels per thread
+__global__ __launch_bounds__(256) void maxpool3s2_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int n,
+                                                         int h, int w, int c, int oh, int ow) {
+  const int c8 = c / 8;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)n * oh * ow * c8) return;
+  const int cc = (int)(i % c8);
+  long t = i / c8;
+  const int ox = (int)(t % ow); t /= ow;
+  const int oy = (int)(t % oh);
+  const int b = (int)(t / oh);
+  float m[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+  for (int dy = 0; dy < 3; ++dy) {
+    const int iy = oy * 2 - 1 + dy;
+    if (iy < 0 || iy >= h) continue;
+    for (int dx = 0; dx < 3; ++dx) {
+      const int ix = ox * 2 - 1 + dx;
+      if (ix < 0 || ix >= w) continue;
+      uint4 u = reinterpret_cast<const uint4*>(x + (((long)b * h + iy) * w + ix) * c)[cc];
+      const uint32_t wds[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        m[2 * j] = fmaxf(m[2 * j], bf2f((bf16_t)(wds[j] & 0xffff)));
+        m[2 * j + 1] = fmaxf(m[2 * j + 1], bf2f((bf16_t)(wds[j] >> 16)));
+      }
+    }
+  }
+  uint4 o;
+  o.x = (uint32_t)f2bf(m[0]) | ((uint32_t)f2bf(m[1]) << 16);
+  o.y = (uint32_t)f2bf(m[2]) | ((uint32_t)f2bf(m[3]) << 16);
+  o.z = (uint32_t)f2bf(m[4]) | ((uint32_t)f2bf(m[5]) << 16);
+  o.w = (uint32_t)f2bf(m[6]) | ((uint32_t)f2bf(m[7]) << 16);
+  reinterpret_cast<uint4*>(y)[i] = o;
+}
+
+// partial column sums of a [rows, cols] matrix: block = 256 columns x COLSUM_ROWS rows
+constexpr int COLSUM_ROWS = 64;
+template <bool BF16>
+__global__ __launch_bounds__(256) void colsum_part_kernel(const void* __restrict__ xv, int rows, int cols, long ld,
+                                                          float* __restrict__ ws) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + tx * 4;
+  const int r0 = blockIdx.y * COLSUM_ROWS;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    for (int r = r0 + ty; r < min(rows, r0 + COLSUM_ROWS); r += 4) {
+      if constexpr (BF16) {
+        uint2 u = *reinterpret_cast<const uint2*>((const bf16_t*)xv + (long)r * ld + c);
+        s[0] += bf2f(u.x & 0xffff); s[1] += bf2f(u.x >> 16); s[2] += bf2f(u.y & 0xffff); s[3] += bf2f(u.y >> 16);
+      } else {
+        float4 v = *reinterpret_cast<const float4*>((const float*)xv + (long)r * ld + c);
+        s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+      }
+    }
+  }
+  __shared__ float red[4][256];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[ty][tx * 4 + j] = s[j];
+  __syncthreads();
+  const int cc = blockIdx.x * 256 + threadIdx.x;
+  if (cc < cols)
+    ws[(long)blockIdx.y * cols + cc] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                       red[3][threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ ws, int parts, int cols,
+                                                           float* __restrict__ out, float beta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int p = 0; p < parts; ++p) s += ws[(long)p * cols + c];
+  out[c] = beta != 0.f ? beta * out[c] + s : s;
+}
+
+// h[t, :] = table[ids[t], :]  (T5Stack embed_tokens, modeling_t5.py:678)
+__global__ __launch_bounds__(256) void embedding_fwd_kernel(const long long* __restrict__ ids,
+                                                            const float* __restrict__ table, float* __restrict__ out,
+                                                            int tokens, int d4, int vocab) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)tokens * d4) return;
+  const int t = (int)(i / d4), j = (int)(i - (long)t * d4);
+  long long id = ids[t];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);     // clamp (reference raises; ids validated on host)
+  reinterpret_cast<float4*>(out)[i] = reinterpret_cast<const float4*>(table + id * (long)d4 * 4)[j];
+}
+
+// dtable[ids[t], :] += dh[t, :]   (dense embedding gradient, nn.Embedding sparse=False)
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(const long long* __restrict__ ids,
+                                                            const float* __restrict__ dh, float* __restrict__ dtable,
+                                                            int tokens, int d, int vocab) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)tokens * d) return;
+  const int t = (int)(i / d), j = (int)(i - (long)t * d);
+  long long id = ids[t];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  atomicAdd(dtable + id * (long)d + j, dh[i]);
+}
+
+// bias[h, i, j] = table[bucket[i*lk + j], h]   (compute_bias, modeling_t5.py:264-279)
+__global__ __launch_bounds__(256) void relbias_fwd_kernel(const float* __restrict__ table,
+                                                          const int* __restrict__ bucket, float* __restrict__ out,
+                                                          int heads, int lqk) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= heads * lqk) return;
+  const int h = i / lqk, p = i - h * lqk;
+  out[i] = table[bucket[p] * heads + h];
+}
+
+__global__ __launch_bounds__(256) void relbias_bwd_kernel(const float* __restrict__ dbias,
+                                                          const int* __restrict__ bucket, float* __restrict__ dtable,
+                                                          int heads, int lqk) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= heads * lqk) return;
+  const int h = i / lqk, p = i - h * lqk;
+  atomicAdd(dtable + bucket[p] * heads + h, dbias[i]);
+}
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                            long n) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    float4 v = *reinterpret_cast<const float4*>(x + i);
+    uint2 u;
+    u.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+    u.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+    *reinterpret_cast<uint2*>(y + i) = u;
+  } else {
+    for (long j = i; j < n; ++j) y[j] = f2bf(x[j]);
+  }
+}
+
+}  // namespace
+
+extern "C" int vqa_image_to_nhwc8(const float* img, void* out, int n, int h, int w, hipStream_t s) {
+  VQA_REQUIRE(img && out && n > 0 && h > 0 && w > 0, "vqa_image_to_nhwc8: bad arguments");
+  const long total = (long)n * h * w;
+  hipLaunchKernelGGL(image_to_nhwc8_kernel, dim3(vqa::cdiv(total, 256)), dim3(256), 0, s, img, (bf16_t*)out, n, h * w);
+  return vqa::check_launch("vqa_image_to_nhwc8");
+}
+
+extern "C" int vqa_maxpool3x3s2_nhwc(const void* x, void* y, int n, int h, int w, int c, int oh, int ow,
+                                     hipStream_t s) {
+  VQA_REQUIRE(x && y && c % 8 == 0, "vqa_maxpool3x3s2_nhwc: bad arguments");
+  const long total = (long)n * oh * ow * (c / 8);
+  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(vqa::cdiv(total, 256)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, n,
+                     h, w, c, oh, ow);
+  return vqa::check_launch("vqa_maxpool3x3s2_nhwc");
+}
+
+extern "C" int vqa_colsum_workspace_floats(int rows, int cols) { return vqa::cdiv(rows, COLSUM_ROWS) * cols; }
+
+extern "C" int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long long ld, float* out, float beta,
+                          float* ws, hipStream_t s) {
+  VQA_REQUIRE(x && out && ws && cols % 4 == 0 && ld % 4 == 0, "vqa_colsum: bad arguments");
+  const int parts = vqa::cdiv(rows, COLSUM_ROWS);
+  dim3 grid(vqa::cdiv(cols, 256), parts);
+  if (x_bf16)
+    hipLaunchKernelGGL(colsum_part_kernel<true>, grid, dim3(256), 0, s, x, rows, cols, (long)ld, ws);
+  else
+    hipLaunchKernelGGL(colsum_part_kernel<false>, grid, dim3(256), 0, s, x, rows, cols, (long)ld, ws);
+  if (int rc = vqa::check_launch("vqa_colsum")) return rc;
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(vqa::cdiv(cols, 256)), dim3(256), 0, s, ws, parts, cols, out, beta);
+  return vqa::check_launch("vqa_colsum/final");
+}
+
+extern "C" int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int tokens, int d, int vocab,
+                                 hipStream_t s) {
+  VQA_REQUIRE(ids && table && out && d % 4 == 0, "vqa_embedding_fwd: bad arguments");
+  const long total = (long)tokens * (d / 4);
+  hipLaunchKernelGGL(embedding_fwd_kernel, dim3(vqa::cdiv(total, 256)), dim3(256), 0, s, ids, table, out, tokens,
+                     d / 4, vocab);
+  return vqa::check_launch("vqa_embedding_fwd");
+}
+
+extern "C" int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab,
+                                 hipStream_t s) {
+  VQA_REQUIRE(ids && dh && dtable, "vqa_embedding_bwd: bad arguments");
+  const long total = (long)tokens * d;
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(vqa::cdiv(total, 256)), dim3(256), 0, s, ids, dh, dtable, tokens, d,
+                     vocab);
+  return vqa::check_launch("vqa_embedding_bwd");
+}
+
+extern "C" int vqa_t5_relbias_fwd(const float* table, const int* bucket, float* out, int heads, int lq, int lk,
+                                  hipStream_t s) {
+  VQA_REQUIRE(table && bucket && out, "vqa_t5_relbias_fwd: bad arguments");
+  hipLaunchKernelGGL(relbias_fwd_kernel, dim3(vqa::cdiv(heads * lq * lk, 256)), dim3(256), 0, s, table, bucket, out,
+                     heads, lq * lk);
+  return vqa::check_launch("vqa_t5_relbias_fwd");
+}
+
+extern "C" int vqa_t5_relbias_bwd(const float* dbias, const int* bucket, float* dtable, int heads, int lq, int lk,
+                                  hipStream_t s) {
+  VQA_REQUIRE(dbias && bucket && dtable, "vqa_t5_relbias_bwd: bad arguments");
+  hipLaunchKernelGGL(relbias_bwd_kernel, dim3(vqa::cdiv(heads * lq * lk, 256)), dim3(256), 0, s, dbias, bucket, dtable,
+                     heads, lq * lk);
+  return vqa::check_launch("vqa_t5_relbias_bwd");
+}
+
+extern "C" int vqa_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t s) {
+  VQA_REQUIRE(x && y && n >= 0, "vqa_cast_f32_bf16: bad arguments");
+  if (n == 0) return VQA_OK;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(vqa::cdiv(vqa::cdiv(n, 4), 256)), dim3(256), 0, s, x, (bf16_t*)y,
+                     (long)n);
+  return vqa::check_launch("vqa_cast_f32_bf16");
+}
+
+extern "C" int vqa_zero(void* p, long long bytes, hipStream_t s) {
+  VQA_REQUIRE(p && bytes >= 0, "vqa_zero: bad arguments");
+  hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, s);
+  if (e != hipSuccess) return vqa::fail((int)e, "vqa_zero: %s", hipGetErrorString(e));
+  return VQA_OK;
+}

@@ -1,0 +1,299 @@
+// Row normalisations over D = 768-wide rows (any D % 256 == 0 up to 1024), one
+// wave per row, fp32 math, fused residual-gradient and bf16 copies.
+//   T5LayerNorm (RMS, eps 1e-6)      TF/models/t5/modeling_t5.py:50-72
+//   nn.LayerNorm(768) (eps 1e-5)     multi_head_vision_text_attn.py:120-126
+// Backward kernels also emit per-block partial column sums (dgamma/dbeta) into
+// a workspace [gridDim.x][D] that vqa_colsum_partials() reduces
+// deterministically (no atomics).
+#include "common.h"
+
+namespace {
+
+constexpr int ROWS_PER_BLOCK = 4;       // 4 waves, one row each
+constexpr int MAXV = 4;                 // up to 4 float4 per lane -> D <= 1024
+
+template <int NV>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, float (&x)[NV][4]) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float4 v = reinterpret_cast<const float4*>(p)[i * 64 + l];
+    x[i][0] = v.x; x[i][1] = v.y; x[i][2] = v.z; x[i][3] = v.w;
+  }
+}
+template <int NV>
+__device__ __forceinline__ void store_row32(float* __restrict__ p, const float (&x)[NV][4]) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    reinterpret_cast<float4*>(p)[i * 64 + l] = make_float4(x[i][0], x[i][1], x[i][2], x[i][3]);
+}
+template <int NV>
+__device__ __forceinline__ void store_row16(bf16_t* __restrict__ p, const float (&x)[NV][4]) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    uint2 u;
+    u.x = (uint32_t)f2bf(x[i][0]) | ((uint32_t)f2bf(x[i][1]) << 16);
+    u.y = (uint32_t)f2bf(x[i][2]) | ((uint32_t)f2bf(x[i][3]) << 16);
+    reinterpret_cast<uint2*>(p)[i * 64 + l] = u;
+  }
+}
+template <int NV>
+__device__ __forceinline__ void load_vec(const float* __restrict__ p, float (&x)[NV][4]) { load_row<NV>(p, x); }
+
+// ------------------------------------------------------------------ RMSNorm
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          float* __restrict__ y32, bf16_t* __restrict__ y16,
+                                                          float* __restrict__ rstd, int rows, float eps) {
+  const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int D = NV * 256;
+  float v[NV][4], g[NV][4];
+  load_row<NV>(x + (long)row * D, v);
+  load_vec<NV>(w, g);
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ss += v[i][j] * v[i][j];
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / D + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[i][j] = g[i][j] * (v[i][j] * r);
+  if (y32) store_row32<NV>(y32 + (long)row * D, v);
+  if (y16) store_row16<NV>(y16 + (long)row * D, v);
+  if (rstd && (threadIdx.x & 63) == 0) rstd[row] = r;
+}
+
+// dx = r*g - (r^3/D) * x * sum(g*x),  g = w*dy ;  dw partial = sum_rows dy*x*r
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                          const float* __restrict__ rstd, const float* __restrict__ w,
+                                                          const float* __restrict__ dres, float* __restrict__ dx32,
+                                                          bf16_t* __restrict__ dx16, float* __restrict__ dw_ws,
+                                                          int rows, int rows_per_block) {
+  constexpr int D = NV * 256;
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  float g[NV][4];
+  load_vec<NV>(w, g);
+  float dwacc[NV][4] = {};
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  for (int row = r0 + wv; row < r1; row += ROWS_PER_BLOCK) {
+    float d[NV][4], v[NV][4];
+    load_row<NV>(dy + (long)row * D, d);
+    load_row<NV>(x + (long)row * D, v);
+    const float r = rstd[row];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s += g[i][j] * d[i][j] * v[i][j];
+        dwacc[i][j] += d[i][j] * v[i][j] * r;
+      }
+    s = wave_sum(s);
+    const float c = r * r * r * s / D;
+    float o[NV][4];
+    if (dres) load_row<NV>(dres + (long)row * D, o);
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float t = r * g[i][j] * d[i][j] - c * v[i][j];
+        o[i][j] = dres ? o[i][j] + t : t;
+      }
+    if (dx32) store_row32<NV>(dx32 + (long)row * D, o);
+    if (dx16) store_row16<NV>(dx16 + (long)row * D, o);
+  }
+  // reduce the 4 waves' dw partials through LDS, write one row per block
+  __shared__ float red[ROWS_PER_BLOCK][NV * 256];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[wv][(i * 64 + l) * 4 + j] = dwacc[i][j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float t = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    dw_ws[(long)blockIdx.x * D + c] = t;
+  }
+}
+
+// ------------------------------------------------------------------ LayerNorm
+template <int NV>
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gam,
+                                                            const float* __restrict__ bet, float* __restrict__ y32,
+                                                            bf16_t* __restrict__ y16, float* __restrict__ mean_out,
+                                                            float* __restrict__ rstd_out, int rows, float eps) {
+  const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int D = NV * 256;
+  float v[NV][4], g[NV][4], b[NV][4];
+  load_row<NV>(x + (long)row * D, v);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += v[i][j];
+  const float mu = wave_sum(s) / D;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { float t = v[i][j] - mu; ss += t * t; }
+  const float r = rsqrtf(wave_sum(ss) / D + eps);
+  load_vec<NV>(gam, g);
+  load_vec<NV>(bet, b);
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[i][j] = (v[i][j] - mu) * r * g[i][j] + b[i][j];
+  if (y32) store_row32<NV>(y32 + (long)row * D, v);
+  if (y16) store_row16<NV>(y16 + (long)row * D, v);
+  if ((threadIdx.x & 63) == 0) { mean_out[row] = mu; rstd_out[row] = r; }
+}
+
+// xh = (x-mu)*r ; g = gam*dy ; dx = r*(g - mean(g) - xh*mean(g*xh)) (+dres)
+// partials: dgamma = sum dy*xh -> ws[0..D), dbeta = sum dy -> ws[D..2D)
+template <int NV>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                            const float* __restrict__ gam, const float* __restrict__ dres,
+                                                            float* __restrict__ dx32, bf16_t* __restrict__ dx16,
+                                                            float* __restrict__ ws, int rows, int rows_per_block) {
+  constexpr int D = NV * 256;
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  float g[NV][4];
+  load_vec<NV>(gam, g);
+  float dga[NV][4] = {}, dba[NV][4] = {};
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  for (int row = r0 + wv; row < r1; row += ROWS_PER_BLOCK) {
+    float d[NV][4], v[NV][4];
+    load_row<NV>(dy + (long)row * D, d);
+    load_row<NV>(x + (long)row * D, v);
+    const float mu = mean[row], r = rstd[row];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[i][j] = (v[i][j] - mu) * r;                    // xhat
+        const float gd = g[i][j] * d[i][j];
+        s1 += gd;
+        s2 += gd * v[i][j];
+        dga[i][j] += d[i][j] * v[i][j];
+        dba[i][j] += d[i][j];
+      }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+    float o[NV][4];
+    if (dres) load_row<NV>(dres + (long)row * D, o);
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float t = r * (g[i][j] * d[i][j] - s1 - v[i][j] * s2);
+        o[i][j] = dres ? o[i][j] + t : t;
+      }
+    if (dx32) store_row32<NV>(dx32 + (long)row * D, o);
+    if (dx16) store_row16<NV>(dx16 + (long)row * D, o);
+  }
+  __shared__ float red[ROWS_PER_BLOCK][NV * 256];
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[wv][(i * 64 + l) * 4 + j] = pass == 0 ? dga[i][j] : dba[i][j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256)
+      ws[((long)blockIdx.x * 2 + pass) * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    __syncthreads();
+  }
+}
+
+// out[c] = beta*out[c] + sum_p ws[p*stride + c]  (fixed order -> deterministic)
+__global__ __launch_bounds__(256) void colsum_partials_kernel(const float* __restrict__ ws, int parts, long stride,
+                                                              int cols, float* __restrict__ out, float beta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int p = 0; p < parts; ++p) s += ws[(long)p * stride + c];
+  out[c] = beta != 0.f ? beta * out[c] + s : s;
+}
+
+constexpr int NORM_BWD_ROWS = 32;      // rows per block in the backward kernels
+
+}  // namespace
+
+#define DISPATCH_NV(D, ...)                                          \
+  switch ((D) / 256) {                                               \
+    case 1: { constexpr int NV = 1; __VA_ARGS__; break; }            \
+    case 2: { constexpr int NV = 2; __VA_ARGS__; break; }            \
+    case 3: { constexpr int NV = 3; __VA_ARGS__; break; }            \
+    case 4: { constexpr int NV = 4; __VA_ARGS__; break; }            \
+    default: return vqa::fail(VQA_ERR_INVALID, "norm: D=%d unsupported (D %% 256 == 0, <= 1024)", (D)); \
+  }
+
+extern "C" int vqa_rmsnorm_fwd(const float* x, const float* w, float* y32, void* y16, float* rstd, int rows, int d,
+                               float eps, hipStream_t s) {
+  VQA_REQUIRE(x && w && (y32 || y16) && rows > 0 && d % 256 == 0, "vqa_rmsnorm_fwd: bad arguments");
+  dim3 grid(vqa::cdiv(rows, ROWS_PER_BLOCK));
+  DISPATCH_NV(d, hipLaunchKernelGGL(rmsnorm_fwd_kernel<NV>, grid, dim3(256), 0, s, x, w, y32, (bf16_t*)y16, rstd,
+                                    rows, eps));
+  return vqa::check_launch("vqa_rmsnorm_fwd");
+}
+
+int vqa_norm_bwd_parts(int rows) { return vqa::cdiv(rows, NORM_BWD_ROWS); }
+extern "C" int vqa_norm_bwd_workspace_floats(int rows, int d) { return 2 * vqa_norm_bwd_parts(rows) * d; }
+
+extern "C" int vqa_rmsnorm_bwd(const float* dy, const float* x, const float* rstd, const float* w, const float* dres,
+                               float* dx32, void* dx16, float* dw, float dw_beta, float* ws, int rows, int d,
+                               hipStream_t s) {
+  VQA_REQUIRE(dy && x && rstd && w && dw && ws && (dx32 || dx16) && d % 256 == 0, "vqa_rmsnorm_bwd: bad arguments");
+  const int parts = vqa_norm_bwd_parts(rows);
+  DISPATCH_NV(d, hipLaunchKernelGGL(rmsnorm_bwd_kernel<NV>, dim3(parts), dim3(256), 0, s, dy, x, rstd, w, dres, dx32,
+                                    (bf16_t*)dx16, ws, rows, NORM_BWD_ROWS));
+  if (int rc = vqa::check_launch("vqa_rmsnorm_bwd")) return rc;
+  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 256)), dim3(256), 0, s, ws, parts, (long)d, d, dw,
+                     dw_beta);
+  return vqa::check_launch("vqa_rmsnorm_bwd/colsum");
+}
+
+extern "C" int vqa_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y32, void* y16,
+                                 float* mean, float* rstd, int rows, int d, float eps, hipStream_t s) {
+  VQA_REQUIRE(x && gamma && beta && mean && rstd && (y32 || y16) && d % 256 == 0, "vqa_layernorm_fwd: bad arguments");
+  dim3 grid(vqa::cdiv(rows, ROWS_PER_BLOCK));
+  DISPATCH_NV(d, hipLaunchKernelGGL(layernorm_fwd_kernel<NV>, grid, dim3(256), 0, s, x, gamma, beta, y32,
+                                    (bf16_t*)y16, mean, rstd, rows, eps));
+  return vqa::check_launch("vqa_layernorm_fwd");
+}
+
+extern "C" int vqa_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
+                                 const float* gamma, const float* dres, float* dx32, void* dx16, float* dgamma,
+                                 float* dbeta, float* ws, int rows, int d, hipStream_t s) {
+  VQA_REQUIRE(dy && x && mean && rstd && gamma && dgamma && dbeta && ws && (dx32 || dx16) && d % 256 == 0,
+              "vqa_layernorm_bwd: bad arguments");
+  const int parts = vqa_norm_bwd_parts(rows);
+  DISPATCH_NV(d, hipLaunchKernelGGL(layernorm_bwd_kernel<NV>, dim3(parts), dim3(256), 0, s, dy, x, mean, rstd, gamma,
+                                    dres, dx32, (bf16_t*)dx16, ws, rows, NORM_BWD_ROWS));
+  if (int rc = vqa::check_launch("vqa_layernorm_bwd")) return rc;
+  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 256)), dim3(256), 0, s, ws, parts, (long)2 * d, d,
+                     dgamma, 0.f);
+  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 256)), dim3(256), 0, s, ws + d, parts, (long)2 * d, d,
+                     dbeta, 0.f);
+  return vqa::check_launch("vqa_layernorm_bwd/colsum");
+}
+
+extern "C" int vqa_colsum_partials(const float* ws, int parts, long long stride, int cols, float* out, float beta,
+                                   hipStream_t s) {
+  VQA_REQUIRE(ws && out && parts > 0 && cols > 0, "vqa_colsum_partials: bad arguments");
+  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(cols, 256)), dim3(256), 0, s, ws, parts, (long)stride, cols,
+                     out, beta);
+  return vqa::check_launch("vqa_colsum_partials");
+}

@@ -1,0 +1,138 @@
+// Optimiser tail of train_one_step (faster_rcnn_vqa_trainer.py:399-404):
+//   clip_grad_norm_(params, 1.0)  ->  AdamW(wd=0.1, amsgrad=True) over the
+//   trainer's param groups (:231-267)  ->  get_linear_schedule_with_warmup
+//   (:279-287, TF/optimization.py:101-107).
+// Everything stays on the device so the whole step can be one hipGraph:
+//   1. vqa_grad_sqnorm    grid-stride partial sums of g^2 (fp64 accumulators)
+//   2. vqa_optim_finalize one thread: norm, clip coefficient, LR multiplier
+//                         lambda(step), bias corrections; advances `step`
+//   3. vqa_adamw_amsgrad  one fused HBM pass over p, g, m, v, vmax -> p, m, v,
+//                         vmax and the bf16 shadow copy used by the GEMMs.
+// The DP average (1/world) enters as grad_scale in steps 2 and 3.
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g, long n4, double* __restrict__ ws) {
+  double s = 0.0;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4*>(g)[i];
+    s += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void finalize_kernel(const double* __restrict__ ws, int parts, float grad_scale, float max_norm,
+                                int warmup, int total, float beta1, float beta2, float* __restrict__ st) {
+  if (threadIdx.x != 0) return;
+  double ss = 0.0;
+  for (int i = 0; i < parts; ++i) ss += ws[i];
+  const float norm = (float)(sqrt(ss) * (double)grad_scale);
+  float coef = 1.f;
+  if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
+  const double step = (double)st[VQA_ST_STEP];
+  double lam;
+  if (step < warmup) lam = step / (double)(warmup > 1 ? warmup : 1);
+  else lam = fmax(0.0, (double)(total - step) / (double)((total - warmup) > 1 ? (total - warmup) : 1));
+  const double t = step + 1.0;
+  st[VQA_ST_GRAD_NORM] = norm;
+  st[VQA_ST_CLIP_COEF] = coef;
+  st[VQA_ST_LR_SCALE] = (float)lam;
+  st[VQA_ST_BC1] = (float)(1.0 - pow((double)beta1, t));
+  st[VQA_ST_BC2_SQRT] = (float)sqrt(1.0 - pow((double)beta2, t));
+  st[VQA_ST_STEP] = (float)t;
+}
+
+struct AdamArgs {
+  float* p; const float* g; float* m; float* v; float* vm; bf16_t* p16;
+  long n4;
+  int ngroups; long gend4[VQA_MAX_GROUPS]; float glr[VQA_MAX_GROUPS];
+  float b1, b2, eps, wd, gscale;
+  const float* st;
+};
+
+__global__ __launch_bounds__(256) void adamw_kernel(AdamArgs A) {
+  const float coef = A.st[VQA_ST_CLIP_COEF], lam = A.st[VQA_ST_LR_SCALE];
+  const float bc1 = A.st[VQA_ST_BC1], bc2s = A.st[VQA_ST_BC2_SQRT];
+  const float gmul = A.gscale * coef;
+  const float omb1 = 1.f - A.b1, omb2 = 1.f - A.b2;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < A.n4; i += (long)gridDim.x * 256) {
+    int gi = 0;
+#pragma unroll
+    for (int k = 0; k < VQA_MAX_GROUPS - 1; ++k) gi += (k < A.ngroups - 1 && i >= A.gend4[k]) ? 1 : 0;
+    const float lr = A.glr[gi] * lam;
+    const float decay = 1.f - lr * A.wd, step_size = lr / bc1;
+    float4 p = reinterpret_cast<float4*>(A.p)[i];
+    const float4 g4 = reinterpret_cast<const float4*>(A.g)[i];
+    float4 m = reinterpret_cast<float4*>(A.m)[i];
+    float4 v = reinterpret_cast<float4*>(A.v)[i];
+    float4 vm = reinterpret_cast<float4*>(A.vm)[i];
+    float* pp = &p.x; const float* gg = &g4.x; float* mm = &m.x; float* vv = &v.x; float* ww = &vm.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gr = gg[j] * gmul;
+      pp[j] *= decay;                                   // decoupled weight decay
+      mm[j] = mm[j] + omb1 * (gr - mm[j]);              // exp_avg.lerp_(grad, 1-beta1)
+      vv[j] = vv[j] * A.b2 + omb2 * gr * gr;            // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+      ww[j] = fmaxf(ww[j], vv[j]);                      // amsgrad running max
+      const float denom = sqrtf(ww[j]) / bc2s + A.eps;
+      pp[j] = pp[j] - step_size * (mm[j] / denom);
+    }
+    reinterpret_cast<float4*>(A.p)[i] = p;
+    reinterpret_cast<float4*>(A.m)[i] = m;
+    reinterpret_cast<float4*>(A.v)[i] = v;
+    reinterpret_cast<float4*>(A.vm)[i] = vm;
+    if (A.p16) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(p.x) | ((uint32_t)f2bf(p.y) << 16);
+      u.y = (uint32_t)f2bf(p.z) | ((uint32_t)f2bf(p.w) << 16);
+      reinterpret_cast<uint2*>(A.p16)[i] = u;
+    }
+  }
+}
+
+int grid_for(long n4) {
+  long b = (n4 + 255) / 256;
+  return (int)(b < 4096 ? b : 4096);
+}
+
+}  // namespace
+
+extern "C" int vqa_grad_sqnorm(const float* g, long long n, double* ws, int parts, hipStream_t s) {
+  VQA_REQUIRE(g && ws && n % 4 == 0 && parts > 0, "vqa_grad_sqnorm: bad arguments (n %% 4 == 0)");
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(parts), dim3(256), 0, s, g, (long)(n / 4), ws);
+  return vqa::check_launch("vqa_grad_sqnorm");
+}
+
+extern "C" int vqa_optim_finalize(const double* ws, int parts, float grad_scale, float max_norm, int warmup, int total,
+                                  float beta1, float beta2, float* state, hipStream_t s) {
+  VQA_REQUIRE(ws && state && parts > 0, "vqa_optim_finalize: bad arguments");
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, ws, parts, grad_scale, max_norm, warmup, total, beta1,
+                     beta2, state);
+  return vqa::check_launch("vqa_optim_finalize");
+}
+
+extern "C" int vqa_adamw_amsgrad(const vqa_adamw_desc* d, hipStream_t s) {
+  VQA_REQUIRE(d && d->param && d->grad && d->exp_avg && d->exp_avg_sq && d->max_exp_avg_sq && d->state,
+              "vqa_adamw_amsgrad: null argument");
+  VQA_REQUIRE(d->n % 4 == 0 && d->ngroups >= 1 && d->ngroups <= VQA_MAX_GROUPS, "vqa_adamw_amsgrad: bad sizes");
+  AdamArgs A;
+  A.p = d->param; A.g = d->grad; A.m = d->exp_avg; A.v = d->exp_avg_sq; A.vm = d->max_exp_avg_sq;
+  A.p16 = (bf16_t*)d->param16;
+  A.n4 = d->n / 4;
+  A.ngroups = d->ngroups;
+  for (int i = 0; i < VQA_MAX_GROUPS; ++i) {
+    VQA_REQUIRE(i >= d->ngroups || d->group_end[i] % 4 == 0, "vqa_adamw_amsgrad: group ends must be multiples of 4");
+    A.gend4[i] = i < d->ngroups ? d->group_end[i] / 4 : A.n4;
+    A.glr[i] = i < d->ngroups ? d->group_lr[i] : 0.f;
+  }
+  A.b1 = d->beta1; A.b2 = d->beta2; A.eps = d->eps; A.wd = d->weight_decay; A.gscale = d->grad_scale;
+  A.st = d->state;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(A.n4)), dim3(256), 0, s, A);
+  return vqa::check_launch("vqa_adamw_amsgrad");
+}

@@ -1,0 +1,566 @@
+"""VQAEngine: the MI355X training step of `ResnetVQAModel` as an explicit,
+statically planned schedule of libvqa_hip kernel calls.
+
+Mirrors, op for op:
+  forward   ResnetVQAModel.forward            model/resnet_vqa_model.py:101-165
+            SGA.forward                        model/multi_head_vision_text_attn.py:145-158
+            T5Stack (encoder, eval)            TF/models/t5/modeling_t5.py:640-751
+  backward  loss.backward()                    trainer/faster_rcnn_vqa_trainer.py:397
+  step      clip_grad_norm_ + AdamW + sched    trainer/faster_rcnn_vqa_trainer.py:399-404
+
+Design (MI355X-first, not a translation of eager PyTorch):
+  * every trainable parameter, gradient and AdamW state lives in one flat fp32
+    arena (layout.ParamLayout) + a bf16 shadow for GEMM operands, so the clip
+    norm and AdamW are single HBM passes and DP all-reduces one contiguous
+    buffer;
+  * the frozen ResNet is BN-folded, bf16, NHWC, run as implicit-GEMM convs
+    (no im2col buffers); the ConvTranspose2d scaler is an implicit GEMM over
+    the layer4 map whose rows are already the [B, HW, 768] token order the
+    reference obtains with view+permute (:142-143);
+  * activations/workspaces are allocated once for a fixed (B, L, H), every
+    kernel call is prepared once with fixed device addresses, and the whole
+    step is replayed as one hipGraph (torch.cuda.CUDAGraph capture);
+  * dropout is off (eval-mode numerics); parity is defined there.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import lib as L
+from . import ops
+from . import synthetic as S
+from .layout import ParamLayout, fold_bn, t5_bucket_map
+
+BF16, F32, I64 = torch.bfloat16, torch.float32, torch.int64
+D = S.D_MODEL
+
+
+class VQAEngine:
+    def __init__(self, state_dict, vision="resnet50", batch=64, seq_len=32, image_size=224, device="cuda:0",
+                 warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1):
+        L.load()
+        self.dev = torch.device(device)
+        self.vision, self.B, self.L, self.H = vision, batch, seq_len, image_size
+        self.NB, self.A = num_blocks, answer_spaces
+        self.warmup, self.total, self.max_norm = warmup, total, max_norm
+        self.betas, self.eps, self.wd = betas, eps, weight_decay
+        self.grad_scale = grad_scale
+        self.T = batch * seq_len
+        self.lay = ParamLayout(vision, answer_spaces, num_blocks)
+        sd = {k: np.asarray(v) for k, v in state_dict.items()}
+        self._frozen = {k: v for k, v in sd.items() if k not in set(self.lay.trainable_keys)}
+        with torch.cuda.device(self.dev):
+            self._alloc_params(sd)
+            self._plan_resnet(sd)
+            self._alloc_activations()
+            self.fwd_calls, self.bwd_calls, self.opt_calls, self.zero_calls = [], [], [], []
+            self._plan_forward()
+            self._plan_backward()
+            self._plan_optimizer()
+        self.graph = None
+        self.allreduce = None            # set by the DP trainer: fn(G32 tensor) on the current stream
+
+    @classmethod
+    def from_state_dict(cls, sd, **kw):
+        return cls(sd, **kw)
+
+    # ------------------------------------------------------------------ allocation
+    def _t(self, shape, dtype=F32, zero=False):
+        f = torch.zeros if zero else torch.empty
+        return f(shape, dtype=dtype, device=self.dev)
+
+    def _alloc_params(self, sd):
+        lay = self.lay
+        flat = lay.pack(sd)
+        self.P32 = torch.from_numpy(flat).to(self.dev)
+        self.P16 = self.P32.to(BF16)
+        self.G32 = self._t(lay.total, zero=True)
+        self.M = self._t(lay.total, zero=True)
+        self.V = self._t(lay.total, zero=True)
+        self.VMAX = self._t(lay.total, zero=True)
+        self.p32, self.p16, self.g32 = {}, {}, {}
+        for s in lay.segments.values():
+            sl = slice(s.offset, s.offset + s.numel)
+            self.p32[s.name] = self.P32[sl].view(s.shape)
+            self.p16[s.name] = self.P16[sl].view(s.shape)
+            self.g32[s.name] = self.G32[sl].view(s.shape)
+        self.opt_state = self._t(8, zero=True)
+        self.bucket = torch.from_numpy(t5_bucket_map(self.L, self.L)).reshape(-1).to(self.dev)
+
+    def _plan_resnet(self, sd):
+        """Frozen torchvision ResNet (eval BN folded) as a list of implicit-GEMM convs."""
+        B, H = self.B, self.H
+        vm = "vision_model."
+        self.res_calls = []
+        self._res_keep = []
+        convs = []                                   # (name_conv, name_bn, stride, pad, relu, role)
+
+        def conv_w(cname, bname, cin_pad=None):
+            w = sd[vm + cname + ".weight"].astype(np.float32)
+            wf, bf = fold_bn(w, sd[vm + bname + ".weight"], sd[vm + bname + ".bias"],
+                             sd[vm + bname + ".running_mean"], sd[vm + bname + ".running_var"])
+            wf = wf.transpose(0, 2, 3, 1)            # [Cout, kh, kw, Cin]
+            if cin_pad and cin_pad > wf.shape[3]:
+                wf = np.concatenate([wf, np.zeros(wf.shape[:3] + (cin_pad - wf.shape[3],), np.float32)], 3)
+            w16 = torch.from_numpy(np.ascontiguousarray(wf)).to(self.dev).to(BF16)
+            b32 = torch.from_numpy(bf).to(self.dev)
+            self._res_keep += [w16, b32]
+            return w16, b32
+
+        # geometry walk to size the ping-pong buffers
+        layers = S.RESNET_LAYERS[self.vision]
+        bottleneck = self.vision == "resnet50"
+        h1 = (H + 2 * 3 - 7) // 2 + 1
+        h2 = (h1 + 2 - 3) // 2 + 1
+        plan = []                                     # (kind, args)
+        maxel = B * h1 * h1 * 64
+        hh, cin = h2, 64
+        for li, (planes, nblk) in enumerate(zip((64, 128, 256, 512), layers)):
+            for bi in range(nblk):
+                stride = (1 if li == 0 else 2) if bi == 0 else 1
+                out = planes * 4 if bottleneck else planes
+                ho = (hh + 2 - 3) // stride + 1
+                maxel = max(maxel, B * hh * hh * planes, B * ho * ho * out)
+                plan.append((li, bi, stride, hh, ho, cin, planes, out))
+                hh, cin = ho, out
+        self.fh, self.fc = hh, cin                    # layer4 spatial size / channels
+        self.V_TOK = B * hh * hh
+        self.IMG = self._t((B, 3, H, H))
+        self.IMG8 = self._t((B, H, H, 8), BF16)
+        bufs = [self._t(maxel, BF16) for _ in range(5)]
+        self.F4 = self._t((B, hh, hh, cin), BF16)
+
+        # stem: conv7x7/2 + BN + ReLU, then maxpool 3x3/2
+        w16, b32 = conv_w("conv1", "bn1", cin_pad=8)
+        self.res_calls.append(ops.Call("vqa_image_to_nhwc8", self.IMG.data_ptr(), self.IMG8.data_ptr(), B, H, H))
+        g = ops.conv_geom(B, H, H, 8, h1, h1, 7, 7, 2, 3)
+        self._gemm(self.res_calls, self.IMG8, w16, B * h1 * h1, 64, 7 * 7 * 8, lda=392, ldb=392, ga=g,
+                   c16=bufs[0], ldc16=64, bias=b32, relu=True)
+        self.res_calls.append(ops.Call("vqa_maxpool3x3s2_nhwc", bufs[0].data_ptr(), bufs[1].data_ptr(), B, h1, h1,
+                                       64, h2, h2))
+        x = bufs[1]
+        free = [bufs[0], bufs[2], bufs[3], bufs[4]]
+        nblocks_total = len(plan)
+        for idx, (li, bi, stride, hi, ho, ci, planes, out) in enumerate(plan):
+            p = f"layer{li + 1}.{bi}."
+            t1, t2, ds, y = free[0], free[1], free[2], free[3]
+            if idx == nblocks_total - 1:
+                y = self.F4
+            if bottleneck:
+                w, b = conv_w(p + "conv1", p + "bn1")
+                self._conv(x, (B, hi, hi, ci), w, b, 1, 0, t1, relu=True)
+                w, b = conv_w(p + "conv2", p + "bn2")
+                self._conv(t1, (B, hi, hi, planes), w, b, stride, 1, t2, relu=True)
+                last_in, last_c, last_h = t2, planes, ho
+                w3, b3 = conv_w(p + "conv3", p + "bn3")
+            else:
+                w, b = conv_w(p + "conv1", p + "bn1")
+                self._conv(x, (B, hi, hi, ci), w, b, stride, 1, t1, relu=True)
+                last_in, last_c, last_h = t1, planes, ho
+                w3, b3 = conv_w(p + "conv2", p + "bn2")
+            res = x
+            if (vm + p + "downsample.0.weight") in sd:
+                w, b = conv_w(p + "downsample.0", p + "downsample.1")
+                self._conv(x, (B, hi, hi, ci), w, b, stride, 0, ds, relu=False)
+                res = ds
+            k3 = 1 if bottleneck else 3
+            self._conv(last_in, (B, last_h, last_h, last_c), w3, b3, 1, 1 if k3 == 3 else 0, y, relu=True,
+                       res16=res)
+            if y is not self.F4:
+                free = [x, t1, t2, ds]
+                x = y
+
+    def _conv(self, x, shape, w16, b32, stride, pad, out, relu, res16=None):
+        n, h, w, c = shape
+        cout, kh, kw, _ = w16.shape
+        oh = (h + 2 * pad - kh) // stride + 1
+        g = ops.conv_geom(n, h, w, c, oh, oh, kh, kw, stride, pad)
+        self._gemm(self.res_calls, x, w16, n * oh * oh, cout, kh * kw * c, lda=kh * kw * c, ldb=kh * kw * c, ga=g,
+                   c16=out, ldc16=cout, bias=b32, relu=relu, res16=res16, ldres=cout)
+
+    def _alloc_activations(self):
+        B, Lq, T, NB, V = self.B, self.L, self.T, self.NB, self.V_TOK
+        t = self._t
+        # inputs
+        self.IDS = t((B, Lq), I64, zero=True)
+        self.MASK = t((B, Lq), I64, zero=True)
+        self.TGT = t((B,), I64, zero=True)
+        # vision tokens
+        self.VIS32, self.VIS16 = t((V, D)), t((V, D), BF16)
+        # T5
+        nl = S.T5_LAYERS
+        self.PB = t((S.T5_HEADS, Lq, Lq))
+        self.HS = [t((T, D)) for _ in range(nl + 1)]
+        self.N0 = [t((T, D), BF16) for _ in range(nl)]
+        self.QKV = [t((T, 3 * D), BF16) for _ in range(nl)]
+        self.PT = [t((B, S.T5_HEADS, Lq, Lq)) for _ in range(nl)]
+        self.O = [t((T, D), BF16) for _ in range(nl)]
+        self.HM = [t((T, D)) for _ in range(nl)]
+        self.N1 = [t((T, D), BF16) for _ in range(nl)]
+        self.FF = [t((T, S.T5_DFF), BF16) for _ in range(nl)]
+        self.R0 = [t(T) for _ in range(nl)]
+        self.R1 = [t(T) for _ in range(nl)]
+        self.RF = t(T)
+        self.TXT32, self.TXT16 = t((T, D)), t((T, D), BF16)
+        # SGA blocks
+        self.sga = []
+        for n in range(NB):
+            ly = V if n == 0 else T
+            lk = self.fh * self.fh if n == 0 else Lq
+            self.sga.append(dict(
+                ly=ly, lk=lk,
+                QKV1=t((T, 3 * D), BF16), P1=t((B, S.SGA_HEADS, Lq, Lq)), O1=t((T, D), BF16),
+                S1=t((T, D)), X1=t((T, D)), X1h=t((T, D), BF16), MU1=t(T), RS1=t(T),
+                Q2=t((T, D), BF16), KV2=t((ly, 2 * D), BF16), P2=t((B, S.SGA_HEADS, Lq, lk)), O2=t((T, D), BF16),
+                S2=t((T, D)), X2=t((T, D)), X2h=t((T, D), BF16), MU2=t(T), RS2=t(T),
+                FFh=t((T, D), BF16), S3=t((T, D)), OUT=t((T, D)), OUTh=t((T, D), BF16), MU3=t(T), RS3=t(T)))
+        # head
+        self.ATT, self.POOLED = t((B, Lq)), t((B, D))
+        self.LOGP, self.NLL, self.LOSS = t((B, self.A)), t(B), t(1)
+        # backward temporaries (reused layer to layer)
+        mx = max(T, V)
+        self.dY = [t((T, D)), t((T, D))]
+        self.dA32, self.dA16 = t((T, D)), t((T, D), BF16)
+        self.dB32, self.dB16 = t((T, D)), t((T, D), BF16)
+        self.dC32 = t((T, D))
+        self.dO16 = t((T, D), BF16)
+        self.dQKV16 = t((T, 3 * D), BF16)
+        self.dQ16 = t((T, D), BF16)
+        self.dKV16 = t((mx, 2 * D), BF16)
+        self.dF16 = t((T, S.T5_DFF), BF16)
+        self.dTXT = t((T, D))
+        self.dVIS32, self.dVIS16 = t((V, D)), t((V, D), BF16)
+        self.dH32, self.dH16 = t((T, D)), t((T, D), BF16)
+        self.dHM32, self.dHM16 = t((T, D)), t((T, D), BF16)
+        self.dPB = t((S.T5_HEADS, Lq, Lq), zero=True)
+        lib = L.load()
+        self.WS_NORM = t(lib.vqa_norm_bwd_workspace_floats(T, D))
+        self.WS_COL = t(lib.vqa_colsum_workspace_floats(mx, 3 * D))
+        self.WS_HEAD = t(lib.vqa_head_workspace_floats(B, Lq, D, self.A))
+        self.SQ_PARTS = 1024
+        self.WS_SQ = t(self.SQ_PARTS, torch.float64)
+
+    # ------------------------------------------------------------------ call helpers
+    def _gemm(self, lst, a, b, m, n, k, **kw):
+        lst.append(ops.gemm_call(ops.gemm_desc(a, b, m, n, k, **kw)))
+
+    def _call(self, lst, name, *args):
+        lst.append(ops.Call(name, *[ops.addr(a) if isinstance(a, torch.Tensor) else a for a in args]))
+
+    def _attn(self, lst, fn, **kw):
+        d = L.AttnDesc()
+        for k, v in kw.items():
+            setattr(d, k, ops.addr(v) if isinstance(v, torch.Tensor) else v)
+        lst.append(ops.Call(fn, ctypes.byref(d), keep=d))
+
+    def _linear(self, lst, x16, wname, m, out32=None, out16=None, bias=True, relu=False, res32=None):
+        w = self.p16[wname]
+        n, k = w.shape
+        self._gemm(lst, x16, w, m, n, k, lda=k, ldb=k, c32=out32, ldc32=n, c16=out16, ldc16=n,
+                   bias=self.p32[wname[:-1] + "b"] if bias else None, relu=relu, res32=res32, ldres=n)
+
+    def _dx(self, lst, dy16, wname, m, out32=None, out16=None, res32=None, mask16=None, beta=0.0):
+        """dX[m, k] = dY[m, n] W[n, k]  (+res) (*mask>0) (+beta*out32)"""
+        w = self.p16[wname]
+        n, k = w.shape
+        self._gemm(lst, dy16, w, m, k, n, lda=n, ldb=k, b_trans=True, c32=out32, ldc32=k, c16=out16, ldc16=k,
+                   res32=res32, ldres=k, mask16=mask16, ldmask=k, beta=beta)
+
+    def _dw(self, lst, dy16, x16, wname, rows, bias_from=None, bias_bf16=True):
+        """dW[n, k] = dY[rows, n]^T X[rows, k]; optional bias grad = colsum(dY)."""
+        g = self.g32[wname]
+        n, k = g.shape
+        self._gemm(lst, dy16, x16, n, k, rows, lda=n, ldb=k, a_trans=True, b_trans=True, c32=g, ldc32=k)
+        if bias_from is not None:
+            self._call(lst, "vqa_colsum", bias_from, int(bias_bf16), rows, n, n, self.g32[wname[:-1] + "b"], 0.0,
+                       self.WS_COL)
+
+    # ------------------------------------------------------------------ forward plan
+    def _plan_forward(self):
+        f = self.fwd_calls
+        B, Lq, T = self.B, self.L, self.T
+        f += self.res_calls
+        # ConvTranspose2d scaler as implicit GEMM over the layer4 map (+bias) -> vision tokens
+        cin, fh = self.fc, self.fh
+        g = ops.conv_geom(B, fh, fh, cin, fh, fh, 3, 3, 1, 1)
+        self._gemm(f, self.F4, self.p16["scaler_w"], self.V_TOK, D, 9 * cin, lda=9 * cin, ldb=9 * cin, ga=g,
+                   c32=self.VIS32, ldc32=D, c16=self.VIS16, ldc16=D, bias=self.p32["scaler_b"])
+        # T5 encoder
+        self._call(f, "vqa_embedding_fwd", self.IDS, self.p32["t5.embed"], self.HS[0], T, D, S.T5_VOCAB)
+        self._call(f, "vqa_t5_relbias_fwd", self.p32["t5.relbias"], self.bucket, self.PB, S.T5_HEADS, Lq, Lq)
+        for i in range(S.T5_LAYERS):
+            self._call(f, "vqa_rmsnorm_fwd", self.HS[i], self.p32[f"t5.{i}.ln0"], None, self.N0[i], self.R0[i], T, D,
+                       1e-6)
+            self._linear(f, self.N0[i], f"t5.{i}.qkv_w", T, out16=self.QKV[i], bias=False)
+            q = self.QKV[i]
+            self._attn(f, "vqa_attn_fwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
+                       ldv=3 * D, o=self.O[i], ldo=D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B,
+                       heads=S.T5_HEADS, lq=Lq, lk=Lq, dh=S.T5_DKV, scale=1.0)
+            self._linear(f, self.O[i], f"t5.{i}.o_w", T, out32=self.HM[i], bias=False, res32=self.HS[i])
+            self._call(f, "vqa_rmsnorm_fwd", self.HM[i], self.p32[f"t5.{i}.ln1"], None, self.N1[i], self.R1[i], T, D,
+                       1e-6)
+            self._linear(f, self.N1[i], f"t5.{i}.wi", T, out16=self.FF[i], bias=False, relu=True)
+            self._linear(f, self.FF[i], f"t5.{i}.wo", T, out32=self.HS[i + 1], bias=False, res32=self.HM[i])
+        self._call(f, "vqa_rmsnorm_fwd", self.HS[-1], self.p32["t5.final_ln"], self.TXT32, self.TXT16, self.RF, T, D,
+                   1e-6)
+        # SGA blocks: x = text always, y chained
+        y16 = self.VIS16
+        sc = 1.0 / math.sqrt(S.SGA_DHEAD)
+        for n in range(self.NB):
+            s, p = self.sga[n], f"sga{n}."
+            self._linear(f, self.TXT16, p + "qkv1_w", T, out16=s["QKV1"])
+            q = s["QKV1"]
+            self._attn(f, "vqa_attn_fwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
+                       ldv=3 * D, o=s["O1"], ldo=D, p=s["P1"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=Lq,
+                       dh=S.SGA_DHEAD, scale=sc)
+            self._linear(f, s["O1"], p + "m1_w", T, out32=s["S1"], res32=self.TXT32)
+            self._call(f, "vqa_layernorm_fwd", s["S1"], self.p32[p + "ln1_g"], self.p32[p + "ln1_b"], s["X1"],
+                       s["X1h"], s["MU1"], s["RS1"], T, D, 1e-5)
+            self._linear(f, s["X1h"], p + "q2_w", T, out16=s["Q2"])
+            self._linear(f, y16, p + "kv2_w", s["ly"], out16=s["KV2"])
+            kv = s["KV2"]
+            self._attn(f, "vqa_attn_fwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
+                       o=s["O2"], ldo=D, p=s["P2"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=s["lk"], dh=S.SGA_DHEAD,
+                       scale=sc)
+            self._linear(f, s["O2"], p + "m2_w", T, out32=s["S2"], res32=s["X1"])
+            self._call(f, "vqa_layernorm_fwd", s["S2"], self.p32[p + "ln2_g"], self.p32[p + "ln2_b"], s["X2"],
+                       s["X2h"], s["MU2"], s["RS2"], T, D, 1e-5)
+            self._linear(f, s["X2h"], p + "fc1_w", T, out16=s["FFh"], relu=True)
+            self._linear(f, s["FFh"], p + "fc2_w", T, out32=s["S3"], res32=s["X2"])
+            self._call(f, "vqa_layernorm_fwd", s["S3"], self.p32[p + "ln3_g"], self.p32[p + "ln3_b"], s["OUT"],
+                       s["OUTh"], s["MU3"], s["RS3"], T, D, 1e-5)
+            y16 = s["OUTh"]
+        last = self.sga[-1]["OUT"]
+        self._call(f, "vqa_head_fwd", last, self.p32["pool_w"], self.p32["pool_b"], self.p32["cls_w"],
+                   self.p32["cls_b"], self.TGT, self.ATT, self.POOLED, self.LOGP, self.NLL, self.LOSS, B, Lq, D, self.A)
+
+    # ------------------------------------------------------------------ backward plan
+    def _plan_backward(self):
+        b = self.bwd_calls
+        B, Lq, T, NB = self.B, self.L, self.T, self.NB
+        # gradients that accumulate: embedding rows, relative bias
+        for z in (self.g32["t5.embed"], self.g32["t5.relbias"], self.dPB):
+            self._call(self.zero_calls, "vqa_zero", z, z.numel() * 4)
+        b += self.zero_calls
+        # head: log_softmax + NLL + classifier + attention pooler
+        last = self.sga[-1]["OUT"]
+        self._call(b, "vqa_head_bwd", last, self.ATT, self.POOLED, self.LOGP, self.TGT, self.p32["pool_w"],
+                   self.p32["cls_w"], self.dY[(NB - 1) & 1], None, self.g32["pool_w"], self.g32["pool_b"],
+                   self.g32["cls_w"], self.g32["cls_b"], self.WS_HEAD, B, Lq, D, self.A)
+        sc = 1.0 / math.sqrt(S.SGA_DHEAD)
+        for n in reversed(range(NB)):
+            s, p = self.sga[n], f"sga{n}."
+            dy = self.dY[n & 1]
+            y16 = self.VIS16 if n == 0 else self.sga[n - 1]["OUTh"]
+            # norm3 + FFN
+            self._call(b, "vqa_layernorm_bwd", dy, s["S3"], s["MU3"], s["RS3"], self.p32[p + "ln3_g"], None,
+                       self.dA32, self.dA16, self.g32[p + "ln3_g"], self.g32[p + "ln3_b"], self.WS_NORM, T, D)
+            self._dw(b, self.dA16, s["FFh"], p + "fc2_w", T, bias_from=self.dA32, bias_bf16=False)
+            self._dx(b, self.dA16, p + "fc2_w", T, out16=self.dB16, mask16=s["FFh"])
+            self._dw(b, self.dB16, s["X2h"], p + "fc1_w", T, bias_from=self.dB16)
+            self._dx(b, self.dB16, p + "fc1_w", T, out32=self.dC32, res32=self.dA32)
+            # norm2 + cross attention (q from x, k/v from y)
+            self._call(b, "vqa_layernorm_bwd", self.dC32, s["S2"], s["MU2"], s["RS2"], self.p32[p + "ln2_g"], None,
+                       self.dA32, self.dA16, self.g32[p + "ln2_g"], self.g32[p + "ln2_b"], self.WS_NORM, T, D)
+            self._dw(b, self.dA16, s["O2"], p + "m2_w", T, bias_from=self.dA32, bias_bf16=False)
+            self._dx(b, self.dA16, p + "m2_w", T, out16=self.dO16)
+            kv = s["KV2"]
+            self._attn(b, "vqa_attn_bwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
+                       p=s["P2"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=s["lk"], dh=S.SGA_DHEAD, scale=sc,
+                       dout=self.dO16, lddo=D, dq=self.dQ16, lddq=D, dk=self.dKV16, lddk=2 * D,
+                       dv=ops.addr(self.dKV16, D), lddv=2 * D)
+            self._dw(b, self.dQ16, s["X1h"], p + "q2_w", T, bias_from=self.dQ16)
+            self._dx(b, self.dQ16, p + "q2_w", T, out32=self.dC32, res32=self.dA32)
+            self._dw(b, self.dKV16, y16, p + "kv2_w", s["ly"], bias_from=self.dKV16)
+            if n == 0:
+                self._dx(b, self.dKV16, p + "kv2_w", s["ly"], out32=self.dVIS32, out16=self.dVIS16)
+            else:
+                self._dx(b, self.dKV16, p + "kv2_w", s["ly"], out32=self.dY[(n - 1) & 1])
+            # norm1 + self attention
+            self._call(b, "vqa_layernorm_bwd", self.dC32, s["S1"], s["MU1"], s["RS1"], self.p32[p + "ln1_g"], None,
+                       self.dA32, self.dA16, self.g32[p + "ln1_g"], self.g32[p + "ln1_b"], self.WS_NORM, T, D)
+            self._dw(b, self.dA16, s["O1"], p + "m1_w", T, bias_from=self.dA32, bias_bf16=False)
+            self._dx(b, self.dA16, p + "m1_w", T, out16=self.dO16)
+            q = s["QKV1"]
+            dq = self.dQKV16
+            self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
+                       ldv=3 * D, p=s["P1"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=Lq, dh=S.SGA_DHEAD, scale=sc,
+                       dout=self.dO16, lddo=D, dq=dq, lddq=3 * D, dk=ops.addr(dq, D), lddk=3 * D,
+                       dv=ops.addr(dq, 2 * D), lddv=3 * D)
+            self._dw(b, dq, self.TXT16, p + "qkv1_w", T, bias_from=dq)
+            # text gradient accumulates over the three blocks (x is the T5 output for every block)
+            self._dx(b, dq, p + "qkv1_w", T, out32=self.dTXT, res32=self.dA32, beta=0.0 if n == NB - 1 else 1.0)
+        # ConvTranspose2d scaler weight/bias gradient: implicit im2col of layer4 as the B operand
+        cin, fh = self.fc, self.fh
+        g = ops.conv_geom(B, fh, fh, cin, fh, fh, 3, 3, 1, 1)
+        self._gemm(b, self.dVIS16, self.F4, D, 9 * cin, self.V_TOK, lda=D, ldb=9 * cin, a_trans=True, b_trans=True,
+                   c32=self.g32["scaler_w"], ldc32=9 * cin, gb=g)
+        self._call(b, "vqa_colsum", self.dVIS32, 0, self.V_TOK, D, D, self.g32["scaler_b"], 0.0, self.WS_COL)
+        # T5 encoder backward
+        self._call(b, "vqa_rmsnorm_bwd", self.dTXT, self.HS[-1], self.RF, self.p32["t5.final_ln"], None, self.dH32,
+                   self.dH16, self.g32["t5.final_ln"], 0.0, self.WS_NORM, T, D)
+        for i in reversed(range(S.T5_LAYERS)):
+            self._dw(b, self.dH16, self.FF[i], f"t5.{i}.wo", T)
+            self._dx(b, self.dH16, f"t5.{i}.wo", T, out16=self.dF16, mask16=self.FF[i])
+            self._dw(b, self.dF16, self.N1[i], f"t5.{i}.wi", T)
+            self._dx(b, self.dF16, f"t5.{i}.wi", T, out32=self.dC32)
+            self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HM[i], self.R1[i], self.p32[f"t5.{i}.ln1"], self.dH32,
+                       self.dHM32, self.dHM16, self.g32[f"t5.{i}.ln1"], 0.0, self.WS_NORM, T, D)
+            self._dw(b, self.dHM16, self.O[i], f"t5.{i}.o_w", T)
+            self._dx(b, self.dHM16, f"t5.{i}.o_w", T, out16=self.dO16)
+            q = self.QKV[i]
+            dq = self.dQKV16
+            self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
+                       ldv=3 * D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B, heads=S.T5_HEADS, lq=Lq,
+                       lk=Lq, dh=S.T5_DKV, scale=1.0, dout=self.dO16, lddo=D, dq=dq, lddq=3 * D,
+                       dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dPB)
+            self._dw(b, dq, self.N0[i], f"t5.{i}.qkv_w", T)
+            self._dx(b, dq, f"t5.{i}.qkv_w", T, out32=self.dC32)
+            self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HS[i], self.R0[i], self.p32[f"t5.{i}.ln0"], self.dHM32,
+                       self.dH32, self.dH16, self.g32[f"t5.{i}.ln0"], 0.0, self.WS_NORM, T, D)
+        self._call(b, "vqa_embedding_bwd", self.IDS, self.dH32, self.g32["t5.embed"], T, D, S.T5_VOCAB)
+        self._call(b, "vqa_t5_relbias_bwd", self.dPB, self.bucket, self.g32["t5.relbias"], S.T5_HEADS, Lq, Lq)
+
+    # ------------------------------------------------------------------ optimizer plan
+    def _plan_optimizer(self):
+        o = self.opt_calls
+        n = self.lay.total
+        self._call(o, "vqa_grad_sqnorm", self.G32, n, self.WS_SQ, self.SQ_PARTS)
+        self._call(o, "vqa_optim_finalize", self.WS_SQ, self.SQ_PARTS, float(self.grad_scale), float(self.max_norm),
+                   int(self.warmup), int(self.total), float(self.betas[0]), float(self.betas[1]), self.opt_state)
+        d = L.AdamWDesc()
+        d.param, d.grad = self.P32.data_ptr(), self.G32.data_ptr()
+        d.exp_avg, d.exp_avg_sq, d.max_exp_avg_sq = self.M.data_ptr(), self.V.data_ptr(), self.VMAX.data_ptr()
+        d.param16 = self.P16.data_ptr()
+        d.n = n
+        ends, lrs = self.lay.group_of_element()
+        d.ngroups = len(ends)
+        for i, (e, lr) in enumerate(zip(ends, lrs)):
+            d.group_end[i], d.group_lr[i] = e, lr
+        d.beta1, d.beta2, d.eps, d.weight_decay = self.betas[0], self.betas[1], self.eps, self.wd
+        d.grad_scale = self.grad_scale
+        d.state = self.opt_state.data_ptr()
+        self._adam_desc = d
+        o.append(ops.Call("vqa_adamw_amsgrad", ctypes.byref(d), keep=d))
+
+    def set_grad_scale(self, s):
+        """DP: grads are summed over ranks; the average enters as a scale."""
+        self.grad_scale = float(s)
+        self.opt_calls = []
+        self._plan_optimizer()
+        self.graph = None
+
+    # ------------------------------------------------------------------ execution
+    def _run(self, calls):
+        s = L.stream_handle()
+        for c in calls:
+            c(s)
+
+    def load_batch(self, batch):
+        """Copy a batch dict (numpy or torch, host or device) into the static input buffers."""
+        def cp(dst, src):
+            if src is None:
+                return
+            src = torch.as_tensor(src)
+            dst.copy_(src.to(dst.dtype).reshape(dst.shape), non_blocking=True)
+        cp(self.IMG, batch["image_tensors"])
+        cp(self.IDS, batch["question_input_ids"])
+        cp(self.MASK, batch["question_attention_masks"])
+        cp(self.TGT, batch.get("annotation_ids"))
+
+    def forward(self):
+        self._run(self.fwd_calls)
+
+    def backward(self):
+        self._run(self.bwd_calls)
+
+    def optimizer_step(self):
+        self._run(self.opt_calls)
+
+    def train_step(self):
+        """zero_grad -> forward -> backward -> (all-reduce) -> clip -> AdamW -> sched, all on-device."""
+        if self.graph is not None:
+            for g in self.graph:
+                if callable(g):
+                    g()
+                else:
+                    g.replay()
+            return
+        self.forward()
+        self.backward()
+        if self.allreduce is not None:
+            self.allreduce(self.G32)
+        self.optimizer_step()
+
+    def capture(self, warm=True):
+        """Capture the step as hipGraph(s): one graph when single-GPU; with a DP
+        all-reduce hook, graph(fwd+bwd) -> eager collective -> graph(optimizer)."""
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        saved = self.opt_state.clone()
+        with torch.cuda.stream(s):
+            if warm:                                    # warm-up launch outside capture
+                self.forward()
+                self.backward()
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        torch.cuda.synchronize(self.dev)
+        parts = []
+        if self.allreduce is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self.forward()
+                self.backward()
+                self.optimizer_step()
+            parts = [g]
+        else:
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1, stream=s):
+                self.forward()
+                self.backward()
+            with torch.cuda.graph(g2, stream=s):
+                self.optimizer_step()
+            ar = self.allreduce
+            parts = [g1, lambda: ar(self.G32), g2]
+        self.opt_state.copy_(saved)
+        self.graph = parts
+
+    # ------------------------------------------------------------------ readouts (tests / API)
+    def forward_backward(self, batch):
+        self.load_batch(batch)
+        self.forward()
+        self.backward()
+        torch.cuda.synchronize(self.dev)
+        return self.LOGP.cpu().numpy(), float(self.LOSS.item())
+
+    def log_probs(self):
+        return self.LOGP
+
+    def loss(self):
+        return self.LOSS
+
+    def grad_norm(self):
+        return float(self.G32.double().norm()) * self.grad_scale
+
+    def group_grad_norms(self):
+        out = {}
+        for g, (a, e) in self.lay.groups.items():
+            out[g] = float(self.G32[a:e].double().norm()) * self.grad_scale
+        return out
+
+    def last_grad_norm(self):
+        return float(self.opt_state[L.ST_GRAD_NORM].item())
+
+    def state_dict(self):
+        """Reference-layout state_dict (SURVEY Appendix B keys), fp32 numpy."""
+        sd = dict(self._frozen)
+        sd.update(self.lay.unpack(self.P32.cpu().numpy()))
+        specs = S.model_specs(self.vision, self.A, self.NB)
+        return {k: sd[k] for k in specs}
+
+    def segment_grad(self, name):
+        return self.g32[name]

@@ -1,0 +1,151 @@
+"""ctypes binding of libvqa_hip.so (include/vqa_hip.h).
+
+The HIP library is the product path: there is no CPU or PyTorch fallback.  If
+the shared object is missing, or does not export every symbol the header
+declares, `load()` raises.  torch is imported first so that the library binds
+to the HIP runtime torch already loaded (same SONAME libamdhip64.so.7), which
+lets us pass torch's stream handles and device pointers straight through.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (must be loaded before the HIP library)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libvqa_hip.so")
+HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "vqa_hip.h")
+
+c_void_p, c_int, c_float, c_ll = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_longlong
+
+
+class ConvGeom(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("n", "h", "w", "c", "oh", "ow", "kh", "kw", "stride", "pad")]
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("a", c_void_p), ("lda", c_ll), ("a_trans", c_int),
+        ("b", c_void_p), ("ldb", c_ll), ("b_trans", c_int),
+        ("m", c_int), ("n", c_int), ("k", c_int),
+        ("c32", c_void_p), ("ldc32", c_ll),
+        ("c16", c_void_p), ("ldc16", c_ll),
+        ("bias", c_void_p),
+        ("res32", c_void_p), ("res16", c_void_p), ("ldres", c_ll),
+        ("mask16", c_void_p), ("ldmask", c_ll),
+        ("alpha", c_float), ("beta", c_float), ("relu", c_int),
+        ("a_conv", c_int), ("ga", ConvGeom),
+        ("b_conv", c_int), ("gb", ConvGeom),
+        ("batch", c_int), ("stride_a", c_ll), ("stride_b", c_ll), ("stride_c32", c_ll),
+        ("stride_c16", c_ll), ("stride_res", c_ll),
+    ]
+
+
+class AttnDesc(ctypes.Structure):
+    _fields_ = [
+        ("q", c_void_p), ("ldq", c_ll), ("k", c_void_p), ("ldk", c_ll), ("v", c_void_p), ("ldv", c_ll),
+        ("o", c_void_p), ("ldo", c_ll), ("p", c_void_p), ("bias", c_void_p), ("key_mask", c_void_p),
+        ("batch", c_int), ("heads", c_int), ("lq", c_int), ("lk", c_int), ("dh", c_int), ("scale", c_float),
+        ("dout", c_void_p), ("lddo", c_ll), ("dq", c_void_p), ("lddq", c_ll), ("dk", c_void_p), ("lddk", c_ll),
+        ("dv", c_void_p), ("lddv", c_ll), ("dbias", c_void_p),
+    ]
+
+
+MAX_GROUPS = 8
+ST_STEP, ST_GRAD_NORM, ST_CLIP_COEF, ST_LR_SCALE, ST_BC1, ST_BC2_SQRT = range(6)
+
+
+class AdamWDesc(ctypes.Structure):
+    _fields_ = [
+        ("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+        ("max_exp_avg_sq", c_void_p), ("param16", c_void_p), ("n", c_ll), ("ngroups", c_int),
+        ("group_end", c_ll * MAX_GROUPS), ("group_lr", c_float * MAX_GROUPS),
+        ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("weight_decay", c_float),
+        ("grad_scale", c_float), ("state", c_void_p),
+    ]
+
+
+_lib = None
+
+
+def header_symbols():
+    """Every `int vqa_*(` / `const char* vqa_*(` export declared in include/vqa_hip.h."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(vqa_\w+)\s*\(", txt, re.M)))
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libvqa_hip.so not built at {LIB_PATH}: run `python __graft_entry__.py` "
+                           "(make -C t5-resnet-vqa_amd/csrc)")
+    lib = ctypes.CDLL(LIB_PATH)
+    missing = [s for s in header_symbols() if not hasattr(lib, s)]
+    if missing:
+        raise RuntimeError(f"libvqa_hip.so lacks exported symbols {missing}")
+    lib.vqa_last_error.restype = ctypes.c_char_p
+    lib.vqa_gemm.argtypes = [ctypes.POINTER(GemmDesc), c_void_p]
+    lib.vqa_attn_fwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
+    lib.vqa_attn_bwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
+    lib.vqa_adamw_amsgrad.argtypes = [ctypes.POINTER(AdamWDesc), c_void_p]
+    for name in ("vqa_norm_bwd_workspace_floats", "vqa_colsum_workspace_floats"):
+        getattr(lib, name).argtypes = [c_int, c_int]
+    lib.vqa_head_workspace_floats.argtypes = [c_int] * 4
+    for name, argtypes in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = c_int
+    _lib = lib
+    return lib
+
+
+_SIGS: dict = {}          # filled by register() below for the plain-argument kernels
+
+
+def register(name, *argtypes):
+    _SIGS[name] = list(argtypes) + [c_void_p]      # every export ends with the stream
+
+
+P = c_void_p
+register("vqa_rmsnorm_fwd", P, P, P, P, P, c_int, c_int, c_float)
+register("vqa_rmsnorm_bwd", P, P, P, P, P, P, P, P, c_float, P, c_int, c_int)
+register("vqa_layernorm_fwd", P, P, P, P, P, P, P, c_int, c_int, c_float)
+register("vqa_layernorm_bwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int)
+register("vqa_colsum_partials", P, c_int, c_ll, c_int, P, c_float)
+register("vqa_image_to_nhwc8", P, P, c_int, c_int, c_int)
+register("vqa_maxpool3x3s2_nhwc", P, P, c_int, c_int, c_int, c_int, c_int, c_int)
+register("vqa_colsum", P, c_int, c_int, c_int, c_ll, P, c_float, P)
+register("vqa_embedding_fwd", P, P, P, c_int, c_int, c_int)
+register("vqa_embedding_bwd", P, P, P, c_int, c_int, c_int)
+register("vqa_t5_relbias_fwd", P, P, P, c_int, c_int, c_int)
+register("vqa_t5_relbias_bwd", P, P, P, c_int, c_int, c_int)
+register("vqa_cast_f32_bf16", P, P, c_ll)
+register("vqa_zero", P, c_ll)
+register("vqa_head_fwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
+register("vqa_head_bwd", P, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
+register("vqa_grad_sqnorm", P, c_ll, P, c_int)
+register("vqa_optim_finalize", P, c_int, c_float, c_float, c_int, c_int, c_float, c_float, P)
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {_lib.vqa_last_error().decode()}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def call(name, *args, stream=None):
+    lib = load()
+    rc = getattr(lib, name)(*args, stream_handle(stream))
+    check(rc, name)

@@ -1,0 +1,98 @@
+"""Thin Python constructors for the C-ABI calls.
+
+Descriptors are built once (the engine's buffers have fixed addresses) and the
+prepared call is replayed every step, so the per-step host cost is one ctypes
+call per kernel (and zero under hipGraph replay).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import lib as L
+
+
+def addr(x, offset_elems=0):
+    """Device address of a tensor (+ element offset), a raw int address, or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr() + offset_elems * x.element_size()
+
+
+def conv_geom(n, h, w, c, oh, ow, kh, kw, stride, pad):
+    return L.ConvGeom(n, h, w, c, oh, ow, kh, kw, stride, pad)
+
+
+def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None, ldc32=0, c16=None, ldc16=0,
+              bias=None, res32=None, res16=None, ldres=0, mask16=None, ldmask=0, alpha=1.0, beta=0.0,
+              relu=False, ga=None, gb=None, batch=1, stride_a=0, stride_b=0, stride_c32=0, stride_c16=0,
+              stride_res=0):
+    for t in (a, b, c16, res16, mask16):
+        assert not isinstance(t, torch.Tensor) or t.dtype == torch.bfloat16, "bf16 operand expected"
+    for t in (c32, bias, res32):
+        assert not isinstance(t, torch.Tensor) or t.dtype == torch.float32, "fp32 tensor expected"
+    d = L.GemmDesc()
+    d.a, d.lda, d.a_trans = addr(a), lda, int(a_trans)
+    d.b, d.ldb, d.b_trans = addr(b), ldb, int(b_trans)
+    d.m, d.n, d.k = m, n, k
+    d.c32, d.ldc32 = addr(c32), ldc32
+    d.c16, d.ldc16 = addr(c16), ldc16
+    d.bias = addr(bias)
+    d.res32 = addr(res32)
+    d.res16 = addr(res16)
+    d.ldres = ldres
+    d.mask16 = addr(mask16)
+    d.ldmask = ldmask
+    d.alpha, d.beta, d.relu = alpha, beta, int(relu)
+    d.a_conv = int(ga is not None)
+    if ga is not None:
+        d.ga = ga
+    d.b_conv = int(gb is not None)
+    if gb is not None:
+        d.gb = gb
+    d.batch, d.stride_a, d.stride_b = batch, stride_a, stride_b
+    d.stride_c32, d.stride_c16, d.stride_res = stride_c32, stride_c16, stride_res
+    return d
+
+
+class Call:
+    """A prepared library call: fixed argument list, replayed on a stream."""
+    __slots__ = ("fn", "args", "name", "keep")
+
+    def __init__(self, name, *args, keep=None):
+        lib = L.load()
+        self.name = name
+        self.fn = getattr(lib, name)
+        self.args = args
+        self.keep = keep            # keeps ctypes structures alive
+
+    def __call__(self, stream_ptr):
+        rc = self.fn(*self.args, stream_ptr)
+        if rc != 0:
+            L.check(rc, self.name)
+
+
+def gemm_call(desc):
+    return Call("vqa_gemm", ctypes.byref(desc), keep=desc)
+
+
+def run(call_or_desc, stream=None):
+    s = L.stream_handle(stream)
+    if isinstance(call_or_desc, L.GemmDesc):
+        call_or_desc = gemm_call(call_or_desc)
+    call_or_desc(s)
+
+
+# ------------------------------------------------------------------ conveniences (tests, API mirror)
+def linear(x16, w16, bias=None, relu=False, out32=None, out16=None):
+    """y = x @ w^T (+bias) ; x [M,K] bf16, w [N,K] bf16."""
+    M, K = x16.shape
+    N = w16.shape[0]
+    if out32 is None and out16 is None:
+        out32 = torch.empty(M, N, device=x16.device, dtype=torch.float32)
+    d = gemm_desc(x16, w16, M, N, K, lda=K, ldb=K, c32=out32, ldc32=N, c16=out16, ldc16=N, bias=bias, relu=relu)
+    run(d)
+    return out32 if out32 is not None else out16

@@ -1,0 +1,128 @@
+"""GEMM / implicit-GEMM conv kernel vs a plain PyTorch fp32 reference of the same op.
+
+Operands are bf16 (exactly representable in fp32), so the only difference to
+the fp32 reference is accumulation order: tolerance 1e-5 relative to the
+row-wise |a|.|b| scale for fp32 outputs, one bf16 ulp for bf16 outputs."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops(pkg):
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    torch.backends.cuda.matmul.allow_tf32 = False
+    return pkg.ops
+
+
+def bf(shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return (torch.randn(shape, device="cuda", generator=g) * scale).to(torch.bfloat16)
+
+
+def close(got, ref, scale, rtol=2e-5):
+    err = (got.float() - ref).abs().max().item()
+    assert err <= rtol * scale + 1e-6, f"max err {err} vs scale {scale}"
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 2304, 768), (100, 200, 136), (64, 170, 768), (3136, 768, 1024),
+                                   (37, 24, 8)])
+def test_linear_forward_epilogue(ops, M, N, K):
+    x, w = bf((M, K), seed=1), bf((N, K), 0.05, seed=2)
+    bias = torch.randn(N, device="cuda")
+    res = torch.randn(M, N, device="cuda")
+    out32 = torch.empty(M, N, device="cuda")
+    out16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    d = ops.gemm_desc(x, w, M, N, K, lda=K, ldb=K, c32=out32, ldc32=N, c16=out16, ldc16=N, bias=bias,
+                      res32=res, ldres=N, relu=True)
+    ops.run(d)
+    torch.cuda.synchronize()
+    ref = torch.relu(x.float() @ w.float().T + bias + res)
+    scale = (x.float().abs() @ w.float().abs().T).max().item()
+    close(out32, ref, scale)
+    assert (out16.float() - ref).abs().max().item() <= ref.abs().max().item() * 2 ** -8 + 1e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 768, 2304), (96, 136, 200), (2048, 768, 3072)])
+def test_input_grad_layout(ops, M, N, K):
+    # dX[M, N] = dY[M, K] @ W[K, N]  (W stored [K, N] row-major: B n-contig)
+    dy, w = bf((M, K), seed=3), bf((K, N), 0.05, seed=4)
+    out = torch.empty(M, N, device="cuda")
+    ops.run(ops.gemm_desc(dy, w, M, N, K, lda=K, ldb=N, b_trans=True, c32=out, ldc32=N))
+    torch.cuda.synchronize()
+    close(out, dy.float() @ w.float(), (dy.float().abs() @ w.float().abs()).max().item())
+
+
+@pytest.mark.parametrize("NO,KI,T", [(768, 768, 2048), (2304, 768, 3136), (136, 64, 200), (8, 16, 40)])
+def test_weight_grad_layout(ops, NO, KI, T):
+    # dW[NO, KI] = dY[T, NO]^T @ X[T, KI]   (A m-contig, B n-contig)
+    dy, x = bf((T, NO), seed=5), bf((T, KI), seed=6)
+    out = torch.empty(NO, KI, device="cuda")
+    ops.run(ops.gemm_desc(dy, x, NO, KI, T, lda=NO, ldb=KI, a_trans=True, b_trans=True, c32=out, ldc32=KI))
+    torch.cuda.synchronize()
+    close(out, dy.float().T @ x.float(), (dy.float().abs().T @ x.float().abs()).max().item())
+
+
+def test_a_mcontig_b_kcontig(ops):
+    M, N, K = 192, 256, 320
+    a, b = bf((K, M), seed=7), bf((N, K), seed=8)
+    out = torch.empty(M, N, device="cuda")
+    ops.run(ops.gemm_desc(a, b, M, N, K, lda=M, ldb=K, a_trans=True, c32=out, ldc32=N))
+    torch.cuda.synchronize()
+    close(out, a.float().T @ b.float().T, (a.float().abs().T @ b.float().abs().T).max().item())
+
+
+def test_beta_mask_bf16_residual_batched(ops):
+    Bt, M, N, K = 3, 64, 96, 128
+    a, b = bf((Bt, M, K), seed=9), bf((Bt, N, K), seed=10)
+    mask = bf((Bt, M, N), seed=11)
+    res = bf((Bt, M, N), seed=12)
+    c = torch.randn(Bt, M, N, device="cuda")
+    c0 = c.clone()
+    ops.run(ops.gemm_desc(a, b, M, N, K, lda=K, ldb=K, c32=c, ldc32=N, res16=res, ldres=N, mask16=mask, ldmask=N,
+                          alpha=0.5, beta=1.0, batch=Bt, stride_a=M * K, stride_b=N * K, stride_c32=M * N,
+                          stride_res=M * N))
+    torch.cuda.synchronize()
+    v = 0.5 * torch.bmm(a.float(), b.float().transpose(1, 2)) + res.float()
+    v = torch.where(mask.float() > 0, v, torch.zeros_like(v))
+    close(c, v + c0, (a.float().abs() @ b.float().abs().transpose(1, 2)).max().item() + 10)
+
+
+@pytest.mark.parametrize("n,h,w,c,co,k,s,p", [
+    (2, 56, 56, 64, 64, 1, 1, 0), (2, 56, 56, 64, 128, 3, 1, 1), (2, 56, 56, 128, 128, 3, 2, 1),
+    (2, 28, 28, 256, 512, 1, 2, 0), (2, 32, 32, 8, 64, 7, 2, 3), (3, 7, 7, 2048, 768, 3, 1, 1)])
+def test_conv_forward_gather(ops, pkg, n, h, w, c, co, k, s, p):
+    x = bf((n, h, w, c), seed=13).abs()
+    wt = bf((co, k, k, c), 0.05, seed=14)                 # [Cout][KH][KW][C]
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    M, K = n * oh * ow, k * k * c
+    bias = torch.randn(co, device="cuda")
+    out = torch.empty(M, co, device="cuda")
+    g = ops.conv_geom(n, h, w, c, oh, ow, k, k, s, p)
+    ops.run(ops.gemm_desc(x, wt, M, co, K, lda=K, ldb=K, c32=out, ldc32=co, bias=bias, relu=True, ga=g))
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), wt.float().permute(0, 3, 1, 2), bias, stride=s, padding=p)
+    ref = torch.relu(ref).permute(0, 2, 3, 1).reshape(M, co)
+    scale = F.conv2d(x.float().abs().permute(0, 3, 1, 2), wt.float().abs().permute(0, 3, 1, 2), stride=s,
+                     padding=p).max().item()
+    close(out, ref, scale)
+
+
+@pytest.mark.parametrize("n,h,c,co", [(2, 7, 64, 96), (4, 7, 2048, 768)])
+def test_conv_weight_grad_gather(ops, n, h, c, co):
+    # ConvTranspose2d(k3,s1,p1) dW as the weight-grad of the equivalent conv: B = implicit im2col
+    x = bf((n, h, h, c), seed=15)
+    dy = bf((n * h * h, co), seed=16)
+    K9 = 9 * c
+    out = torch.empty(co, K9, device="cuda")
+    g = ops.conv_geom(n, h, h, c, h, h, 3, 3, 1, 1)
+    ops.run(ops.gemm_desc(dy, x, co, K9, n * h * h, lda=co, ldb=K9, a_trans=True, b_trans=True, c32=out,
+                          ldc32=K9, gb=g))
+    torch.cuda.synchronize()
+    cols = F.unfold(x.float().permute(0, 3, 1, 2), 3, padding=1)        # [n, c*9, h*h] (c major)
+    cols = cols.view(n, c, 9, h * h).permute(0, 3, 2, 1).reshape(n * h * h, K9)   # [(n,h,w), (tap, c)]
+    ref = dy.float().T @ cols
+    close(out, ref, (dy.float().abs().T @ cols.abs()).max().item())

@@ -1,0 +1,251 @@
+"""Per-kernel numerics vs a plain PyTorch fp32 reference of the same op (GPU)."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def k(pkg):
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    pkg.lib.load()
+    return pkg
+
+
+def run(pkg, name, *args):
+    pkg.ops.Call(name, *[pkg.ops.addr(a) if isinstance(a, torch.Tensor) else a for a in args])(
+        pkg.lib.stream_handle())
+
+
+def rnd(shape, seed, scale=1.0, dtype=torch.float32):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return (torch.randn(shape, device="cuda", generator=g) * scale).to(dtype)
+
+
+@pytest.mark.parametrize("rows", [2048, 37])
+def test_rmsnorm_fwd_bwd(k, rows):
+    D = 768
+    x, w = rnd((rows, D), 1), 1 + 0.1 * rnd(D, 2)
+    dy, dres = rnd((rows, D), 3), rnd((rows, D), 4)
+    y32, y16, rstd = torch.empty_like(x), torch.empty(rows, D, device="cuda", dtype=torch.bfloat16), \
+        torch.empty(rows, device="cuda")
+    run(k, "vqa_rmsnorm_fwd", x, w, y32, y16, rstd, rows, D, 1e-6)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    ref = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6))
+    ref.backward(dy)
+    torch.testing.assert_close(y32, ref.detach(), rtol=1e-5, atol=1e-5)
+    dx32, dx16, dw = torch.empty_like(x), torch.empty_like(y16), torch.empty(D, device="cuda")
+    ws = torch.empty(k.lib.load().vqa_norm_bwd_workspace_floats(rows, D), device="cuda")
+    run(k, "vqa_rmsnorm_bwd", dy, x, rstd, w, dres, dx32, dx16, dw, 0.0, ws, rows, D)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dx32, xr.grad + dres, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dw, wr.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("rows", [2048, 50])
+def test_layernorm_fwd_bwd(k, rows):
+    D = 768
+    x, g, b = rnd((rows, D), 5, 3.0) + 0.5, 1 + 0.1 * rnd(D, 6), 0.1 * rnd(D, 7)
+    dy = rnd((rows, D), 8)
+    y32, y16 = torch.empty_like(x), torch.empty(rows, D, device="cuda", dtype=torch.bfloat16)
+    mu, rs = torch.empty(rows, device="cuda"), torch.empty(rows, device="cuda")
+    run(k, "vqa_layernorm_fwd", x, g, b, y32, y16, mu, rs, rows, D, 1e-5)
+    xr, gr, br = (t.clone().requires_grad_(True) for t in (x, g, b))
+    ref = F.layer_norm(xr, (D,), gr, br, 1e-5)
+    ref.backward(dy)
+    torch.testing.assert_close(y32, ref.detach(), rtol=1e-5, atol=1e-5)
+    dx, dg, db = torch.empty_like(x), torch.empty(D, device="cuda"), torch.empty(D, device="cuda")
+    ws = torch.empty(k.lib.load().vqa_norm_bwd_workspace_floats(rows, D), device="cuda")
+    run(k, "vqa_layernorm_bwd", dy, x, mu, rs, g, None, dx, None, dg, db, ws, rows, D)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dx, xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dg, gr.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-3)
+
+
+def attn_ref(q, kk, v, scale, bias, mask):
+    s = q @ kk.transpose(-1, -2) * scale
+    if bias is not None:
+        s = s + bias
+    if mask is not None:
+        s = s + (1.0 - mask[:, None, None, :].float()) * torch.finfo(torch.float32).min
+    return torch.softmax(s, -1) @ v
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,dh,t5", [(4, 8, 32, 49, 96, False), (4, 8, 32, 32, 96, False),
+                                              (3, 12, 32, 32, 64, True), (2, 8, 16, 64, 96, False),
+                                              (2, 12, 16, 16, 64, True)])
+def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5):
+    D = H * dh
+    q16 = rnd((B * Lq, 3 * D), 10, dtype=torch.bfloat16)                   # fused qkv-like layout
+    kv16 = rnd((B * Lk, 2 * D), 11, dtype=torch.bfloat16)
+    do16 = rnd((B * Lq, D), 12, dtype=torch.bfloat16)
+    bias = rnd((H, Lq, Lk), 13) if t5 else None
+    mask = None
+    if t5:
+        lens = torch.tensor([Lk - 3 * i for i in range(B)], device="cuda")
+        mask = (torch.arange(Lk, device="cuda")[None, :] < lens[:, None]).long()
+    scale = 1.0 if t5 else 1.0 / math.sqrt(dh)
+    L = k.lib
+    o = torch.empty(B * Lq, D, device="cuda", dtype=torch.bfloat16)
+    p = torch.empty(B, H, Lq, Lk, device="cuda")
+    d = L.AttnDesc()
+    A = k.ops.addr
+    d.q, d.ldq, d.k, d.ldk, d.v, d.ldv = A(q16), 3 * D, A(kv16), 2 * D, A(kv16, D), 2 * D
+    d.o, d.ldo, d.p = A(o), D, A(p)
+    d.bias, d.key_mask = A(bias), A(mask)
+    d.batch, d.heads, d.lq, d.lk, d.dh, d.scale = B, H, Lq, Lk, dh, scale
+    L.check(L.load().vqa_attn_fwd(ctypes.byref(d), L.stream_handle()), "fwd")
+    qf = q16[:, :D].float().view(B, Lq, H, dh).transpose(1, 2).requires_grad_(True)
+    kf = kv16[:, :D].float().view(B, Lk, H, dh).transpose(1, 2).requires_grad_(True)
+    vf = kv16[:, D:].float().view(B, Lk, H, dh).transpose(1, 2).requires_grad_(True)
+    bf = bias.clone().requires_grad_(True) if t5 else None
+    ref = attn_ref(qf, kf, vf, scale, bf, mask)
+    ref_o = ref.transpose(1, 2).reshape(B * Lq, D)
+    torch.testing.assert_close(o.float(), ref_o.detach(), rtol=1e-2, atol=1e-2)
+    ref_o.backward(do16.float())
+    dq = torch.empty(B * Lq, D, device="cuda", dtype=torch.bfloat16)
+    dkv = torch.empty(B * Lk, 2 * D, device="cuda", dtype=torch.bfloat16)
+    dbias = torch.zeros(H, Lq, Lk, device="cuda") if t5 else None
+    d.dout, d.lddo, d.dq, d.lddq = A(do16), D, A(dq), D
+    d.dk, d.lddk, d.dv, d.lddv, d.dbias = A(dkv), 2 * D, A(dkv, D), 2 * D, A(dbias)
+    L.check(L.load().vqa_attn_bwd(ctypes.byref(d), L.stream_handle()), "bwd")
+    torch.cuda.synchronize()
+
+    def chk(got, ref_t):
+        ref_t = ref_t.transpose(1, 2).reshape(got.shape)
+        err = (got.float() - ref_t).abs().max().item()
+        assert err <= 1e-2 * ref_t.abs().max().item() + 1e-3, err
+    chk(dq, qf.grad)
+    chk(dkv[:, :D], kf.grad)
+    chk(dkv[:, D:], vf.grad)
+    if t5:
+        torch.testing.assert_close(dbias, bf.grad, rtol=1e-3, atol=1e-3)
+
+
+def test_head_fwd_bwd(k):
+    B, L, D, A = 8, 32, 768, 170
+    x = rnd((B, L, D), 20)
+    wp, bp = 0.03 * rnd(D, 21), 0.1 * rnd(1, 22)
+    wc, bc = 0.03 * rnd((A, D), 23), 0.1 * rnd(A, 24)
+    tgt = torch.randint(0, A, (B,), device="cuda")
+    att, pooled, logp = torch.empty(B, L, device="cuda"), torch.empty(B, D, device="cuda"), \
+        torch.empty(B, A, device="cuda")
+    nll, loss = torch.empty(B, device="cuda"), torch.empty(1, device="cuda")
+    run(k, "vqa_head_fwd", x, wp, bp, wc, bc, tgt, att, pooled, logp, nll, loss, B, L, D, A)
+    xr, wpr, bpr, wcr, bcr = (t.clone().requires_grad_(True) for t in (x, wp, bp, wc, bc))
+    a = torch.softmax(xr @ wpr[:, None] + bpr, dim=1)
+    pr = torch.bmm(a.transpose(1, 2), xr).squeeze(1)
+    lp = F.log_softmax(pr @ wcr.T + bcr, -1)
+    ls = F.nll_loss(lp, tgt)
+    ls.backward()
+    torch.testing.assert_close(logp, lp.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(loss[0], ls.detach(), rtol=1e-5, atol=1e-6)
+    dx = torch.empty_like(x)
+    dwp, dbp, dwc, dbc = torch.empty_like(wp), torch.empty(1, device="cuda"), torch.empty_like(wc), \
+        torch.empty_like(bc)
+    ws = torch.empty(k.lib.load().vqa_head_workspace_floats(B, L, D, A), device="cuda")
+    run(k, "vqa_head_bwd", x, att, pooled, logp, tgt, wp, wc, dx, None, dwp, dbp, dwc, dbc, ws, B, L, D, A)
+    torch.cuda.synchronize()
+    for got, ref in ((dx, xr.grad), (dwp, wpr.grad), (dbp, bpr.grad), (dwc, wcr.grad), (dbc, bcr.grad)):
+        torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-6)
+
+
+def test_embedding_relbias_colsum_cast(k):
+    T, D, Vv = 300, 768, 1000
+    ids = torch.randint(0, Vv, (T,), device="cuda")
+    ids[:50] = 7                                               # heavy duplicates
+    table = rnd((Vv, D), 30)
+    out = torch.empty(T, D, device="cuda")
+    run(k, "vqa_embedding_fwd", ids, table, out, T, D, Vv)
+    torch.testing.assert_close(out, table[ids])
+    dh = rnd((T, D), 31)
+    dt = torch.zeros(Vv, D, device="cuda")
+    run(k, "vqa_embedding_bwd", ids, dh, dt, T, D, Vv)
+    ref = torch.zeros(Vv, D, device="cuda").index_add_(0, ids, dh)
+    torch.testing.assert_close(dt, ref, rtol=1e-5, atol=1e-5)
+    Lq = 32
+    bucket = torch.from_numpy(k.layout.t5_bucket_map(Lq, Lq)).reshape(-1).cuda()
+    tab = rnd((32, 12), 32)
+    pb = torch.empty(12, Lq, Lq, device="cuda")
+    run(k, "vqa_t5_relbias_fwd", tab, bucket, pb, 12, Lq, Lq)
+    torch.testing.assert_close(pb, tab[bucket.long()].T.reshape(12, Lq, Lq))
+    dpb = rnd((12, Lq, Lq), 33)
+    dtab = torch.zeros(32, 12, device="cuda")
+    run(k, "vqa_t5_relbias_bwd", dpb, bucket, dtab, 12, Lq, Lq)
+    ref = torch.zeros(32, 12, device="cuda").index_add_(0, bucket.long(), dpb.reshape(12, -1).T)
+    torch.testing.assert_close(dtab, ref, rtol=1e-5, atol=1e-5)
+    for bf in (0, 1):
+        x = rnd((3136, 2304), 34, dtype=torch.bfloat16 if bf else torch.float32)
+        o = torch.full((2304,), 2.0, device="cuda")
+        ws = torch.empty(k.lib.load().vqa_colsum_workspace_floats(3136, 2304), device="cuda")
+        run(k, "vqa_colsum", x, bf, 3136, 2304, 2304, o, 1.0, ws)
+        torch.testing.assert_close(o, x.float().sum(0) + 2.0, rtol=1e-4, atol=1e-3)
+    x = rnd(1003, 35)
+    y = torch.empty(1003, device="cuda", dtype=torch.bfloat16)
+    run(k, "vqa_cast_f32_bf16", x, y, 1003)
+    assert torch.equal(y, x.to(torch.bfloat16))
+
+
+def test_image_and_maxpool(k):
+    img = torch.rand(2, 3, 20, 20, device="cuda")
+    out = torch.empty(2, 20, 20, 8, device="cuda", dtype=torch.bfloat16)
+    run(k, "vqa_image_to_nhwc8", img, out, 2, 20, 20)
+    ref = torch.zeros(2, 20, 20, 8, device="cuda")
+    ref[..., :3] = img.permute(0, 2, 3, 1)
+    assert torch.equal(out, ref.to(torch.bfloat16))
+    x = rnd((2, 21, 21, 64), 36, dtype=torch.bfloat16)
+    y = torch.empty(2, 11, 11, 64, device="cuda", dtype=torch.bfloat16)
+    run(k, "vqa_maxpool3x3s2_nhwc", x, y, 2, 21, 21, 64, 11, 11)
+    ref = F.max_pool2d(x.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.equal(y.float(), ref)
+
+
+def test_adamw_amsgrad_matches_torch(k):
+    n = 4096 + 64
+    torch.manual_seed(0)
+    p0 = torch.randn(n, device="cuda")
+    grads = [torch.randn(n, device="cuda") * 3 for _ in range(4)]
+    ends, lrs = [1024, 2048, n], [1e-3, 5e-4, 5e-3]
+    ref_params = [p0[0:1024].clone(), p0[1024:2048].clone(), p0[2048:].clone()]
+    for t in ref_params:
+        t.requires_grad_(True)
+    opt = torch.optim.AdamW([{"params": [t], "lr": lr} for t, lr in zip(ref_params, lrs)], weight_decay=0.1,
+                            amsgrad=True, foreach=False)
+    sched = torch.optim.lr_scheduler.LambdaLR(
+        opt, lambda s: s / 2 if s < 2 else max(0.0, (10 - s) / 8))
+    p, m, v, vm = p0.clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda"), \
+        torch.zeros(n, device="cuda")
+    p16 = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    st = torch.zeros(8, device="cuda")
+    ws = torch.empty(64, device="cuda", dtype=torch.float64)
+    L = k.lib
+    d = L.AdamWDesc()
+    A = k.ops.addr
+    d.param, d.grad, d.exp_avg, d.exp_avg_sq, d.max_exp_avg_sq, d.param16 = A(p), 0, A(m), A(v), A(vm), A(p16)
+    d.n, d.ngroups = n, 3
+    for i in range(3):
+        d.group_end[i], d.group_lr[i] = ends[i], lrs[i]
+    d.beta1, d.beta2, d.eps, d.weight_decay, d.grad_scale, d.state = 0.9, 0.999, 1e-8, 0.1, 1.0, A(st)
+    for g in grads:
+        gg = g.clone()
+        d.grad = A(gg)
+        run(k, "vqa_grad_sqnorm", gg, n, ws, 64)
+        run(k, "vqa_optim_finalize", ws, 64, 1.0, 1.0, 2, 10, 0.9, 0.999, st)
+        L.check(L.load().vqa_adamw_amsgrad(ctypes.byref(d), L.stream_handle()), "adamw")
+        for t, a, b in zip(ref_params, [0, 1024, 2048], ends):
+            t.grad = g[a:b].clone()
+        norm = torch.nn.utils.clip_grad_norm_(ref_params, 1.0)
+        opt.step()
+        sched.step()
+        torch.cuda.synchronize()
+        assert abs(st[1].item() - norm.item()) <= 1e-5 * norm.item()
+        torch.testing.assert_close(p, torch.cat([t.detach() for t in ref_params]), rtol=1e-6, atol=1e-7)
+    assert torch.equal(p16, p.to(torch.bfloat16))

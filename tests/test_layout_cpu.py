@@ -1,0 +1,61 @@
+"""Host-side logic: flat arena layout <-> reference state_dict, bucket map,
+BN folding.  CPU only."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+
+@pytest.mark.parametrize("vision,count", [("resnet50", 141_648_171), ("resnet34", 141_648_171 - 14_156_544 + 3_539_712)])
+def test_trainable_count_and_roundtrip(pkg, vision, count):
+    lay = pkg.layout.ParamLayout(vision)
+    assert lay.num_params == count
+    keys = set(lay.trainable_keys)
+    sd = pkg.synthetic.make_state_dict(vision, seed=3, keys=keys)
+    flat = lay.pack(sd)
+    back = lay.unpack(flat)
+    assert set(back) == keys
+    for k in keys:
+        np.testing.assert_array_equal(back[k], sd[k])
+    ends, lrs = lay.group_of_element()
+    assert ends == sorted(ends) and ends[-1] == lay.total and lrs == [1e-5, 5e-4, 5e-4, 5e-4, 5e-3]
+    for s in lay.segments.values():
+        assert s.offset % 64 == 0
+
+
+def test_convT_repack_is_equivalent_conv(pkg):
+    lay = pkg.layout
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 16, 5, 5, generator=g)
+    w = torch.randn(16, 8, 3, 3, generator=g)
+    ref = F.conv_transpose2d(x, w, stride=1, padding=1)
+    wc = torch.as_tensor(lay._convT_to_conv(w.numpy()))              # [Cout, kh, kw, Cin]
+    got = F.conv2d(x, wc.permute(0, 3, 1, 2), padding=1)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(lay._conv_to_convT(wc.numpy()), w.numpy())
+
+
+def test_bucket_map_matches_reference(pkg, golden):
+    g = golden("t5_encoder")
+    rel, buckets = g["rel"], g["buckets"]
+    L = 41
+    bm = pkg.layout.t5_bucket_map(L, 2 * L - 1)           # rel = j - i covers -40..80
+    got = {int(j - 40): int(bm[40, j]) for j in range(0, 81)}   # row i=40 -> rel = j - 40
+    for r, b in zip(rel, buckets):
+        assert got[int(r)] == int(b), (r, got[int(r)], b)
+    from oracle import vqa_oracle as orc
+    for L in (16, 32, 49, 64):
+        ref = orc.t5_relative_position_bucket(torch.arange(L)[None, :] - torch.arange(L)[:, None]).numpy()
+        np.testing.assert_array_equal(pkg.layout.t5_bucket_map(L, L), ref)
+
+
+def test_bn_fold(pkg):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 4, 6, 6, generator=g)
+    w = torch.randn(5, 4, 3, 3, generator=g)
+    bw, bb, rm, rv = torch.rand(5, generator=g) + .5, torch.randn(5, generator=g), torch.randn(5, generator=g), \
+        torch.rand(5, generator=g) + .5
+    ref = F.batch_norm(F.conv2d(x, w, padding=1), rm, rv, bw, bb, training=False, eps=1e-5)
+    wf, bf = pkg.layout.fold_bn(w.numpy(), bw.numpy(), bb.numpy(), rm.numpy(), rv.numpy())
+    got = F.conv2d(x, torch.as_tensor(wf), torch.as_tensor(bf), padding=1)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
