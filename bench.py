@@ -1,0 +1,166 @@
+"""Benchmark: question-image pairs/s of the ResNet50 + T5-base + 3xSGA training
+step (fwd + bwd + [RCCL all-reduce] + clip + AdamW(amsgrad) + schedule) on
+MI355X, bf16 MFMA / fp32 masters, B=64 per GPU, 224x224 images, 32-token
+questions (BASELINE.json configs[1]; configs[2] when launched on 8 GPUs).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N ... bench.py --gpus N     (one process per GPU)
+
+Synthetic data (no datasets offline): a pool of 4 batches per rank is made
+resident in HBM before timing; each timed step copies one into the static input
+buffers (device to device) and replays the captured step graph.
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+from __graft_entry__ import load_package  # noqa: E402
+
+FLOP_PER_PAIR = 30.95e9        # fwd+bwd algorithmic FLOPs, R50 @224, L=32
+MFMA_PEAK_TFLOPS = 2517.0      # bf16 dense: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def cpu_baseline(pkg, batch=8, steps=3, warm=1):
+    """The CPU oracle (fp32 restatement of the reference step) on this host's cores."""
+    from oracle import vqa_oracle as orc
+    threads = torch.get_num_threads()
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    tr = orc.OracleTrainer(sd, "resnet50", warmup=10, total=1000)
+    nb = orc.to_torch_batch(pkg.synthetic.make_batch(batch, 32, 224, seed=1))
+    times = []
+    for i in range(warm + steps):
+        t0 = time.perf_counter()
+        tr.train_one_step(nb)
+        if i >= warm:
+            times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": round(batch / t, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"oracle fp32 train step (zero_grad+fwd+bwd+clip+AdamW amsgrad), R50+T5-base+3xSGA, "
+                      f"B={batch}, 224x224, L=32, median of {steps} steps after {warm} warm-up, "
+                      f"torch CPU {threads} threads"}
+
+
+def time_kernel(call, reps, stream):
+    """Average duration of one prepared launch, HIP events on the launch stream."""
+    from vqa_amd import lib as L  # noqa
+    h = L.stream_handle(stream)
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        call(h)
+    start.record(stream)
+    for _ in range(reps):
+        call(h)
+    end.record(stream)
+    end.synchronize()
+    return start.elapsed_time(end) / reps * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--seq-len", type=int, default=32)
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    pkg = load_package()
+    B, L, H = args.batch, args.seq_len, args.image_size
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)       # identical init on every rank
+    eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev,
+                               warmup=10, total=100000)
+    del sd
+    if world > 1:
+        eng.allreduce = lambda g: dist.all_reduce(g)
+        eng.set_grad_scale(1.0 / world)
+    pool = []
+    for i in range(4):
+        nb = pkg.synthetic.make_batch(B, L, H, seed=1 + rank * 16 + i)
+        pool.append({k: torch.as_tensor(v).to(dev) for k, v in nb.items() if v is not None})
+    torch.cuda.synchronize()
+    eng.load_batch(pool[0])
+    if not args.no_graph:
+        eng.capture()
+
+    def step(i):
+        eng.load_batch(pool[i % len(pool)])
+        eng.train_step()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    loss = float(eng.LOSS.item())
+    gnorm = eng.last_grad_norm()
+
+    # dominant kernel: the ConvTranspose2d weight-gradient implicit GEMM (unique instantiation
+    # gemm_kernel<128,128,false,false,false,true>): M=768, N=9*2048, K=B*49
+    wg_call = next(c for c in eng.bwd_calls if c.name == "vqa_gemm" and c.keep.b_conv == 1)
+    kdur = time_kernel(wg_call, 20, torch.cuda.current_stream(dev))
+    kflop = 2.0 * wg_call.keep.m * wg_call.keep.n * wg_call.keep.k
+    k_tflops = kflop / kdur / 1e12
+
+    pairs = world * B * args.steps
+    value = pairs / dt
+    out = {
+        "metric": "question-image pairs/sec, ResNet50+T5-base+SGA train step, 1/2/4/8 MI355X",
+        "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": "ResNet50 + T5-base + 3xSGA train step (BASELINE configs[1]; configs[2] at N=8)",
+                   "model": "resnet50+t5-base+3xSGA", "global_batch": world * B, "per_gpu_batch": B,
+                   "seq_len": L, "image_size": H, "answers": 170, "parallelism": f"dp{world}",
+                   "graph": not args.no_graph},
+        "roofline": {"bound": "mfma", "kernel": "gemm_kernel<128,128,0,0,0,1> (ConvTranspose2d dW implicit GEMM)",
+                     "achieved": round(k_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(k_tflops / MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel_avg_us": round(kdur * 1e6, 2), "flop_per_launch": kflop,
+                     "step_mfma_frac": round(value / world * FLOP_PER_PAIR / (MFMA_PEAK_TFLOPS * 1e12), 4)},
+        "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pkg)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

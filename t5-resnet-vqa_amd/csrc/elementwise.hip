@@ -154,6 +154,11 @@ __global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restr
   }
 }
 
+__global__ __launch_bounds__(256) void zero_kernel(uint4* __restrict__ p, long n16) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256)
+    p[i] = make_uint4(0, 0, 0, 0);
+}
+
 }  // namespace
 
 extern "C" int vqa_image_to_nhwc8(const float* img, void* out, int n, int h, int w, hipStream_t s) {
@@ -230,9 +235,14 @@ extern "C" int vqa_cast_f32_bf16(const float* x, void* y, long long n, hipStream
   return vqa::check_launch("vqa_cast_f32_bf16");
 }
 
+// A kernel, not hipMemsetAsync: memset nodes captured into a hipGraph replayed
+// garbage into the zeroed gradient buffers on the ROCm 7.0 runtime torch ships.
 extern "C" int vqa_zero(void* p, long long bytes, hipStream_t s) {
-  VQA_REQUIRE(p && bytes >= 0, "vqa_zero: bad arguments");
-  hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, s);
-  if (e != hipSuccess) return vqa::fail((int)e, "vqa_zero: %s", hipGetErrorString(e));
-  return VQA_OK;
+  VQA_REQUIRE(p && bytes >= 0 && ((uintptr_t)p & 15) == 0 && bytes % 16 == 0,
+              "vqa_zero: pointer and size must be 16-byte aligned");
+  if (bytes == 0) return VQA_OK;
+  const long n16 = (long)(bytes / 16);
+  const int grid = (int)((n16 + 255) / 256 < 8192 ? (n16 + 255) / 256 : 8192);
+  hipLaunchKernelGGL(zero_kernel, dim3(grid), dim3(256), 0, s, (uint4*)p, n16);
+  return vqa::check_launch("vqa_zero");
 }
