@@ -65,6 +65,7 @@ typedef struct vqa_gemm_desc {
   int a_conv; vqa_conv_geom ga;
   int b_conv; vqa_conv_geom gb;
   int batch; long long stride_a, stride_b, stride_c32, stride_c16, stride_res;
+  int config;              /* 0 auto; 1: 128x128 tile; 2: 128x64; 3: 64x64; 4: 64x64 2-stage (tuning) */
 } vqa_gemm_desc;
 
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
@@ -79,7 +80,8 @@ int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
  * q[(b*lq + i)*ldq + h*dh + e] (likewise K, V, O, dO, dQ, dK, dV), so Q/K/V are
  * read in place from fused projection outputs.  p: saved P [B, H, Lq, Lk].
  * Backward: dS = P (dP - rowsum(P dP)), dQ = scale dS K, dK = scale dS^T Q,
- * dV = P^T dO; dbias[h,i,j] += sum_b dS (atomic) when dbias != NULL. */
+ * dV = P^T dO; when dbias != NULL the per-sample dS is written to
+ * dbias[b, h, i, j] (reduce with vqa_batch_sum; no atomics -> deterministic). */
 typedef struct vqa_attn_desc {
   const void* q; long long ldq;
   const void* k; long long ldk;
@@ -140,12 +142,16 @@ int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long long ld, floa
 int vqa_colsum_workspace_floats(int rows, int cols);
 int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int tokens, int d, int vocab,
                       hipStream_t stream);
-int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab,
+/* deterministic: each touched row is written once (fixed token order); ws = 2*tokens ints */
+int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab, int* ws,
                       hipStream_t stream);
 int vqa_t5_relbias_fwd(const float* table, const int* bucket, float* out, int heads, int lq, int lk,
                        hipStream_t stream);
+/* dtable[b, h] = sum_{(i,j): bucket = b} dbias[h, i, j] (overwrites, fixed order) */
 int vqa_t5_relbias_bwd(const float* dbias, const int* bucket, float* dtable, int heads, int lq, int lk,
-                       hipStream_t stream);
+                       int nbuckets, hipStream_t stream);
+/* out[i] = beta*out[i] + sum_b x[b*n + i] (fixed order; reduces per-sample attention dS) */
+int vqa_batch_sum(const float* x, int batch, long long n, float* out, float beta, hipStream_t stream);
 int vqa_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t stream);
 int vqa_zero(void* p, long long bytes, hipStream_t stream);
 

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnP P) {
     if (l < lk) {
       const float ds = pr * (dp - di);
       dS[i * sst + l] = ds;
-      if (P.dbias) atomicAdd(P.dbias + ((long)h * lq + i) * lk + l, ds);
+      if (P.dbias) P.dbias[(((long)b * P.heads + h) * lq + i) * lk + l] = ds;   // per-sample dS
     }
   }
   __syncthreads();

@@ -88,15 +88,6 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const void* __restrict
                                        red[3][threadIdx.x];
 }
 
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ ws, int parts, int cols,
-                                                           float* __restrict__ out, float beta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int p = 0; p < parts; ++p) s += ws[(long)p * cols + c];
-  out[c] = beta != 0.f ? beta * out[c] + s : s;
-}
-
 // h[t, :] = table[ids[t], :]  (T5Stack embed_tokens, modeling_t5.py:678)
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(const long long* __restrict__ ids,
                                                             const float* __restrict__ table, float* __restrict__ out,
@@ -109,16 +100,41 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const long long* __r
   reinterpret_cast<float4*>(out)[i] = reinterpret_cast<const float4*>(table + id * (long)d4 * 4)[j];
 }
 
-// dtable[ids[t], :] += dh[t, :]   (dense embedding gradient, nn.Embedding sparse=False)
+// Deterministic dense embedding gradient (nn.Embedding sparse=False): every
+// vocabulary row touched by the batch is written ONCE by its first occurrence
+// ("leader"), summing the occurrences in token order along a next[] chain.
+// No atomics, so the result is bit-identical run to run (DP ranks stay in
+// lockstep, graph replay == eager).  links: [0, T) next index (-1 = end),
+// [T, 2T) leader flag.
+__global__ __launch_bounds__(1024) void embedding_links_kernel(const long long* __restrict__ ids, int tokens,
+                                                               int* __restrict__ links) {
+  extern __shared__ int sid[];
+  for (int t = threadIdx.x; t < tokens; t += blockDim.x) sid[t] = (int)ids[t];
+  __syncthreads();
+  for (int t = threadIdx.x; t < tokens; t += blockDim.x) {
+    const int v = sid[t];
+    int nxt = -1, lead = 1;
+    for (int u = 0; u < t; ++u) lead &= (sid[u] != v);
+    for (int u = t + 1; u < tokens; ++u)
+      if (sid[u] == v) { nxt = u; break; }
+    links[t] = nxt;
+    links[tokens + t] = lead;
+  }
+}
+
 __global__ __launch_bounds__(256) void embedding_bwd_kernel(const long long* __restrict__ ids,
                                                             const float* __restrict__ dh, float* __restrict__ dtable,
-                                                            int tokens, int d, int vocab) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)tokens * d) return;
-  const int t = (int)(i / d), j = (int)(i - (long)t * d);
+                                                            const int* __restrict__ links, int tokens, int d,
+                                                            int vocab) {
+  const int t = blockIdx.x;
+  if (!links[tokens + t]) return;
   long long id = ids[t];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
-  atomicAdd(dtable + id * (long)d + j, dh[i]);
+  for (int c = threadIdx.x; c < d; c += 256) {
+    float s = 0.f;
+    for (int u = t; u >= 0; u = links[u]) s += dh[(long)u * d + c];
+    dtable[id * (long)d + c] = s;
+  }
 }
 
 // bias[h, i, j] = table[bucket[i*lk + j], h]   (compute_bias, modeling_t5.py:264-279)
@@ -131,13 +147,27 @@ __global__ __launch_bounds__(256) void relbias_fwd_kernel(const float* __restric
   out[i] = table[bucket[p] * heads + h];
 }
 
+// dtable[b, h] = sum over (i, j) with bucket(i, j) == b of dbias[h, i, j], fixed order
 __global__ __launch_bounds__(256) void relbias_bwd_kernel(const float* __restrict__ dbias,
                                                           const int* __restrict__ bucket, float* __restrict__ dtable,
-                                                          int heads, int lqk) {
+                                                          int heads, int lqk, int nbuckets) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= heads * lqk) return;
-  const int h = i / lqk, p = i - h * lqk;
-  atomicAdd(dtable + bucket[p] * heads + h, dbias[i]);
+  if (i >= heads * nbuckets) return;
+  const int bk = i / heads, h = i - bk * heads;
+  float s = 0.f;
+  for (int p = 0; p < lqk; ++p)
+    if (bucket[p] == bk) s += dbias[(long)h * lqk + p];
+  dtable[bk * heads + h] = s;
+}
+
+// out[i] = beta*out[i] + sum_b x[b*n + i]   (fixed order)
+__global__ __launch_bounds__(256) void batch_sum_kernel(const float* __restrict__ x, int batch, long n,
+                                                        float* __restrict__ out, float beta) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int b = 0; b < batch; ++b) s += x[(long)b * n + i];
+  out[i] = beta != 0.f ? beta * out[i] + s : s;
 }
 
 __global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
@@ -189,8 +219,7 @@ extern "C" int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long lo
   else
     hipLaunchKernelGGL(colsum_part_kernel<false>, grid, dim3(256), 0, s, x, rows, cols, (long)ld, ws);
   if (int rc = vqa::check_launch("vqa_colsum")) return rc;
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(vqa::cdiv(cols, 256)), dim3(256), 0, s, ws, parts, cols, out, beta);
-  return vqa::check_launch("vqa_colsum/final");
+  return vqa_colsum_partials(ws, parts, cols, cols, out, beta, s);
 }
 
 extern "C" int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int tokens, int d, int vocab,
@@ -203,12 +232,18 @@ extern "C" int vqa_embedding_fwd(const long long* ids, const float* table, float
 }
 
 extern "C" int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab,
-                                 hipStream_t s) {
-  VQA_REQUIRE(ids && dh && dtable, "vqa_embedding_bwd: bad arguments");
-  const long total = (long)tokens * d;
-  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(vqa::cdiv(total, 256)), dim3(256), 0, s, ids, dh, dtable, tokens, d,
-                     vocab);
+                                 int* ws, hipStream_t s) {
+  VQA_REQUIRE(ids && dh && dtable && ws && tokens > 0 && tokens <= 16384, "vqa_embedding_bwd: bad arguments");
+  hipLaunchKernelGGL(embedding_links_kernel, dim3(1), dim3(1024), tokens * sizeof(int), s, ids, tokens, ws);
+  if (int rc = vqa::check_launch("vqa_embedding_bwd/links")) return rc;
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(tokens), dim3(256), 0, s, ids, dh, dtable, ws, tokens, d, vocab);
   return vqa::check_launch("vqa_embedding_bwd");
+}
+
+extern "C" int vqa_batch_sum(const float* x, int batch, long long n, float* out, float beta, hipStream_t s) {
+  VQA_REQUIRE(x && out && batch > 0 && n > 0, "vqa_batch_sum: bad arguments");
+  hipLaunchKernelGGL(batch_sum_kernel, dim3(vqa::cdiv(n, 256)), dim3(256), 0, s, x, batch, (long)n, out, beta);
+  return vqa::check_launch("vqa_batch_sum");
 }
 
 extern "C" int vqa_t5_relbias_fwd(const float* table, const int* bucket, float* out, int heads, int lq, int lk,
@@ -220,10 +255,10 @@ extern "C" int vqa_t5_relbias_fwd(const float* table, const int* bucket, float* 
 }
 
 extern "C" int vqa_t5_relbias_bwd(const float* dbias, const int* bucket, float* dtable, int heads, int lq, int lk,
-                                  hipStream_t s) {
+                                  int nbuckets, hipStream_t s) {
   VQA_REQUIRE(dbias && bucket && dtable, "vqa_t5_relbias_bwd: bad arguments");
-  hipLaunchKernelGGL(relbias_bwd_kernel, dim3(vqa::cdiv(heads * lq * lk, 256)), dim3(256), 0, s, dbias, bucket, dtable,
-                     heads, lq * lk);
+  hipLaunchKernelGGL(relbias_bwd_kernel, dim3(vqa::cdiv(heads * nbuckets, 256)), dim3(256), 0, s, dbias, bucket,
+                     dtable, heads, lq * lk, nbuckets);
   return vqa::check_launch("vqa_t5_relbias_bwd");
 }
 

@@ -8,20 +8,29 @@
 //   conv weight grad implicit im2col as B (ConvTranspose2d dW, resnet_vqa_model.py:72-78)
 //
 // Tile BM x BN x 64, 256 threads = 4 waves (2x2), each wave (BM/2)x(BN/2) built
-// from 32x32 v_mfma_f32_32x32x16_bf16 tiles.  Operands are register-staged
-// into a double-buffered LDS image:
-//   k-contig operand  -> [rows][64] (128-B rows), XOR swizzle chunk^((row>>1)&7),
-//                        fragments by ds_read_b128 (conflict-free on the 4x16 lane groups);
-//   m/n-contig operand-> [64 k][rows], XOR swizzle per T10 image (b),
+// from 32x32 v_mfma_f32_32x32x16_bf16 tiles.  Operand tiles stream HBM -> LDS
+// through a STAGES-deep ring filled by global_load_lds_dwordx4 (LDS-DMA, no
+// VGPR staging), retired with a counted `s_waitcnt vmcnt` and a raw s_barrier
+// so STAGES-1 K-tiles stay in flight across barriers (cdna_hip_programming.md
+// §5 "Pipelining across barriers").  LDS images:
+//   k-contig operand  -> [rows][64] (128-B rows), chunk ^= (row>>1)&7,
+//                        fragments by ds_read_b128 (conflict-free on its 4x16 lane groups);
+//   m/n-contig operand-> [64 k][rows], chunk ^= T10 image-(b) pattern,
 //                        fragments by ds_read_b64_tr_b16 (hardware transpose).
-// Block ids are remapped so that the blocks sharing an XCD (b % 8) get a
+// glds writes LDS lane-linearly, so the swizzle is applied to the per-lane
+// SOURCE address (an XOR involution); lanes whose element is outside the
+// matrix / conv padding read a 16-B zero page instead (no predication).
+// Block ids are remapped so that blocks sharing an XCD (b % 8) get a
 // contiguous range of tiles (bijective form, cdna_hip_programming.md §5).
 #include "common.h"
+
+__device__ __attribute__((aligned(64))) uint4 vqa_zero_page[4];   // zero-initialised code-object global
 
 namespace {
 
 constexpr int BK = 64;
 constexpr int NT = 256;
+typedef __attribute__((address_space(3))) void lds_void_t;
 
 struct GemmParams {
   const bf16_t* a; long lda;
@@ -36,143 +45,208 @@ struct GemmParams {
   vqa_conv_geom ga, gb;
   long sa, sb, sc32, sc16, sres;
   int tiles_m, tiles_n;
+  int vec;                 // 4-wide vector epilogue legal (N, ld*, pointers aligned)
 };
 
 // byte offset of 16-B chunk `ch` of row `row` in a k-contig image ([rows][64 bf16])
-__device__ __forceinline__ int kc_off(int row, int ch) {
-  return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4);
-}
+__device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + ((ch ^ kc_swz(row)) << 4); }
 // byte offset of chunk `ch` of k-row `kr` in an m/n-contig image ([64][ROWLEN bf16])
 template <int ROWLEN>
+__device__ __forceinline__ int mn_swz(int kr) {
+  if constexpr (ROWLEN == 128) return ((kr & 3) << 2) | ((kr >> 2) & 3);
+  else return ((((kr >> 1) & 1) << 2) | ((kr >> 2) & 3));
+}
+template <int ROWLEN>
 __device__ __forceinline__ int mn_off(int kr, int ch) {
-  if constexpr (ROWLEN == 128) {
-    return kr * 256 + ((ch ^ (((kr & 3) << 2) | ((kr >> 2) & 3))) << 4);
-  } else {
-    static_assert(ROWLEN == 64, "row length");
-    return kr * 128 + ((ch ^ ((((kr >> 1) & 1) << 2) | ((kr >> 2) & 3))) << 4);
-  }
+  return kr * (ROWLEN * 2) + ((ch ^ mn_swz<ROWLEN>(kr)) << 4);
 }
 
-// ---------------------------------------------------------------- staging
-// One operand tile: ROWS x 64 (k-contig) or 64 x ROWS (m/n-contig), ROWS*8 chunks.
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+// ---------------------------------------------------------------- LDS-DMA loader
+// One operand tile of ROWS (m or n) x 64 (k): ROWS*128 bytes = ROWS/8 wave
+// instructions of 1 KiB; NI per wave.  KC image: 8 rows per instruction;
+// MN image: 1024 / (2*ROWS) k-rows per instruction.
 template <int ROWS, bool KC, bool GATHER>
-struct Stager {
-  static constexpr int NCH = ROWS * 8 / NT;     // 16-B chunks per thread
-  static constexpr int CPR = ROWS / 8;          // chunks per k-row in the m/n-contig image
-  uint4 r[NCH];
-  // gather state (KC: per-chunk output pixel; MN: per-thread (kh,kw,c))
-  int img[GATHER && KC ? NCH : 1], ih0[GATHER && KC ? NCH : 1], iw0[GATHER && KC ? NCH : 1];
-  int fkh, fkw, fc;
+struct Loader {
+  static constexpr int NI = ROWS / 32;
+  static constexpr int RPI = KC ? 8 : 1024 / (ROWS * 2);
+  static constexpr int CPR = KC ? 8 : ROWS / 8;          // 16-B chunks per image row
+  long off[NI];            // KC: element offset of (row, chunk) at k0 = 0; MN: column index
+  int kof[NI];             // KC: k offset of the chunk inside the tile; MN: k-row inside the tile
+  int g0[NI], g1[NI], g2[NI];
+  bool ok[NI];
 
-  __device__ __forceinline__ void init(int row0, int nrows, const vqa_conv_geom& g) {
-    const int tid = threadIdx.x;
-    if constexpr (GATHER && KC) {
+  __device__ __forceinline__ void init(int row0, int nrows, long ld, const vqa_conv_geom& g) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
 #pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        int row = row0 + ((i * NT + tid) >> 3);
-        if (row < nrows) {
-          int hw = g.oh * g.ow;
-          int im = row / hw, rem = row - im * hw;
-          int oh = rem / g.ow, ow = rem - oh * g.ow;
-          img[i] = im; ih0[i] = oh * g.stride - g.pad; iw0[i] = ow * g.stride - g.pad;
-        } else {
-          img[i] = 0; ih0[i] = -(1 << 28); iw0[i] = -(1 << 28);
-        }
-      }
-    }
-    if constexpr (GATHER && !KC) {
-      int col = row0 + (tid % CPR) * 8;       // feature index (kh,kw,c)
-      int tap = col / g.c;
-      fc = col - tap * g.c;
-      fkh = tap / g.kw;
-      fkw = tap - fkh * g.kw;
-    }
-  }
-
-  __device__ __forceinline__ void load(const bf16_t* __restrict__ base, long ld, int row0, int nrows,
-                                       int k0, int K, const vqa_conv_geom& g) {
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int idx = i * NT + tid;
-      bool ok;
-      const bf16_t* p;
+    for (int j = 0; j < NI; ++j) {
+      const int ins = w * NI + j;
       if constexpr (KC) {
-        const int row = row0 + (idx >> 3);
-        const int kk = k0 + (idx & 7) * 8;
-        ok = (row < nrows) & (kk < K);
-        if constexpr (!GATHER) {
-          p = base + (long)row * ld + kk;
-        } else {
-          int tap = kk / g.c;
-          int c = kk - tap * g.c;
-          int kh = tap / g.kw, kw = tap - kh * g.kw;
-          int ih = ih0[i] + kh, iw = iw0[i] + kw;
-          ok = ok & (ih >= 0) & (ih < g.h) & (iw >= 0) & (iw < g.w);
-          p = base + (((long)img[i] * g.h + ih) * g.w + iw) * g.c + c;
+        const int row = ins * 8 + (l >> 3);
+        const int ch = (l & 7) ^ kc_swz(row);
+        const int grow = row0 + row;
+        ok[j] = grow < nrows;
+        kof[j] = ch * 8;
+        off[j] = (long)grow * ld + ch * 8;
+        if constexpr (GATHER) {                  // output pixel (img, oh, ow) of this row
+          if (ok[j]) {
+            const int hw = g.oh * g.ow;
+            const int im = grow / hw, rem = grow - im * hw;
+            const int oh = rem / g.ow, ow = rem - oh * g.ow;
+            g0[j] = im; g1[j] = oh * g.stride - g.pad; g2[j] = ow * g.stride - g.pad;
+          } else {
+            g0[j] = 0; g1[j] = -(1 << 28); g2[j] = -(1 << 28);
+          }
         }
       } else {
-        const int kr = idx / CPR;
-        const int col = row0 + (idx % CPR) * 8;
-        const int kk = k0 + kr;
-        ok = (kk < K) & (col < nrows);
-        if constexpr (!GATHER) {
-          p = base + (long)kk * ld + col;
-        } else {
-          int hw = g.oh * g.ow;
-          int im = kk / hw, rem = kk - im * hw;
-          int oh = rem / g.ow, ow = rem - oh * g.ow;
-          int ih = oh * g.stride - g.pad + fkh, iw = ow * g.stride - g.pad + fkw;
-          ok = ok & (ih >= 0) & (ih < g.h) & (iw >= 0) & (iw < g.w);
-          p = base + (((long)im * g.h + ih) * g.w + iw) * g.c + fc;
+        const int kr = ins * RPI + l / CPR;
+        const int ch = (l % CPR) ^ mn_swz<ROWS>(kr);
+        const int col = row0 + ch * 8;
+        ok[j] = col < nrows;
+        off[j] = col;
+        kof[j] = kr;
+        if constexpr (GATHER) {                  // feature (kh, kw, c) of this column
+          const int tap = col / g.c;
+          g1[j] = col - tap * g.c;
+          g2[j] = tap;
         }
       }
-      r[i] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
     }
   }
 
-  __device__ __forceinline__ void store(char* lds) {
-    const int tid = threadIdx.x;
+  __device__ __forceinline__ void issue(const bf16_t* __restrict__ base, long ld, char* stage, int k0, int K,
+                                        const vqa_conv_geom& g) {
+    const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int idx = i * NT + tid;
-      int off;
-      if constexpr (KC) off = kc_off(idx >> 3, idx & 7);
-      else off = mn_off<ROWS>(idx / CPR, idx % CPR);
-      *reinterpret_cast<uint4*>(lds + off) = r[i];
+    for (int j = 0; j < NI; ++j) {
+      const void* src = vqa_zero_page;
+      const int kk = k0 + kof[j];
+      if (ok[j] && kk < K) {
+        if constexpr (KC && !GATHER) {
+          src = base + off[j] + k0;
+        } else if constexpr (KC && GATHER) {
+          const int tap = kk / g.c, c = kk - tap * g.c;
+          const int kh = tap / g.kw, kw = tap - kh * g.kw;
+          const int ih = g1[j] + kh, iw = g2[j] + kw;
+          if (ih >= 0 && ih < g.h && iw >= 0 && iw < g.w)
+            src = base + (((long)g0[j] * g.h + ih) * g.w + iw) * g.c + c;
+        } else if constexpr (!KC && !GATHER) {
+          src = base + (long)kk * ld + off[j];
+        } else {
+          const int hw = g.oh * g.ow;
+          const int im = kk / hw, rem = kk - im * hw;
+          const int oh = rem / g.ow, ow = rem - oh * g.ow;
+          const int kh = g2[j] / g.kw, kw = g2[j] - kh * g.kw;
+          const int ih = oh * g.stride - g.pad + kh, iw = ow * g.stride - g.pad + kw;
+          if (ih >= 0 && ih < g.h && iw >= 0 && iw < g.w)
+            src = base + (((long)im * g.h + ih) * g.w + iw) * g.c + g1[j];
+        }
+      }
+      glds16(src, stage + (w * NI + j) * 1024);
     }
   }
 };
 
-// fragment of one 32-row MFMA operand tile at k-step s (16 deep)
-template <int ROWS, bool KC>
-__device__ __forceinline__ bf16x8_t read_frag(const char* lds, int row_base, int s) {
-  const int l = threadIdx.x & 63;
-  if constexpr (KC) {
-    const int row = row_base + (l & 31);
-    const int ch = 2 * s + (l >> 5);
-    uint4 v = *reinterpret_cast<const uint4*>(lds + kc_off(row, ch));
-    return __builtin_bit_cast(bf16x8_t, v);
-  } else {
-    const int h = l >> 5, g1 = (l >> 4) & 1, i16 = l & 15, q = i16 >> 2, p = i16 & 3;
-    const int col = row_base + 16 * g1 + 4 * p;
-    const int ch = col >> 3, half = (col >> 2) & 1;
-    const int kr0 = 16 * s + 8 * h + q;
-    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_s16x4_t*)(lds + mn_off<ROWS>(kr0, ch) + 8 * half));
-    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_s16x4_t*)(lds + mn_off<ROWS>(kr0 + 4, ch) + 8 * half));
-    typedef short s16x8_t __attribute__((ext_vector_type(8)));
-    s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
-  }
+// ---------------------------------------------------------------- fragment reads
+// Issued as inline asm: the compiler cannot prove a ds_read does not alias an
+// in-flight LDS-DMA of the ring and would otherwise put `s_waitcnt vmcnt(0)`
+// in front of every K-tile's first read, draining the pipeline.  The waits
+// are therefore explicit (counted lgkmcnt + sched_barrier, guide §5.4 rule 18).
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ i32x4_t ds_b128(uint32_t addr) {
+  i32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ i32x2_t ds_tr16(uint32_t addr) {
+  i32x2_t v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int BM, int BN, bool AKC, bool BKC, bool GA, bool GB>
+// Per-lane LDS byte offsets of one operand's fragments (k-step 0), relative to
+// the operand image base.  KC: lane reads row (base + l&31), chunk 2s + (l>>5);
+// MN: two ds_read_b64_tr_b16 per fragment (k rows 16s+8h+q and +4).
+template <int ROWS, bool KC, int T>
+struct FragAddr {
+  uint32_t o[KC ? 4 : 2 * T];
+  __device__ __forceinline__ void init(int row_base) {
+    const int l = threadIdx.x & 63;
+    if constexpr (KC) {
+      const int row = row_base + (l & 31);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) o[s] = kc_off(row, 2 * s + (l >> 5));
+    } else {
+      const int h = l >> 5, g1 = (l >> 4) & 1, i16 = l & 15, q = i16 >> 2, p = i16 & 3;
+#pragma unroll
+      for (int i = 0; i < T; ++i) {
+        const int col = row_base + i * 32 + 16 * g1 + 4 * p;
+        const int ch = col >> 3, half = (col >> 2) & 1;
+        const int kr0 = 8 * h + q;
+        o[2 * i] = mn_off<ROWS>(kr0, ch) + 8 * half;
+        o[2 * i + 1] = mn_off<ROWS>(kr0 + 4, ch) + 8 * half;
+      }
+    }
+  }
+  // issue the reads of k-step s for the T fragments of this wave
+  __device__ __forceinline__ void read(uint32_t base, int s, i32x4_t (&f)[T]) const {
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+      if constexpr (KC) {
+        f[i] = ds_b128(base + o[s] + i * 32 * 128);
+      } else {
+        const uint32_t so = s * 16 * ROWS * 2;          // 16 k-rows per step; swizzle is s-invariant
+        const i32x2_t lo = ds_tr16(base + o[2 * i] + so);
+        const i32x2_t hi = ds_tr16(base + o[2 * i + 1] + so);
+        f[i] = i32x4_t{lo[0], lo[1], hi[0], hi[1]};
+      }
+    }
+  }
+  static constexpr int READS = KC ? T : 2 * T;
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NL, int STAGES>
+__device__ __forceinline__ void wait_tiles(int ahead) {
+  // keep `ahead` younger K-tiles (NL loads each) in flight, retire everything older
+  if constexpr (STAGES >= 4) {
+    if (ahead >= 2) { wait_vm<2 * NL>(); return; }
+  }
+  if constexpr (STAGES >= 3) {
+    if (ahead >= 1) { wait_vm<NL>(); return; }
+  }
+  wait_vm<0>();
+}
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BM, int BN, int STAGES, bool AKC, bool BKC, bool GA, bool GB>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, ST_BYTES = A_BYTES + B_BYTES;
+  using LA = Loader<BM, AKC, GA>;
+  using LB = Loader<BN, BKC, GB>;
+  constexpr int NL = LA::NI + LB::NI;                 // glds instructions per thread per K-tile
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * ST_BYTES];
 
   // XCD-aware bijective remap of the linear block id
   const int nwg = P.tiles_m * P.tiles_n;
@@ -189,10 +263,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int wm = w >> 1, wn = w & 1;
 
-  Stager<BM, AKC, GA> sa;
-  Stager<BN, BKC, GB> sb;
-  sa.init(m0, P.m, P.ga);
-  sb.init(n0, P.n, P.gb);
+  LA la;
+  LB lb;
+  la.init(m0, P.m, P.lda, P.ga);
+  lb.init(n0, P.n, P.ldb, P.gb);
+  using FA = FragAddr<BM, AKC, TM>;
+  using FB = FragAddr<BN, BKC, TN>;
+  FA fra;
+  FB frb;
+  fra.init(wm * WM);
+  frb.init(wn * WN);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
 
   f32x16_t acc[TM][TN];
 #pragma unroll
@@ -203,89 +284,190 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int nk = (P.k + BK - 1) / BK;
-  sa.load(A, P.lda, m0, P.m, 0, P.k, P.ga);
-  sb.load(B, P.ldb, n0, P.n, 0, P.k, P.gb);
-  sa.store(smem);
-  sb.store(smem + A_BYTES);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * (A_BYTES + B_BYTES);
-    char* nxt = smem + ((kt + 1) & 1) * (A_BYTES + B_BYTES);
-    const bool more = kt + 1 < nk;
-    if (more) {
-      sa.load(A, P.lda, m0, P.m, (kt + 1) * BK, P.k, P.ga);
-      sb.load(B, P.ldb, n0, P.n, (kt + 1) * BK, P.k, P.gb);
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) {
+    if (s < nk) {
+      la.issue(A, P.lda, smem + s * ST_BYTES, s * BK, P.k, P.ga);
+      lb.issue(B, P.ldb, smem + s * ST_BYTES + A_BYTES, s * BK, P.k, P.gb);
     }
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(nk - 1, kt + STAGES - 2) - kt;
+    wait_tiles<NL, STAGES>(ahead);
+    barrier();
+    const int nt = kt + STAGES - 1;
+    if (nt < nk) {
+      char* st = smem + (nt % STAGES) * ST_BYTES;
+      la.issue(A, P.lda, st, nt * BK, P.k, P.ga);
+      lb.issue(B, P.ldb, st + A_BYTES, nt * BK, P.k, P.gb);
+    }
+    const uint32_t cur = lds0 + (kt % STAGES) * ST_BYTES;
+    constexpr int R = FA::READS + FB::READS;
+    i32x4_t fa[2][TM], fb[2][TN];
+    fra.read(cur, 0, fa[0]);
+    frb.read(cur + A_BYTES, 0, fb[0]);
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
-      bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = read_frag<BM, AKC>(cur, wm * WM + i * 32, s);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = read_frag<BN, BKC>(cur + A_BYTES, wn * WN + j * 32, s);
+      if (s + 1 < BK / 16) {
+        fra.read(cur, s + 1, fa[(s + 1) & 1]);
+        frb.read(cur + A_BYTES, s + 1, fb[(s + 1) & 1]);
+        wait_lgkm<R>();
+      } else {
+        wait_lgkm<0>();
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          // swapped operands: D = B^T-tile x A^T-tile, so a lane owns one output ROW and
+          // 4 consecutive output COLUMNS per register group (vectorised epilogue)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, fb[s & 1][j]),
+                                                              __builtin_bit_cast(bf16x8_t, fa[s & 1][i]),
+                                                              acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      sa.store(nxt);
-      sb.store(nxt + A_BYTES);
-    }
-    __syncthreads();
   }
 
-  // epilogue: acc[i][j][e] -> row m0+wm*WM+i*32+(e&3)+8*(e>>2)+4*(l>>5), col n0+wn*WN+j*32+(l&31)
+  // epilogue: acc[i][j][4g+t] -> row m0+wm*WM+i*32+(l&31), col n0+wn*WN+j*32+8g+4(l>>5)+t.
+  // All inputs (bias, residual, mask, old C) are loaded before any store so the
+  // compiler can keep them in flight (C may alias them as far as it knows).
   float* C32 = P.c32 ? P.c32 + (long)z * P.sc32 : nullptr;
   bf16_t* C16 = P.c16 ? P.c16 + (long)z * P.sc16 : nullptr;
   const float* R32 = P.res32 ? P.res32 + (long)z * P.sres : nullptr;
   const bf16_t* R16 = P.res16 ? P.res16 + (long)z * P.sres : nullptr;
   const bf16_t* MK = P.mask16 ? P.mask16 + (long)z * P.sres : nullptr;
+  const bool beta = P.beta != 0.f && C32;
+  const int rl = l & 31, ch = l >> 5;
+  if (P.vec) {
+    float4 add[TM][TN][4];
+    uint2 msk[TM][TN][4];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + wn * WN + j * 32 + (l & 31);
-    if (col >= P.n) continue;
-    const float bias = P.bias ? P.bias[col] : 0.f;
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
-        if (row >= P.m) continue;
-        float v = acc[i][j][e] * P.alpha + bias;
-        if (R32) v += R32[(long)row * P.ldres + col];
-        if (R16) v += bf2f(R16[(long)row * P.ldres + col]);
-        if (P.relu) v = fmaxf(v, 0.f);
-        if (MK && !(bf2f(MK[(long)row * P.ldmask + col]) > 0.f)) v = 0.f;
-        if (C32) {
-          float* cp = C32 + (long)row * P.ldc32 + col;
-          *cp = P.beta != 0.f ? v + P.beta * *cp : v;
+        for (int g = 0; g < 4; ++g) {
+          const int row = m0 + wm * WM + i * 32 + rl;
+          const int col = n0 + wn * WN + j * 32 + 8 * g + 4 * ch;
+          float4 a4 = make_float4(0.f, 0.f, 0.f, 0.f);
+          uint2 m2 = make_uint2(0x3f803f80u, 0x3f803f80u);       // bf16 1.0 x4 (no mask)
+          if (row < P.m && col < P.n) {
+            if (P.bias) a4 = *reinterpret_cast<const float4*>(P.bias + col);
+            if (R32) {
+              const float4 r = *reinterpret_cast<const float4*>(R32 + (long)row * P.ldres + col);
+              a4.x += r.x; a4.y += r.y; a4.z += r.z; a4.w += r.w;
+            }
+            if (R16) {
+              const uint2 r = *reinterpret_cast<const uint2*>(R16 + (long)row * P.ldres + col);
+              a4.x += bf2f(r.x & 0xffff); a4.y += bf2f(r.x >> 16); a4.z += bf2f(r.y & 0xffff); a4.w += bf2f(r.y >> 16);
+            }
+            if (MK) m2 = *reinterpret_cast<const uint2*>(MK + (long)row * P.ldmask + col);
+          }
+          add[i][j][g] = a4;
+          msk[i][j][g] = m2;
         }
-        if (C16) C16[(long)row * P.ldc16 + col] = f2bf(v);
-      }
+    float4 old[TM][TN][4];
+    if (beta) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int row = m0 + wm * WM + i * 32 + rl;
+            const int col = n0 + wn * WN + j * 32 + 8 * g + 4 * ch;
+            old[i][j][g] = (row < P.m && col < P.n) ? *reinterpret_cast<const float4*>(C32 + (long)row * P.ldc32 + col)
+                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
     }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = m0 + wm * WM + i * 32 + rl;
+          const int col = n0 + wn * WN + j * 32 + 8 * g + 4 * ch;
+          if (row >= P.m || col >= P.n) continue;
+          const float4 a4 = add[i][j][g];
+          const uint2 m2 = msk[i][j][g];
+          float v[4] = {acc[i][j][4 * g] * P.alpha + a4.x, acc[i][j][4 * g + 1] * P.alpha + a4.y,
+                        acc[i][j][4 * g + 2] * P.alpha + a4.z, acc[i][j][4 * g + 3] * P.alpha + a4.w};
+          const float mk[4] = {bf2f(m2.x & 0xffff), bf2f(m2.x >> 16), bf2f(m2.y & 0xffff), bf2f(m2.y >> 16)};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (P.relu) v[t] = fmaxf(v[t], 0.f);
+            if (!(mk[t] > 0.f)) v[t] = 0.f;
+          }
+          if (C32) {
+            float4 o = make_float4(v[0], v[1], v[2], v[3]);
+            if (beta) {
+              const float4 c = old[i][j][g];
+              o.x += P.beta * c.x; o.y += P.beta * c.y; o.z += P.beta * c.z; o.w += P.beta * c.w;
+            }
+            *reinterpret_cast<float4*>(C32 + (long)row * P.ldc32 + col) = o;
+          }
+          if (C16) {
+            uint2 u;
+            u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+            u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            *reinterpret_cast<uint2*>(C16 + (long)row * P.ldc16 + col) = u;
+          }
+        }
+  } else {
+    // generic scalar path (odd N or leading dimensions)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = m0 + wm * WM + i * 32 + rl;
+          const int col = n0 + wn * WN + j * 32 + 8 * (e >> 2) + 4 * ch + (e & 3);
+          if (row >= P.m || col >= P.n) continue;
+          float v = acc[i][j][e] * P.alpha + (P.bias ? P.bias[col] : 0.f);
+          if (R32) v += R32[(long)row * P.ldres + col];
+          if (R16) v += bf2f(R16[(long)row * P.ldres + col]);
+          if (P.relu) v = fmaxf(v, 0.f);
+          if (MK && !(bf2f(MK[(long)row * P.ldmask + col]) > 0.f)) v = 0.f;
+          if (C32) {
+            float* cp = C32 + (long)row * P.ldc32 + col;
+            *cp = beta ? v + P.beta * *cp : v;
+          }
+          if (C16) C16[(long)row * P.ldc16 + col] = f2bf(v);
+        }
   }
 }
 
-template <int BM, int BN, bool AKC, bool BKC, bool GA, bool GB>
+template <int BM, int BN, int STAGES, bool AKC, bool BKC, bool GA, bool GB>
 int launch(GemmParams& P, int batch, hipStream_t s) {
   P.tiles_m = vqa::cdiv(P.m, BM);
   P.tiles_n = vqa::cdiv(P.n, BN);
   dim3 grid(P.tiles_m * P.tiles_n, 1, batch);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, AKC, BKC, GA, GB>), grid, dim3(NT), 0, s, P);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, STAGES, AKC, BKC, GA, GB>), grid, dim3(NT), 0, s, P);
   return vqa::check_launch("vqa_gemm");
 }
 
+// config: 0 = auto; 1 = 128x128 (3 stages); 2 = 128x64 (4); 3 = 64x64 (4); 4 = 64x64 (2)
+// Auto (measured on MI355X, tools/gemm_tune.py): the LDS-DMA fill rate per CU
+// grows with resident waves, so 64x64 tiles at 2 blocks/CU win almost
+// everywhere at this model's sizes; 128x128 only pays for narrow-N, long-K
+// convolutions (half the operand re-reads); with <= 2 K-tiles the ring is
+// useless and a 2-stage ring doubles the resident blocks.
 template <bool AKC, bool BKC, bool GA, bool GB>
-int dispatch_tile(GemmParams& P, int batch, hipStream_t s) {
-  // Largest tile that still gives >= ~1 wave of blocks over 256 CUs.
-  const long t128 = (long)vqa::cdiv(P.m, 128) * vqa::cdiv(P.n, 128) * batch;
-  const long t12864 = (long)vqa::cdiv(P.m, 128) * vqa::cdiv(P.n, 64) * batch;
-  if (t128 >= 256) return launch<128, 128, AKC, BKC, GA, GB>(P, batch, s);
-  if (t12864 >= 256) return launch<128, 64, AKC, BKC, GA, GB>(P, batch, s);
-  return launch<64, 64, AKC, BKC, GA, GB>(P, batch, s);
+int dispatch_tile(GemmParams& P, int batch, int config, hipStream_t s) {
+  if (config == 0) {
+    const long t128 = (long)vqa::cdiv(P.m, 128) * vqa::cdiv(P.n, 128) * batch;
+    const int nk = vqa::cdiv(P.k, BK);
+    if (nk <= 2) config = 4;
+    else if (P.n <= 256 && P.k >= 1024 && t128 >= 128) config = 1;
+    else config = 3;
+  }
+  switch (config) {
+    case 1: return launch<128, 128, 3, AKC, BKC, GA, GB>(P, batch, s);
+    case 2: return launch<128, 64, 4, AKC, BKC, GA, GB>(P, batch, s);
+    case 4: return launch<64, 64, 2, AKC, BKC, GA, GB>(P, batch, s);
+    default: return launch<64, 64, 4, AKC, BKC, GA, GB>(P, batch, s);
+  }
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -307,6 +489,7 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   VQA_REQUIRE(!d->a_conv || d->ga.c % 8 == 0, "vqa_gemm: conv input channels must be a multiple of 8");
   VQA_REQUIRE(!d->b_conv || d->gb.c % 8 == 0, "vqa_gemm: conv input channels must be a multiple of 8");
   VQA_REQUIRE(d->batch >= 1, "vqa_gemm: batch must be >= 1");
+  VQA_REQUIRE(d->config >= 0 && d->config <= 4, "vqa_gemm: config must be 0..4");
   GemmParams P;
   P.a = (const bf16_t*)d->a; P.lda = d->lda;
   P.b = (const bf16_t*)d->b; P.ldb = d->ldb;
@@ -318,13 +501,19 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   P.alpha = d->alpha; P.beta = d->beta; P.relu = d->relu;
   P.ga = d->ga; P.gb = d->gb;
   P.sa = d->stride_a; P.sb = d->stride_b; P.sc32 = d->stride_c32; P.sc16 = d->stride_c16; P.sres = d->stride_res;
-  const int batch = d->batch;
+  const int batch = d->batch, cfg = d->config;
+  auto al = [](const void* p, int bytes) { return p == nullptr || ((uintptr_t)p % bytes) == 0; };
+  P.vec = d->n % 4 == 0 && (!d->c32 || (d->ldc32 % 4 == 0 && al(d->c32, 16) && d->stride_c32 % 4 == 0)) &&
+          (!d->c16 || (d->ldc16 % 4 == 0 && al(d->c16, 8) && d->stride_c16 % 4 == 0)) &&
+          (!d->res32 || (d->ldres % 4 == 0 && al(d->res32, 16))) && (!d->res16 || (d->ldres % 4 == 0 && al(d->res16, 8))) &&
+          (!d->mask16 || (d->ldmask % 4 == 0 && al(d->mask16, 8))) && (!(d->res32 || d->res16 || d->mask16) || d->stride_res % 4 == 0) &&
+          al(d->bias, 16);
   const bool akc = !d->a_trans, bkc = !d->b_trans;
-  if (akc && bkc && !d->a_conv) return dispatch_tile<true, true, false, false>(P, batch, stream);
-  if (akc && bkc && d->a_conv) return dispatch_tile<true, true, true, false>(P, batch, stream);
-  if (akc && !bkc && !d->a_conv && !d->b_conv) return dispatch_tile<true, false, false, false>(P, batch, stream);
-  if (!akc && !bkc && !d->b_conv) return dispatch_tile<false, false, false, false>(P, batch, stream);
-  if (!akc && !bkc && d->b_conv) return dispatch_tile<false, false, false, true>(P, batch, stream);
-  if (!akc && bkc) return dispatch_tile<false, true, false, false>(P, batch, stream);
+  if (akc && bkc && !d->a_conv) return dispatch_tile<true, true, false, false>(P, batch, cfg, stream);
+  if (akc && bkc && d->a_conv) return dispatch_tile<true, true, true, false>(P, batch, cfg, stream);
+  if (akc && !bkc && !d->a_conv && !d->b_conv) return dispatch_tile<true, false, false, false>(P, batch, cfg, stream);
+  if (!akc && !bkc && !d->b_conv) return dispatch_tile<false, false, false, false>(P, batch, cfg, stream);
+  if (!akc && !bkc && d->b_conv) return dispatch_tile<false, false, false, true>(P, batch, cfg, stream);
+  if (!akc && bkc) return dispatch_tile<false, true, false, false>(P, batch, cfg, stream);
   return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: unsupported layout combination");
 }

@@ -1,63 +1,138 @@
 // Answer head: AttentionPooler (resnet_vqa_model.py:14-26) + classification
 // Linear(768, A) + log_softmax + NLLLoss(mean) (resnet_vqa_model.py:152-160),
-// forward and backward.  Tiny (B x 170 x 768): fp32 throughout, straight from
-// the fp32 master weights; one workgroup per sample plus deterministic
-// reductions for the weight gradients.
+// forward and backward, fp32 end to end (straight from the fp32 masters).
+//   pooler kernels: one workgroup per sample, each thread keeps its D/256
+//     columns of all L rows in registers, so scores, softmax, pooling and the
+//     pooler backward need a single read of the sample;
+//   classifier contractions (logits, dpooled, dWc): an LDS-tiled fp32 GEMM;
+//   every reduction runs in a fixed order (bit-reproducible).
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
 
-constexpr int MAXL = 64;
 constexpr int MAXA = 1024;
 
-__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wp,
-                                                       const float* __restrict__ bp, const float* __restrict__ wc,
-                                                       const float* __restrict__ bc,
-                                                       const long long* __restrict__ targets, float* __restrict__ att,
-                                                       float* __restrict__ pooled, float* __restrict__ logp,
-                                                       float* __restrict__ nll, int L, int D, int A) {
-  __shared__ float sc[MAXL];
-  __shared__ float pl[1024];
-  __shared__ float lg[MAXA];
+// ------------------------------------------------------------ small fp32 GEMM
+// C[m, n] = sum_k A(m, k) B(k, n) (+ bias[n]);  A(m,k) = a[m*sam + k*sak], B(k,n) = b[k*sbk + n*sbn]
+constexpr int SG_T = 32, SG_K = 32;
+__global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const float* __restrict__ a, long sam, long sak,
+                                                    const float* __restrict__ b, long sbk, long sbn,
+                                                    float* __restrict__ c, long ldc, const float* __restrict__ bias) {
+  __shared__ float As[SG_K][SG_T + 1], Bs[SG_K][SG_T + 1];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;          // 32 x 8 threads, 4 rows each
+  const int m0 = blockIdx.y * SG_T, n0 = blockIdx.x * SG_T;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += SG_K) {
+    for (int i = threadIdx.x; i < SG_T * SG_K; i += 256) {
+      const int r = i / SG_K, kk = i - r * SG_K;                    // A tile: row r, k kk
+      const int m = m0 + r, k = k0 + kk;
+      As[kk][r] = (m < M && k < K) ? a[(long)m * sam + (long)k * sak] : 0.f;
+      const int kb = i / SG_T, nn = i - kb * SG_T;                 // B tile: k kb, col nn
+      const int kg = k0 + kb, n = n0 + nn;
+      Bs[kb][nn] = (kg < K && n < N) ? b[(long)kg * sbk + (long)n * sbn] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < SG_K; ++kk) {
+      const float bv = Bs[kk][tx];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = fmaf(As[kk][ty * 4 + r], bv, acc[r]);
+    }
+    __syncthreads();
+  }
+  const int n = n0 + tx;
+  if (n >= N) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + ty * 4 + r;
+    if (m < M) c[(long)m * ldc + n] = acc[r] + (bias ? bias[n] : 0.f);
+  }
+}
+
+int sgemm(hipStream_t s, int M, int N, int K, const float* a, long sam, long sak, const float* b, long sbk, long sbn,
+          float* c, long ldc, const float* bias) {
+  dim3 grid(vqa::cdiv(N, SG_T), vqa::cdiv(M, SG_T));
+  hipLaunchKernelGGL(sgemm_kernel, grid, dim3(256), 0, s, M, N, K, a, sam, sak, b, sbk, sbn, c, ldc, bias);
+  return vqa::check_launch("head/sgemm");
+}
+
+// ------------------------------------------------------------ pooler
+// block-wide reduction of NV per-thread vectors of length L (one value per row t)
+template <int LMAX>
+__device__ __forceinline__ void block_row_sums(float (&part)[LMAX], int L, float* red /*[4][LMAX]*/,
+                                               float* out /*[LMAX]*/) {
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < LMAX; ++t) {
+    if (t < L) {
+      const float v = wave_sum(part[t]);
+      if (l == 0) red[wv * LMAX + t] = v;
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < L; t += 256) out[t] = red[t] + red[LMAX + t] + red[2 * LMAX + t] + red[3 * LMAX + t];
+  __syncthreads();
+}
+
+// scores = x wp + bp ; a = softmax_t(scores) ; pooled = a^T x     (D <= 768: 3 columns per thread)
+template <int LMAX>
+__global__ __launch_bounds__(256) void pool_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wp,
+                                                       const float* __restrict__ bp, float* __restrict__ att,
+                                                       float* __restrict__ pooled, int L, int D) {
+  constexpr int NC = 3;
+  __shared__ float red[4 * LMAX], sc[LMAX];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* xb = x + (long)b * L * D;
+  float xr[LMAX][NC], part[LMAX];
+  float w[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) w[j] = (tid + 256 * j < D) ? wp[tid + 256 * j] : 0.f;
+#pragma unroll
+  for (int t = 0; t < LMAX; ++t) {
+    part[t] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int d = tid + 256 * j;
+      xr[t][j] = (t < L && d < D) ? xb[(long)t * D + d] : 0.f;
+      part[t] = fmaf(xr[t][j], w[j], part[t]);
+    }
+  }
+  block_row_sums<LMAX>(part, L, red, sc);
+  if (tid < 64) {                                     // softmax over the sequence (Softmax(dim=1))
+    const float s = tid < L ? sc[tid] + bp[0] : -INFINITY;
+    const float m = wave_max(s);
+    const float e = tid < L ? __expf(s - m) : 0.f;
+    const float z = wave_sum(e);
+    if (tid < L) { sc[tid] = e / z; att[(long)b * L + tid] = e / z; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int d = tid + 256 * j;
+    if (d >= D) continue;
+    float p = 0.f;
+#pragma unroll
+    for (int t = 0; t < LMAX; ++t)
+      if (t < L) p = fmaf(sc[t], xr[t][j], p);
+    pooled[(long)b * D + d] = p;
+  }
+}
+
+// log_softmax over the A logits of one sample, NLL of its target
+__global__ __launch_bounds__(256) void lse_kernel(const float* __restrict__ logits, const long long* __restrict__ tgt,
+                                                  float* __restrict__ logp, float* __restrict__ nll, int A) {
   __shared__ float red[4];
   const int b = blockIdx.x, wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const float* xb = x + (long)b * L * D;
-  // scores[t] = x[t]·wp + bp
-  for (int t = wv; t < L; t += 4) {
-    float s = 0.f;
-    for (int d = l; d < D; d += 64) s += xb[(long)t * D + d] * wp[d];
-    s = wave_sum(s);
-    if (l == 0) sc[t] = s + bp[0];
-  }
-  __syncthreads();
-  if (wv == 0) {                                      // softmax over the sequence (Softmax(dim=1))
-    const float s = l < L ? sc[l] : -INFINITY;
-    const float m = wave_max(s);
-    const float e = l < L ? __expf(s - m) : 0.f;
-    const float z = wave_sum(e);
-    if (l < L) { sc[l] = e / z; att[(long)b * L + l] = e / z; }
-  }
-  __syncthreads();
-  for (int d = threadIdx.x; d < D; d += 256) {        // pooled = a^T x
-    float s = 0.f;
-    for (int t = 0; t < L; ++t) s += sc[t] * xb[(long)t * D + d];
-    pl[d] = s;
-    pooled[(long)b * D + d] = s;
-  }
-  __syncthreads();
-  for (int c = wv; c < A; c += 4) {                   // logits = pooled Wc^T + bc
-    float s = 0.f;
-    for (int d = l; d < D; d += 64) s += pl[d] * wc[(long)c * D + d];
-    s = wave_sum(s);
-    if (l == 0) lg[c] = s + bc[c];
-  }
-  __syncthreads();
+  const float* lg = logits + (long)b * A;
   float m = -INFINITY;
   for (int c = threadIdx.x; c < A; c += 256) m = fmaxf(m, lg[c]);
   m = wave_max(m);
   if (l == 0) red[wv] = m;
   __syncthreads();
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float lt = (threadIdx.x == 0 && tgt) ? lg[tgt[b]] : 0.f;    // read before the in-place write below
   __syncthreads();
   float z = 0.f;
   for (int c = threadIdx.x; c < A; c += 256) z += __expf(lg[c] - m);
@@ -66,126 +141,130 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
   __syncthreads();
   const float lse = m + __logf(red[0] + red[1] + red[2] + red[3]);
   for (int c = threadIdx.x; c < A; c += 256) logp[(long)b * A + c] = lg[c] - lse;
-  if (threadIdx.x == 0 && targets) nll[b] = -(lg[targets[b]] - lse);
+  if (threadIdx.x == 0 && tgt) nll[b] = -(lt - lse);
 }
 
-__global__ void mean_kernel(const float* __restrict__ v, int n, float* __restrict__ out) {
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int i = 0; i < n; ++i) s += v[i];
-    out[0] = s / n;
-  }
+// fixed-order mean / sum of n values by one workgroup
+__global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ v, int n, float scale,
+                                                     float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += v[i];
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) out[0] = s * scale;
 }
 
-// per-sample backward: dlogits, dpooled, pooler backward -> dx; saves dlogits / dscore
-__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ x, const float* __restrict__ att,
-                                                       const float* __restrict__ logp,
-                                                       const long long* __restrict__ targets,
-                                                       const float* __restrict__ wp, const float* __restrict__ wc,
-                                                       float* __restrict__ dx32, bf16_t* __restrict__ dx16,
-                                                       float* __restrict__ dlogits, float* __restrict__ dscore, int L,
-                                                       int D, int A, float inv_b) {
-  __shared__ float dl[MAXA];
-  __shared__ float dp[1024];
-  __shared__ float a[MAXL], da[MAXL];
-  const int b = blockIdx.x, wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+// dlogits = (softmax - onehot) / B
+__global__ __launch_bounds__(256) void dlogits_kernel(const float* __restrict__ logp, const long long* __restrict__ tgt,
+                                                      float* __restrict__ dl, int A, float inv_b) {
+  const int b = blockIdx.x;
+  const long long t = tgt[b];
+  for (int c = threadIdx.x; c < A; c += 256)
+    dl[(long)b * A + c] = (__expf(logp[(long)b * A + c]) - (c == t ? 1.f : 0.f)) * inv_b;
+}
+
+// pooler backward for one sample: da = x dpooled ; dscore = a (da - sum a da) ;
+// dx = a dpooled^T + dscore wp^T
+template <int LMAX>
+__global__ __launch_bounds__(256) void pool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ att,
+                                                       const float* __restrict__ dpooled,
+                                                       const float* __restrict__ wp, float* __restrict__ dx32,
+                                                       bf16_t* __restrict__ dx16, float* __restrict__ dscore, int L,
+                                                       int D) {
+  constexpr int NC = 3;
+  __shared__ float red[4 * LMAX], da[LMAX], a[LMAX];
+  const int b = blockIdx.x, tid = threadIdx.x;
   const float* xb = x + (long)b * L * D;
-  const long long t = targets[b];
-  for (int c = threadIdx.x; c < A; c += 256) {
-    const float g = (__expf(logp[(long)b * A + c]) - (c == t ? 1.f : 0.f)) * inv_b;
-    dl[c] = g;
-    dlogits[(long)b * A + c] = g;
+  float xr[LMAX][NC], part[LMAX], dp[NC], w[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int d = tid + 256 * j;
+    dp[j] = d < D ? dpooled[(long)b * D + d] : 0.f;
+    w[j] = d < D ? wp[d] : 0.f;
   }
-  for (int i = threadIdx.x; i < L; i += 256) a[i] = att[(long)b * L + i];
-  __syncthreads();
-  for (int d = threadIdx.x; d < D; d += 256) {
-    float s = 0.f;
-    for (int c = 0; c < A; ++c) s += dl[c] * wc[(long)c * D + d];
-    dp[d] = s;
+#pragma unroll
+  for (int t = 0; t < LMAX; ++t) {
+    part[t] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int d = tid + 256 * j;
+      xr[t][j] = (t < L && d < D) ? xb[(long)t * D + d] : 0.f;
+      part[t] = fmaf(xr[t][j], dp[j], part[t]);
+    }
   }
-  __syncthreads();
-  for (int i = wv; i < L; i += 4) {
-    float s = 0.f;
-    for (int d = l; d < D; d += 64) s += dp[d] * xb[(long)i * D + d];
-    s = wave_sum(s);
-    if (l == 0) da[i] = s;
-  }
-  __syncthreads();
-  if (wv == 0) {
-    const float ai = l < L ? a[l] : 0.f, dai = l < L ? da[l] : 0.f;
-    const float sum = wave_sum(ai * dai);
-    if (l < L) {
-      const float ds = ai * (dai - sum);
-      da[l] = ds;
-      dscore[(long)b * L + l] = ds;
+  for (int t = tid; t < L; t += 256) a[t] = att[(long)b * L + t];
+  block_row_sums<LMAX>(part, L, red, da);
+  if (tid < 64) {
+    const float ai = tid < L ? a[tid] : 0.f, dai = tid < L ? da[tid] : 0.f;
+    const float s = wave_sum(ai * dai);
+    if (tid < L) {
+      const float ds = ai * (dai - s);
+      da[tid] = ds;
+      dscore[(long)b * L + tid] = ds;
     }
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < L * D; idx += 256) {
-    const int i = idx / D, d = idx - i * D;
-    const float g = a[i] * dp[d] + da[i] * wp[d];
-    dx32[(long)b * L * D + idx] = g;
-    if (dx16) dx16[(long)b * L * D + idx] = f2bf(g);
+#pragma unroll
+  for (int t = 0; t < LMAX; ++t) {
+    if (t >= L) continue;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int d = tid + 256 * j;
+      if (d >= D) continue;
+      const float g = a[t] * dp[j] + da[t] * w[j];
+      dx32[((long)b * L + t) * D + d] = g;
+      if (dx16) dx16[((long)b * L + t) * D + d] = f2bf(g);
+    }
   }
 }
 
-// dWc[c][d] = sum_b dlogits[b][c] pooled[b][d] ; dbc[c] = sum_b dlogits[b][c]
-__global__ __launch_bounds__(256) void head_wgrad_cls_kernel(const float* __restrict__ dlogits,
-                                                             const float* __restrict__ pooled, float* __restrict__ dwc,
-                                                             float* __restrict__ dbc, int B, int D, int A) {
-  const int c = blockIdx.x;
-  for (int d = threadIdx.x; d < D; d += 256) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dlogits[(long)b * A + c] * pooled[(long)b * D + d];
-    dwc[(long)c * D + d] = s;
-  }
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dlogits[(long)b * A + c];
-    dbc[c] = s;
-  }
-}
-
-// partials of dWp[d] = sum_rows dscore[row] x[row][d]  over 64-row chunks
-__global__ __launch_bounds__(256) void head_wgrad_pool_kernel(const float* __restrict__ x,
-                                                              const float* __restrict__ dscore, float* __restrict__ ws,
-                                                              int rows, int D) {
+// partial dWp[d] = sum_rows dscore[row] x[row][d] over 64-row chunks
+__global__ __launch_bounds__(256) void wpool_part_kernel(const float* __restrict__ x, const float* __restrict__ ds,
+                                                         float* __restrict__ ws, int rows, int D) {
   const int r0 = blockIdx.y * 64;
-  for (int d = blockIdx.x * 256 + threadIdx.x; d < D; d += gridDim.x * 256) {
-    float s = 0.f;
-    for (int r = r0; r < min(rows, r0 + 64); ++r) s += dscore[r] * x[(long)r * D + d];
-    ws[(long)blockIdx.y * D + d] = s;
-  }
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= D) return;
+  float s = 0.f;
+#pragma unroll 8
+  for (int r = r0; r < min(rows, r0 + 64); ++r) s = fmaf(ds[r], x[(long)r * D + d], s);
+  ws[(long)blockIdx.y * D + d] = s;
 }
 
-__global__ void sum_kernel(const float* __restrict__ v, int n, float* __restrict__ out) {
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int i = 0; i < n; ++i) s += v[i];
-    out[0] = s;
-  }
+template <typename F>
+int with_lmax(int L, F f) {
+  if (L <= 16) return f(std::integral_constant<int, 16>());
+  if (L <= 32) return f(std::integral_constant<int, 32>());
+  return f(std::integral_constant<int, 64>());
 }
 
 }  // namespace
 
+extern "C" int vqa_head_workspace_floats(int batch, int seq, int d, int answers) {
+  return 2 * batch * answers + batch * d + batch * seq + vqa::cdiv(batch * seq, 64) * d;
+}
+
+// ws layout: logits | dlogits [B*A] each, dpooled [B*D], dscore [B*L], dWp partials
 extern "C" int vqa_head_fwd(const float* x, const float* wp, const float* bp, const float* wc, const float* bc,
                             const long long* targets, float* att, float* pooled, float* logp, float* nll, float* loss,
                             int batch, int seq, int d, int answers, hipStream_t s) {
   VQA_REQUIRE(x && wp && bp && wc && bc && att && pooled && logp, "vqa_head_fwd: null argument");
-  VQA_REQUIRE(seq <= MAXL && d <= 1024 && answers <= MAXA, "vqa_head_fwd: shape out of range");
+  VQA_REQUIRE(seq <= 64 && d <= 768 && answers <= MAXA, "vqa_head_fwd: shape out of range (L<=64, D<=768)");
   VQA_REQUIRE(!targets || (nll && loss), "vqa_head_fwd: targets need nll and loss outputs");
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(batch), dim3(256), 0, s, x, wp, bp, wc, bc, targets, att, pooled, logp, nll,
-                     seq, d, answers);
-  if (int rc = vqa::check_launch("vqa_head_fwd")) return rc;
+  int rc = with_lmax(seq, [&](auto lm) {
+    hipLaunchKernelGGL(pool_fwd_kernel<decltype(lm)::value>, dim3(batch), dim3(256), 0, s, x, wp, bp, att, pooled,
+                       seq, d);
+    return vqa::check_launch("vqa_head_fwd/pool");
+  });
+  if (rc) return rc;
+  // logits are staged in logp, then replaced by log_softmax in place
+  if ((rc = sgemm(s, batch, answers, d, pooled, d, 1, wc, 1, d, logp, answers, bc))) return rc;
+  hipLaunchKernelGGL(lse_kernel, dim3(batch), dim3(256), 0, s, logp, targets, logp, nll, answers);
+  if ((rc = vqa::check_launch("vqa_head_fwd/lse"))) return rc;
   if (targets) {
-    hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(64), 0, s, nll, batch, loss);
+    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, s, nll, batch, 1.0f / batch, loss);
     return vqa::check_launch("vqa_head_fwd/mean");
   }
   return VQA_OK;
-}
-
-extern "C" int vqa_head_workspace_floats(int batch, int seq, int d, int answers) {
-  return batch * answers + batch * seq + vqa::cdiv(batch * seq, 64) * d;
 }
 
 extern "C" int vqa_head_bwd(const float* x, const float* att, const float* pooled, const float* logp,
@@ -194,18 +273,29 @@ extern "C" int vqa_head_bwd(const float* x, const float* att, const float* poole
                             int answers, hipStream_t s) {
   VQA_REQUIRE(x && att && pooled && logp && targets && wp && wc && dx32 && dwp && dbp && dwc && dbc && ws,
               "vqa_head_bwd: null argument");
-  VQA_REQUIRE(seq <= MAXL && d <= 1024 && answers <= MAXA, "vqa_head_bwd: shape out of range");
-  float* dlogits = ws;
-  float* dscore = ws + batch * answers;
-  float* part = dscore + batch * seq;
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(batch), dim3(256), 0, s, x, att, logp, targets, wp, wc, dx32, (bf16_t*)dx16,
-                     dlogits, dscore, seq, d, answers, 1.0f / batch);
-  if (int rc = vqa::check_launch("vqa_head_bwd")) return rc;
-  hipLaunchKernelGGL(head_wgrad_cls_kernel, dim3(answers), dim3(256), 0, s, dlogits, pooled, dwc, dbc, batch, d,
-                     answers);
+  VQA_REQUIRE(seq <= 64 && d <= 768 && answers <= MAXA, "vqa_head_bwd: shape out of range");
+  float* dl = ws + batch * answers;
+  float* dpool = dl + batch * answers;
+  float* dsc = dpool + batch * d;
+  float* part = dsc + batch * seq;
+  hipLaunchKernelGGL(dlogits_kernel, dim3(batch), dim3(256), 0, s, logp, targets, dl, answers, 1.0f / batch);
+  int rc = vqa::check_launch("vqa_head_bwd/dlogits");
+  if (rc) return rc;
+  // dpooled[b, :] = dlogits[b, :] Wc
+  if ((rc = sgemm(s, batch, d, answers, dl, answers, 1, wc, d, 1, dpool, d, nullptr))) return rc;
+  rc = with_lmax(seq, [&](auto lm) {
+    hipLaunchKernelGGL(pool_bwd_kernel<decltype(lm)::value>, dim3(batch), dim3(256), 0, s, x, att, dpool, wp, dx32,
+                       (bf16_t*)dx16, dsc, seq, d);
+    return vqa::check_launch("vqa_head_bwd/pool");
+  });
+  if (rc) return rc;
+  // dWc = dlogits^T pooled ; dbc = column sums of dlogits
+  if ((rc = sgemm(s, answers, d, batch, dl, 1, answers, pooled, d, 1, dwc, d, nullptr))) return rc;
+  if ((rc = vqa_colsum_partials(dl, batch, answers, answers, dbc, 0.f, s))) return rc;
   const int rows = batch * seq, parts = vqa::cdiv(rows, 64);
-  hipLaunchKernelGGL(head_wgrad_pool_kernel, dim3(vqa::cdiv(d, 256), parts), dim3(256), 0, s, x, dscore, part, rows, d);
-  if (int rc = vqa::check_launch("vqa_head_bwd/wgrad")) return rc;
-  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(64), 0, s, dscore, rows, dbp);
+  hipLaunchKernelGGL(wpool_part_kernel, dim3(vqa::cdiv(d, 256), parts), dim3(256), 0, s, x, dsc, part, rows, d);
+  if ((rc = vqa::check_launch("vqa_head_bwd/wpool"))) return rc;
+  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, s, dsc, rows, 1.0f, dbp);
+  if ((rc = vqa::check_launch("vqa_head_bwd/dbp"))) return rc;
   return vqa_colsum_partials(part, parts, d, d, dwp, 0.f, s);
 }

@@ -217,17 +217,30 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
   }
 }
 
-// out[c] = beta*out[c] + sum_p ws[p*stride + c]  (fixed order -> deterministic)
-__global__ __launch_bounds__(256) void colsum_partials_kernel(const float* __restrict__ ws, int parts, long stride,
-                                                              int cols, float* __restrict__ out, float beta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+// out[c] = beta*out[c] + sum_p ws[p*stride + c]  (fixed order -> deterministic).
+// 1024 threads = 64 columns x 16 part-groups, so the partial reads are spread
+// over 16 waves instead of one long dependent chain per column.
+__global__ __launch_bounds__(1024) void colsum_partials_kernel(const float* __restrict__ ws, int parts, long stride,
+                                                               int cols, float* __restrict__ out, float beta) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
   float s = 0.f;
-  for (int p = 0; p < parts; ++p) s += ws[(long)p * stride + c];
-  out[c] = beta != 0.f ? beta * out[c] + s : s;
+  if (c < cols) {
+#pragma unroll 4
+    for (int p = ty; p < parts; p += 16) s += ws[(long)p * stride + c];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][tx];
+    out[c] = beta != 0.f ? beta * out[c] + t : t;
+  }
 }
 
-constexpr int NORM_BWD_ROWS = 32;      // rows per block in the backward kernels
+constexpr int NORM_BWD_ROWS = 16;      // rows per block in the backward kernels
 
 }  // namespace
 
@@ -260,7 +273,7 @@ extern "C" int vqa_rmsnorm_bwd(const float* dy, const float* x, const float* rst
   DISPATCH_NV(d, hipLaunchKernelGGL(rmsnorm_bwd_kernel<NV>, dim3(parts), dim3(256), 0, s, dy, x, rstd, w, dres, dx32,
                                     (bf16_t*)dx16, ws, rows, NORM_BWD_ROWS));
   if (int rc = vqa::check_launch("vqa_rmsnorm_bwd")) return rc;
-  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 256)), dim3(256), 0, s, ws, parts, (long)d, d, dw,
+  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 64)), dim3(1024), 0, s, ws, parts, (long)d, d, dw,
                      dw_beta);
   return vqa::check_launch("vqa_rmsnorm_bwd/colsum");
 }
@@ -283,9 +296,9 @@ extern "C" int vqa_layernorm_bwd(const float* dy, const float* x, const float* m
   DISPATCH_NV(d, hipLaunchKernelGGL(layernorm_bwd_kernel<NV>, dim3(parts), dim3(256), 0, s, dy, x, mean, rstd, gamma,
                                     dres, dx32, (bf16_t*)dx16, ws, rows, NORM_BWD_ROWS));
   if (int rc = vqa::check_launch("vqa_layernorm_bwd")) return rc;
-  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 256)), dim3(256), 0, s, ws, parts, (long)2 * d, d,
+  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 64)), dim3(1024), 0, s, ws, parts, (long)2 * d, d,
                      dgamma, 0.f);
-  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 256)), dim3(256), 0, s, ws + d, parts, (long)2 * d, d,
+  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 64)), dim3(1024), 0, s, ws + d, parts, (long)2 * d, d,
                      dbeta, 0.f);
   return vqa::check_launch("vqa_layernorm_bwd/colsum");
 }
@@ -293,7 +306,7 @@ extern "C" int vqa_layernorm_bwd(const float* dy, const float* x, const float* m
 extern "C" int vqa_colsum_partials(const float* ws, int parts, long long stride, int cols, float* out, float beta,
                                    hipStream_t s) {
   VQA_REQUIRE(ws && out && parts > 0 && cols > 0, "vqa_colsum_partials: bad arguments");
-  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(cols, 256)), dim3(256), 0, s, ws, parts, (long)stride, cols,
+  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(cols, 64)), dim3(1024), 0, s, ws, parts, (long)stride, cols,
                      out, beta);
   return vqa::check_launch("vqa_colsum_partials");
 }

@@ -238,6 +238,8 @@ class VQAEngine:
         self.dH32, self.dH16 = t((T, D)), t((T, D), BF16)
         self.dHM32, self.dHM16 = t((T, D)), t((T, D), BF16)
         self.dPB = t((S.T5_HEADS, Lq, Lq), zero=True)
+        self.dSB = t((B, S.T5_HEADS, Lq, Lq))             # per-sample attention dS (rel-bias grad)
+        self.WS_EMB = t(2 * T, torch.int32)
         lib = L.load()
         self.WS_NORM = t(lib.vqa_norm_bwd_workspace_floats(T, D))
         self.WS_COL = t(lib.vqa_colsum_workspace_floats(mx, 3 * D))
@@ -343,9 +345,9 @@ class VQAEngine:
     def _plan_backward(self):
         b = self.bwd_calls
         B, Lq, T, NB = self.B, self.L, self.T, self.NB
-        # gradients that accumulate: embedding rows, relative bias
-        for z in (self.g32["t5.embed"], self.g32["t5.relbias"], self.dPB):
-            self._call(self.zero_calls, "vqa_zero", z, z.numel() * 4)
+        # the dense embedding gradient only gets the touched rows written
+        z = self.g32["t5.embed"]
+        self._call(self.zero_calls, "vqa_zero", z, z.numel() * 4)
         b += self.zero_calls
         # head: log_softmax + NLL + classifier + attention pooler
         last = self.sga[-1]["OUT"]
@@ -418,13 +420,17 @@ class VQAEngine:
             self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B, heads=S.T5_HEADS, lq=Lq,
                        lk=Lq, dh=S.T5_DKV, scale=1.0, dout=self.dO16, lddo=D, dq=dq, lddq=3 * D,
-                       dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dPB)
+                       dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dSB)
+            # relative-position bias is shared by all 12 layers: dPB = sum_layers sum_b dS
+            self._call(b, "vqa_batch_sum", self.dSB, B, S.T5_HEADS * Lq * Lq, self.dPB,
+                       0.0 if i == S.T5_LAYERS - 1 else 1.0)
             self._dw(b, dq, self.N0[i], f"t5.{i}.qkv_w", T)
             self._dx(b, dq, f"t5.{i}.qkv_w", T, out32=self.dC32)
             self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HS[i], self.R0[i], self.p32[f"t5.{i}.ln0"], self.dHM32,
                        self.dH32, self.dH16, self.g32[f"t5.{i}.ln0"], 0.0, self.WS_NORM, T, D)
-        self._call(b, "vqa_embedding_bwd", self.IDS, self.dH32, self.g32["t5.embed"], T, D, S.T5_VOCAB)
-        self._call(b, "vqa_t5_relbias_bwd", self.dPB, self.bucket, self.g32["t5.relbias"], S.T5_HEADS, Lq, Lq)
+        self._call(b, "vqa_embedding_bwd", self.IDS, self.dH32, self.g32["t5.embed"], T, D, S.T5_VOCAB, self.WS_EMB)
+        self._call(b, "vqa_t5_relbias_bwd", self.dPB, self.bucket, self.g32["t5.relbias"], S.T5_HEADS, Lq, Lq,
+                   S.T5_BUCKETS)
 
     # ------------------------------------------------------------------ optimizer plan
     def _plan_optimizer(self):

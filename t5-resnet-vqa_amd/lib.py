@@ -39,7 +39,7 @@ class GemmDesc(ctypes.Structure):
         ("a_conv", c_int), ("ga", ConvGeom),
         ("b_conv", c_int), ("gb", ConvGeom),
         ("batch", c_int), ("stride_a", c_ll), ("stride_b", c_ll), ("stride_c32", c_ll),
-        ("stride_c16", c_ll), ("stride_res", c_ll),
+        ("stride_c16", c_ll), ("stride_res", c_ll), ("config", c_int),
     ]
 
 
@@ -120,9 +120,10 @@ register("vqa_image_to_nhwc8", P, P, c_int, c_int, c_int)
 register("vqa_maxpool3x3s2_nhwc", P, P, c_int, c_int, c_int, c_int, c_int, c_int)
 register("vqa_colsum", P, c_int, c_int, c_int, c_ll, P, c_float, P)
 register("vqa_embedding_fwd", P, P, P, c_int, c_int, c_int)
-register("vqa_embedding_bwd", P, P, P, c_int, c_int, c_int)
+register("vqa_embedding_bwd", P, P, P, c_int, c_int, c_int, P)
 register("vqa_t5_relbias_fwd", P, P, P, c_int, c_int, c_int)
-register("vqa_t5_relbias_bwd", P, P, P, c_int, c_int, c_int)
+register("vqa_t5_relbias_bwd", P, P, P, c_int, c_int, c_int, c_int)
+register("vqa_batch_sum", P, c_int, c_ll, P, c_float)
 register("vqa_cast_f32_bf16", P, P, c_ll)
 register("vqa_zero", P, c_ll)
 register("vqa_head_fwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)

@@ -28,9 +28,10 @@ def close(got, ref, scale, rtol=2e-5):
     assert err <= rtol * scale + 1e-6, f"max err {err} vs scale {scale}"
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(2048, 2304, 768), (100, 200, 136), (64, 170, 768), (3136, 768, 1024),
                                    (37, 24, 8)])
-def test_linear_forward_epilogue(ops, M, N, K):
+def test_linear_forward_epilogue(ops, M, N, K, cfg):
     x, w = bf((M, K), seed=1), bf((N, K), 0.05, seed=2)
     bias = torch.randn(N, device="cuda")
     res = torch.randn(M, N, device="cuda")
@@ -38,6 +39,7 @@ def test_linear_forward_epilogue(ops, M, N, K):
     out16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     d = ops.gemm_desc(x, w, M, N, K, lda=K, ldb=K, c32=out32, ldc32=N, c16=out16, ldc16=N, bias=bias,
                       res32=res, ldres=N, relu=True)
+    d.config = cfg
     ops.run(d)
     torch.cuda.synchronize()
     ref = torch.relu(x.float() @ w.float().T + bias + res)
@@ -46,22 +48,28 @@ def test_linear_forward_epilogue(ops, M, N, K):
     assert (out16.float() - ref).abs().max().item() <= ref.abs().max().item() * 2 ** -8 + 1e-6
 
 
-@pytest.mark.parametrize("M,N,K", [(2048, 768, 2304), (96, 136, 200), (2048, 768, 3072)])
-def test_input_grad_layout(ops, M, N, K):
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(2048, 768, 2304), (96, 136, 200), (2048, 3072, 768)])
+def test_input_grad_layout(ops, M, N, K, cfg):
     # dX[M, N] = dY[M, K] @ W[K, N]  (W stored [K, N] row-major: B n-contig)
     dy, w = bf((M, K), seed=3), bf((K, N), 0.05, seed=4)
     out = torch.empty(M, N, device="cuda")
-    ops.run(ops.gemm_desc(dy, w, M, N, K, lda=K, ldb=N, b_trans=True, c32=out, ldc32=N))
+    d = ops.gemm_desc(dy, w, M, N, K, lda=K, ldb=N, b_trans=True, c32=out, ldc32=N)
+    d.config = cfg
+    ops.run(d)
     torch.cuda.synchronize()
     close(out, dy.float() @ w.float(), (dy.float().abs() @ w.float().abs()).max().item())
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 @pytest.mark.parametrize("NO,KI,T", [(768, 768, 2048), (2304, 768, 3136), (136, 64, 200), (8, 16, 40)])
-def test_weight_grad_layout(ops, NO, KI, T):
+def test_weight_grad_layout(ops, NO, KI, T, cfg):
     # dW[NO, KI] = dY[T, NO]^T @ X[T, KI]   (A m-contig, B n-contig)
     dy, x = bf((T, NO), seed=5), bf((T, KI), seed=6)
     out = torch.empty(NO, KI, device="cuda")
-    ops.run(ops.gemm_desc(dy, x, NO, KI, T, lda=NO, ldb=KI, a_trans=True, b_trans=True, c32=out, ldc32=KI))
+    d = ops.gemm_desc(dy, x, NO, KI, T, lda=NO, ldb=KI, a_trans=True, b_trans=True, c32=out, ldc32=KI)
+    d.config = cfg
+    ops.run(d)
     torch.cuda.synchronize()
     close(out, dy.float().T @ x.float(), (dy.float().abs().T @ x.float().abs()).max().item())
 
@@ -91,10 +99,11 @@ def test_beta_mask_bf16_residual_batched(ops):
     close(c, v + c0, (a.float().abs() @ b.float().abs().transpose(1, 2)).max().item() + 10)
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 3])
 @pytest.mark.parametrize("n,h,w,c,co,k,s,p", [
     (2, 56, 56, 64, 64, 1, 1, 0), (2, 56, 56, 64, 128, 3, 1, 1), (2, 56, 56, 128, 128, 3, 2, 1),
     (2, 28, 28, 256, 512, 1, 2, 0), (2, 32, 32, 8, 64, 7, 2, 3), (3, 7, 7, 2048, 768, 3, 1, 1)])
-def test_conv_forward_gather(ops, pkg, n, h, w, c, co, k, s, p):
+def test_conv_forward_gather(ops, pkg, n, h, w, c, co, k, s, p, cfg):
     x = bf((n, h, w, c), seed=13).abs()
     wt = bf((co, k, k, c), 0.05, seed=14)                 # [Cout][KH][KW][C]
     oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
@@ -102,7 +111,9 @@ def test_conv_forward_gather(ops, pkg, n, h, w, c, co, k, s, p):
     bias = torch.randn(co, device="cuda")
     out = torch.empty(M, co, device="cuda")
     g = ops.conv_geom(n, h, w, c, oh, ow, k, k, s, p)
-    ops.run(ops.gemm_desc(x, wt, M, co, K, lda=K, ldb=K, c32=out, ldc32=co, bias=bias, relu=True, ga=g))
+    d = ops.gemm_desc(x, wt, M, co, K, lda=K, ldb=K, c32=out, ldc32=co, bias=bias, relu=True, ga=g)
+    d.config = cfg
+    ops.run(d)
     torch.cuda.synchronize()
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), wt.float().permute(0, 3, 1, 2), bias, stride=s, padding=p)
     ref = torch.relu(ref).permute(0, 2, 3, 1).reshape(M, co)
@@ -111,16 +122,19 @@ def test_conv_forward_gather(ops, pkg, n, h, w, c, co, k, s, p):
     close(out, ref, scale)
 
 
+@pytest.mark.parametrize("cfg", [0, 2, 3])
 @pytest.mark.parametrize("n,h,c,co", [(2, 7, 64, 96), (4, 7, 2048, 768)])
-def test_conv_weight_grad_gather(ops, n, h, c, co):
+def test_conv_weight_grad_gather(ops, n, h, c, co, cfg):
     # ConvTranspose2d(k3,s1,p1) dW as the weight-grad of the equivalent conv: B = implicit im2col
     x = bf((n, h, h, c), seed=15)
     dy = bf((n * h * h, co), seed=16)
     K9 = 9 * c
     out = torch.empty(co, K9, device="cuda")
     g = ops.conv_geom(n, h, h, c, h, h, 3, 3, 1, 1)
-    ops.run(ops.gemm_desc(dy, x, co, K9, n * h * h, lda=co, ldb=K9, a_trans=True, b_trans=True, c32=out,
-                          ldc32=K9, gb=g))
+    d = ops.gemm_desc(dy, x, co, K9, n * h * h, lda=co, ldb=K9, a_trans=True, b_trans=True, c32=out,
+                      ldc32=K9, gb=g)
+    d.config = cfg
+    ops.run(d)
     torch.cuda.synchronize()
     cols = F.unfold(x.float().permute(0, 3, 1, 2), 3, padding=1)        # [n, c*9, h*h] (c major)
     cols = cols.view(n, c, 9, h * h).permute(0, 3, 2, 1).reshape(n * h * h, K9)   # [(n,h,w), (tap, c)]

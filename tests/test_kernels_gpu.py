@@ -113,7 +113,7 @@ def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5):
     ref_o.backward(do16.float())
     dq = torch.empty(B * Lq, D, device="cuda", dtype=torch.bfloat16)
     dkv = torch.empty(B * Lk, 2 * D, device="cuda", dtype=torch.bfloat16)
-    dbias = torch.zeros(H, Lq, Lk, device="cuda") if t5 else None
+    dbias = torch.zeros(B, H, Lq, Lk, device="cuda") if t5 else None     # per-sample dS
     d.dout, d.lddo, d.dq, d.lddq = A(do16), D, A(dq), D
     d.dk, d.lddk, d.dv, d.lddv, d.dbias = A(dkv), 2 * D, A(dkv, D), 2 * D, A(dbias)
     L.check(L.load().vqa_attn_bwd(ctypes.byref(d), L.stream_handle()), "bwd")
@@ -127,7 +127,10 @@ def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5):
     chk(dkv[:, :D], kf.grad)
     chk(dkv[:, D:], vf.grad)
     if t5:
-        torch.testing.assert_close(dbias, bf.grad, rtol=1e-3, atol=1e-3)
+        red = torch.full((H, Lq, Lk), 3.0, device="cuda")
+        run(k, "vqa_batch_sum", dbias, B, H * Lq * Lk, red, 1.0)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(red - 3.0, bf.grad, rtol=1e-3, atol=1e-3)
 
 
 def test_head_fwd_bwd(k):
@@ -168,9 +171,13 @@ def test_embedding_relbias_colsum_cast(k):
     torch.testing.assert_close(out, table[ids])
     dh = rnd((T, D), 31)
     dt = torch.zeros(Vv, D, device="cuda")
-    run(k, "vqa_embedding_bwd", ids, dh, dt, T, D, Vv)
+    ws = torch.empty(2 * T, device="cuda", dtype=torch.int32)
+    run(k, "vqa_embedding_bwd", ids, dh, dt, T, D, Vv, ws)
     ref = torch.zeros(Vv, D, device="cuda").index_add_(0, ids, dh)
     torch.testing.assert_close(dt, ref, rtol=1e-5, atol=1e-5)
+    dt2 = torch.zeros(Vv, D, device="cuda")
+    run(k, "vqa_embedding_bwd", ids, dh, dt2, T, D, Vv, ws)
+    assert torch.equal(dt, dt2), "embedding backward must be deterministic"
     Lq = 32
     bucket = torch.from_numpy(k.layout.t5_bucket_map(Lq, Lq)).reshape(-1).cuda()
     tab = rnd((32, 12), 32)
@@ -179,7 +186,7 @@ def test_embedding_relbias_colsum_cast(k):
     torch.testing.assert_close(pb, tab[bucket.long()].T.reshape(12, Lq, Lq))
     dpb = rnd((12, Lq, Lq), 33)
     dtab = torch.zeros(32, 12, device="cuda")
-    run(k, "vqa_t5_relbias_bwd", dpb, bucket, dtab, 12, Lq, Lq)
+    run(k, "vqa_t5_relbias_bwd", dpb, bucket, dtab, 12, Lq, Lq, 32)
     ref = torch.zeros(32, 12, device="cuda").index_add_(0, bucket.long(), dpb.reshape(12, -1).T)
     torch.testing.assert_close(dtab, ref, rtol=1e-5, atol=1e-5)
     for bf in (0, 1):
