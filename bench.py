@@ -91,21 +91,23 @@ def main():
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev,
                                warmup=10, total=100000)
     del sd
-    if world > 1:
-        eng.allreduce = lambda g: dist.all_reduce(g)
-        eng.set_grad_scale(1.0 / world)
     pool = []
     for i in range(4):
         nb = pkg.synthetic.make_batch(B, L, H, seed=1 + rank * 16 + i)
         pool.append({k: torch.as_tensor(v).to(dev) for k, v in nb.items() if v is not None})
     torch.cuda.synchronize()
     eng.load_batch(pool[0])
-    if not args.no_graph:
-        eng.capture()
+    if world > 1:
+        dps = pkg.dp.DataParallelStep(eng, use_graph=not args.no_graph)
+        run_step = dps.step
+    else:
+        if not args.no_graph:
+            eng.capture()
+        run_step = eng.train_step
 
     def step(i):
         eng.load_batch(pool[i % len(pool)])
-        eng.train_step()
+        run_step()
 
     for i in range(args.warmup):
         step(i)
@@ -128,11 +130,15 @@ def main():
     loss = float(eng.LOSS.item())
     gnorm = eng.last_grad_norm()
 
-    # dominant kernel: the ConvTranspose2d weight-gradient implicit GEMM (unique instantiation
-    # gemm_kernel<128,128,false,false,false,true>): M=768, N=9*2048, K=B*49
-    wg_call = next(c for c in eng.bwd_calls if c.name == "vqa_gemm" and c.keep.b_conv == 1)
+    # dominant single launch: the ConvTranspose2d weight-gradient implicit GEMM (its gather-B
+    # instantiation is used by no other call): M=768, N=9*2048, K=B*49, 2*M*N*K FLOP per launch
+    from vqa_amd import lib as VL
+    wg_call = next(c for c in eng.bwd_calls if c.name == "vqa_gemm" and c.desc.b_conv == 1)
+    cfg = VL.load().vqa_gemm_select(wg_call.desc)
+    bm, bn, st = {1: (128, 128, 3), 2: (128, 64, 4), 3: (64, 64, 4), 4: (64, 64, 2)}[cfg]
+    kname = f"gemm_kernel<{bm}, {bn}, {st}, false, false, false, true> (ConvTranspose2d dW implicit GEMM)"
     kdur = time_kernel(wg_call, 20, torch.cuda.current_stream(dev))
-    kflop = 2.0 * wg_call.keep.m * wg_call.keep.n * wg_call.keep.k
+    kflop = 2.0 * wg_call.desc.m * wg_call.desc.n * wg_call.desc.k
     k_tflops = kflop / kdur / 1e12
 
     pairs = world * B * args.steps
@@ -146,7 +152,7 @@ def main():
                    "model": "resnet50+t5-base+3xSGA", "global_batch": world * B, "per_gpu_batch": B,
                    "seq_len": L, "image_size": H, "answers": 170, "parallelism": f"dp{world}",
                    "graph": not args.no_graph},
-        "roofline": {"bound": "mfma", "kernel": "gemm_kernel<128,128,0,0,0,1> (ConvTranspose2d dW implicit GEMM)",
+        "roofline": {"bound": "mfma", "kernel": kname,
                      "achieved": round(k_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(k_tflops / MFMA_PEAK_TFLOPS, 4), "traffic": None,
                      "kernel_avg_us": round(kdur * 1e6, 2), "flop_per_launch": kflop,

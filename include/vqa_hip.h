@@ -69,6 +69,8 @@ typedef struct vqa_gemm_desc {
 } vqa_gemm_desc;
 
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
+/* tile configuration (1..4) that vqa_gemm would run for this descriptor */
+int vqa_gemm_select(const vqa_gemm_desc* d);
 
 /* ------------------------------------------------------------- attention ---
  * Multi-head attention core for Lq, Lk <= 64 (one workgroup per (b, head)):
@@ -142,7 +144,7 @@ int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long long ld, floa
 int vqa_colsum_workspace_floats(int rows, int cols);
 int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int tokens, int d, int vocab,
                       hipStream_t stream);
-/* deterministic: each touched row is written once (fixed token order); ws = 2*tokens ints */
+/* deterministic: each touched row is written once (sorted, fixed token order); tokens <= 8192; ws = 2*tokens ints */
 int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab, int* ws,
                       hipStream_t stream);
 int vqa_t5_relbias_fwd(const float* table, const int* bucket, float* out, int heads, int lq, int lk,

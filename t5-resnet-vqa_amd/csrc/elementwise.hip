@@ -100,40 +100,61 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const long long* __r
   reinterpret_cast<float4*>(out)[i] = reinterpret_cast<const float4*>(table + id * (long)d4 * 4)[j];
 }
 
-// Deterministic dense embedding gradient (nn.Embedding sparse=False): every
-// vocabulary row touched by the batch is written ONCE by its first occurrence
-// ("leader"), summing the occurrences in token order along a next[] chain.
-// No atomics, so the result is bit-identical run to run (DP ranks stay in
-// lockstep, graph replay == eager).  links: [0, T) next index (-1 = end),
-// [T, 2T) leader flag.
-__global__ __launch_bounds__(1024) void embedding_links_kernel(const long long* __restrict__ ids, int tokens,
-                                                               int* __restrict__ links) {
-  extern __shared__ int sid[];
-  for (int t = threadIdx.x; t < tokens; t += blockDim.x) sid[t] = (int)ids[t];
+// Deterministic dense embedding gradient (nn.Embedding sparse=False), no atomics:
+//   1. one workgroup bitonic-sorts the keys (id << 16 | position) in LDS, which
+//      groups equal ids with their positions in token order;
+//   2. one workgroup per sorted slot: the first slot of each id-run sums the
+//      run's dh rows in that fixed order and writes the table row once.
+// Bit-identical run to run (DP ranks stay in lockstep, graph replay == eager).
+// ws: [0, T) sorted positions, [T, 2T) sorted ids (clamped).
+__global__ __launch_bounds__(1024) void embedding_sort_kernel(const long long* __restrict__ ids, int tokens, int vocab,
+                                                              int* __restrict__ ws) {
+  extern __shared__ unsigned long long key[];
+  int n = 1;
+  while (n < tokens) n <<= 1;
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    if (t < tokens) {
+      long long id = ids[t];
+      id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+      key[t] = ((unsigned long long)id << 16) | (unsigned long long)t;
+    } else {
+      key[t] = ~0ull;
+    }
+  }
   __syncthreads();
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int p = i ^ j;
+        if (p > i) {
+          const unsigned long long a = key[i], b = key[p];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) { key[i] = b; key[p] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
   for (int t = threadIdx.x; t < tokens; t += blockDim.x) {
-    const int v = sid[t];
-    int nxt = -1, lead = 1;
-    for (int u = 0; u < t; ++u) lead &= (sid[u] != v);
-    for (int u = t + 1; u < tokens; ++u)
-      if (sid[u] == v) { nxt = u; break; }
-    links[t] = nxt;
-    links[tokens + t] = lead;
+    ws[t] = (int)(key[t] & 0xffff);
+    ws[tokens + t] = (int)(key[t] >> 16);
   }
 }
 
-__global__ __launch_bounds__(256) void embedding_bwd_kernel(const long long* __restrict__ ids,
-                                                            const float* __restrict__ dh, float* __restrict__ dtable,
-                                                            const int* __restrict__ links, int tokens, int d,
-                                                            int vocab) {
-  const int t = blockIdx.x;
-  if (!links[tokens + t]) return;
-  long long id = ids[t];
-  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(const float* __restrict__ dh, float* __restrict__ dtable,
+                                                            const int* __restrict__ ws, int tokens, int d) {
+  const int s0 = blockIdx.x;
+  const int* pos = ws;
+  const int* sid = ws + tokens;
+  const int id = sid[s0];
+  if (s0 > 0 && sid[s0 - 1] == id) return;           // not the first slot of its run
+  int s1 = s0 + 1;
+  while (s1 < tokens && sid[s1] == id) ++s1;
   for (int c = threadIdx.x; c < d; c += 256) {
     float s = 0.f;
-    for (int u = t; u >= 0; u = links[u]) s += dh[(long)u * d + c];
-    dtable[id * (long)d + c] = s;
+#pragma unroll 4
+    for (int u = s0; u < s1; ++u) s += dh[(long)pos[u] * d + c];
+    dtable[(long)id * d + c] = s;
   }
 }
 
@@ -147,27 +168,18 @@ __global__ __launch_bounds__(256) void relbias_fwd_kernel(const float* __restric
   out[i] = table[bucket[p] * heads + h];
 }
 
-// dtable[b, h] = sum over (i, j) with bucket(i, j) == b of dbias[h, i, j], fixed order
+// dtable[b, h] = sum over (i, j) with bucket(i, j) == b of dbias[h, i, j]:
+// one workgroup per (bucket, head), fixed-order block reduction
 __global__ __launch_bounds__(256) void relbias_bwd_kernel(const float* __restrict__ dbias,
                                                           const int* __restrict__ bucket, float* __restrict__ dtable,
-                                                          int heads, int lqk, int nbuckets) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= heads * nbuckets) return;
-  const int bk = i / heads, h = i - bk * heads;
+                                                          int heads, int lqk) {
+  __shared__ float red[4];
+  const int bk = blockIdx.x / heads, h = blockIdx.x - bk * heads;
   float s = 0.f;
-  for (int p = 0; p < lqk; ++p)
+  for (int p = threadIdx.x; p < lqk; p += 256)
     if (bucket[p] == bk) s += dbias[(long)h * lqk + p];
-  dtable[bk * heads + h] = s;
-}
-
-// out[i] = beta*out[i] + sum_b x[b*n + i]   (fixed order)
-__global__ __launch_bounds__(256) void batch_sum_kernel(const float* __restrict__ x, int batch, long n,
-                                                        float* __restrict__ out, float beta) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  float s = 0.f;
-  for (int b = 0; b < batch; ++b) s += x[(long)b * n + i];
-  out[i] = beta != 0.f ? beta * out[i] + s : s;
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) dtable[bk * heads + h] = s;
 }
 
 __global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
@@ -233,17 +245,21 @@ extern "C" int vqa_embedding_fwd(const long long* ids, const float* table, float
 
 extern "C" int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab,
                                  int* ws, hipStream_t s) {
-  VQA_REQUIRE(ids && dh && dtable && ws && tokens > 0 && tokens <= 16384, "vqa_embedding_bwd: bad arguments");
-  hipLaunchKernelGGL(embedding_links_kernel, dim3(1), dim3(1024), tokens * sizeof(int), s, ids, tokens, ws);
-  if (int rc = vqa::check_launch("vqa_embedding_bwd/links")) return rc;
-  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(tokens), dim3(256), 0, s, ids, dh, dtable, ws, tokens, d, vocab);
+  // keys hold the position in 16 bits and the padded sort buffer lives in LDS (<= 64 KiB)
+  VQA_REQUIRE(ids && dh && dtable && ws && tokens > 0 && tokens <= 8192, "vqa_embedding_bwd: bad arguments");
+  int n = 1;
+  while (n < tokens) n <<= 1;
+  hipLaunchKernelGGL(embedding_sort_kernel, dim3(1), dim3(1024), n * sizeof(unsigned long long), s, ids, tokens, vocab,
+                     ws);
+  if (int rc = vqa::check_launch("vqa_embedding_bwd/sort")) return rc;
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(tokens), dim3(256), 0, s, dh, dtable, ws, tokens, d);
   return vqa::check_launch("vqa_embedding_bwd");
 }
 
+// a batch-sum is a column sum over `batch` partial rows
 extern "C" int vqa_batch_sum(const float* x, int batch, long long n, float* out, float beta, hipStream_t s) {
-  VQA_REQUIRE(x && out && batch > 0 && n > 0, "vqa_batch_sum: bad arguments");
-  hipLaunchKernelGGL(batch_sum_kernel, dim3(vqa::cdiv(n, 256)), dim3(256), 0, s, x, batch, (long)n, out, beta);
-  return vqa::check_launch("vqa_batch_sum");
+  VQA_REQUIRE(x && out && batch > 0 && n > 0 && n < (1ll << 31), "vqa_batch_sum: bad arguments");
+  return vqa_colsum_partials(x, batch, n, (int)n, out, beta, s);
 }
 
 extern "C" int vqa_t5_relbias_fwd(const float* table, const int* bucket, float* out, int heads, int lq, int lk,
@@ -257,8 +273,8 @@ extern "C" int vqa_t5_relbias_fwd(const float* table, const int* bucket, float* 
 extern "C" int vqa_t5_relbias_bwd(const float* dbias, const int* bucket, float* dtable, int heads, int lq, int lk,
                                   int nbuckets, hipStream_t s) {
   VQA_REQUIRE(dbias && bucket && dtable, "vqa_t5_relbias_bwd: bad arguments");
-  hipLaunchKernelGGL(relbias_bwd_kernel, dim3(vqa::cdiv(heads * nbuckets, 256)), dim3(256), 0, s, dbias, bucket,
-                     dtable, heads, lq * lk, nbuckets);
+  hipLaunchKernelGGL(relbias_bwd_kernel, dim3(heads * nbuckets), dim3(256), 0, s, dbias, bucket, dtable, heads,
+                     lq * lk);
   return vqa::check_launch("vqa_t5_relbias_bwd");
 }
 

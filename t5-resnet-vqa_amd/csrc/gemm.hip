@@ -453,15 +453,17 @@ int launch(GemmParams& P, int batch, hipStream_t s) {
 // everywhere at this model's sizes; 128x128 only pays for narrow-N, long-K
 // convolutions (half the operand re-reads); with <= 2 K-tiles the ring is
 // useless and a 2-stage ring doubles the resident blocks.
+int auto_config(int m, int n, int k, int batch) {
+  const long t128 = (long)vqa::cdiv(m, 128) * vqa::cdiv(n, 128) * batch;
+  const int nk = vqa::cdiv(k, BK);
+  if (nk <= 2) return 4;
+  if (n <= 256 && k >= 1024 && t128 >= 128) return 1;
+  return 3;
+}
+
 template <bool AKC, bool BKC, bool GA, bool GB>
 int dispatch_tile(GemmParams& P, int batch, int config, hipStream_t s) {
-  if (config == 0) {
-    const long t128 = (long)vqa::cdiv(P.m, 128) * vqa::cdiv(P.n, 128) * batch;
-    const int nk = vqa::cdiv(P.k, BK);
-    if (nk <= 2) config = 4;
-    else if (P.n <= 256 && P.k >= 1024 && t128 >= 128) config = 1;
-    else config = 3;
-  }
+  if (config == 0) config = auto_config(P.m, P.n, P.k, batch);
   switch (config) {
     case 1: return launch<128, 128, 3, AKC, BKC, GA, GB>(P, batch, s);
     case 2: return launch<128, 64, 4, AKC, BKC, GA, GB>(P, batch, s);
@@ -473,6 +475,11 @@ int dispatch_tile(GemmParams& P, int batch, int config, hipStream_t s) {
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
+
+extern "C" int vqa_gemm_select(const vqa_gemm_desc* d) {
+  if (!d) return 0;
+  return d->config ? d->config : auto_config(d->m, d->n, d->k, d->batch);
+}
 
 extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   VQA_REQUIRE(d != nullptr, "vqa_gemm: null descriptor");

@@ -29,9 +29,15 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g
 
 __global__ void finalize_kernel(const double* __restrict__ ws, int parts, float grad_scale, float max_norm,
                                 int warmup, int total, float beta1, float beta2, float* __restrict__ st) {
+  // fixed-order two-level sum of the partials by one workgroup
+  __shared__ double red[256];
+  double part = 0.0;
+  for (int i = threadIdx.x; i < parts; i += 256) part += ws[i];
+  red[threadIdx.x] = part;
+  __syncthreads();
   if (threadIdx.x != 0) return;
   double ss = 0.0;
-  for (int i = 0; i < parts; ++i) ss += ws[i];
+  for (int i = 0; i < 256; ++i) ss += red[i];
   const float norm = (float)(sqrt(ss) * (double)grad_scale);
   float coef = 1.f;
   if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
@@ -112,7 +118,7 @@ extern "C" int vqa_grad_sqnorm(const float* g, long long n, double* ws, int part
 extern "C" int vqa_optim_finalize(const double* ws, int parts, float grad_scale, float max_norm, int warmup, int total,
                                   float beta1, float beta2, float* state, hipStream_t s) {
   VQA_REQUIRE(ws && state && parts > 0, "vqa_optim_finalize: bad arguments");
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, ws, parts, grad_scale, max_norm, warmup, total, beta1,
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, ws, parts, grad_scale, max_norm, warmup, total, beta1,
                      beta2, state);
   return vqa::check_launch("vqa_optim_finalize");
 }

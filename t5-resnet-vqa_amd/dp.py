@@ -1,0 +1,146 @@
+"""Data-parallel training step: one process per MI355X, gradients exchanged
+with RCCL (torch.distributed backend "nccl") over xGMI, overlapped with the
+backward pass.  (The reference trains on one device only,
+trainer/faster_rcnn_vqa_trainer.py:61-62; this is the build's added strategy,
+SURVEY.md §8e.)
+
+Step on every rank (identical initial weights, rank-local batch):
+  graph(forward) -> for each backward segment: graph(segment) ; async
+  all-reduce(SUM) of the gradient bucket that segment finalised  ->
+  all-gather of (token id, dH row) pairs -> deterministic embedding scatter ->
+  wait for the buckets -> graph(clip + AdamW), grads scaled by 1/world.
+
+Buckets: the flat gradient arena is laid out in backward-completion order
+(layout.py), so each finished bucket is a contiguous slice [a, b) of G32 and
+RCCL works in place on it.  The dense 98.7 MB T5 embedding gradient is never
+all-reduced: each rank ships only its <= B*L touched (id, row) pairs and every
+rank rebuilds the identical summed rows with the sorted fixed-order scatter.
+Because every exchange and kernel is deterministic, all ranks hold bit-identical
+parameters after every step.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import lib as L
+from . import ops
+from . import synthetic as S
+
+
+def plan_buckets(ready_marks, end, min_bytes=24 << 20):
+    """Group the engine's ready marks (call index, prefix end) into buckets of
+    at least `min_bytes` of fp32 gradient.  Returns [(call_index, start, stop)]."""
+    out, start = [], 0
+    for i, (ci, stop) in enumerate(ready_marks):
+        stop = min(stop, end)
+        last = i == len(ready_marks) - 1
+        if stop - start >= min_bytes // 4 or (last and stop > start):
+            out.append((ci, start, stop))
+            start = stop
+    return out
+
+
+def allreduce_buckets(flat, buckets, group=None):
+    """Launch one async SUM all-reduce per bucket slice of `flat`; returns works."""
+    import torch.distributed as dist
+    return [dist.all_reduce(flat[a:b], group=group, async_op=True) for _, a, b in buckets]
+
+
+def gather_rows(ids, rows, out_ids, out_rows, group=None):
+    """All-gather the rank-local (token id, gradient row) pairs (rank-major order)."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo":                  # CPU tests: list form
+        w = dist.get_world_size(group)
+        w1 = dist.all_gather(list(out_ids.chunk(w)), ids.reshape(-1), group=group, async_op=True)
+        w2 = dist.all_gather(list(out_rows.chunk(w)), rows, group=group, async_op=True)
+        return [w1, w2]
+    w1 = dist.all_gather_into_tensor(out_ids, ids.reshape(-1), group=group, async_op=True)
+    w2 = dist.all_gather_into_tensor(out_rows, rows, group=group, async_op=True)
+    return [w1, w2]
+
+
+class DataParallelStep:
+    def __init__(self, engine, group=None, bucket_mb=24, use_graph=True):
+        import torch.distributed as dist
+        self.eng, self.group = engine, group
+        self.world = dist.get_world_size(group)
+        e = engine
+        e.set_grad_scale(1.0 / self.world)
+        emb = e.lay["t5.embed"]
+        self.buckets = plan_buckets(e.ready_marks, emb.offset, bucket_mb << 20)
+        calls = e.bwd_calls[:-1]                            # all but the local embedding scatter
+        assert e.bwd_calls[-1] is e.emb_call
+        self.segments, prev = [], 0
+        for ci, _, _ in self.buckets:
+            self.segments.append(calls[prev:ci])
+            prev = ci
+        self.tail = calls[prev:]                            # nothing should remain after the last mark
+        T, D = e.T, S.D_MODEL
+        dev = e.dev
+        self.GIDS = torch.zeros(self.world * T, dtype=torch.int64, device=dev)
+        self.GDH = torch.zeros(self.world * T, D, dtype=torch.float32, device=dev)
+        self.WS = torch.empty(2 * self.world * T, dtype=torch.int32, device=dev)
+        self.emb_call = ops.Call("vqa_embedding_bwd", self.GIDS.data_ptr(), self.GDH.data_ptr(),
+                                 e.g32["t5.embed"].data_ptr(), self.world * T, D, S.T5_VOCAB, self.WS.data_ptr(),
+                                 keep=(self.GIDS, self.GDH, self.WS, e.g32["t5.embed"]))
+        self.graphs = None
+        if use_graph:
+            self.capture()
+
+    def _run(self, calls):
+        s = L.stream_handle()
+        for c in calls:
+            c(s)
+
+    def capture(self):
+        e = self.eng
+        s = torch.cuda.Stream(e.dev)
+        s.wait_stream(torch.cuda.current_stream(e.dev))
+        with torch.cuda.stream(s):                          # warm-up outside capture
+            e.forward()
+            e.backward()
+        torch.cuda.current_stream(e.dev).wait_stream(s)
+        torch.cuda.synchronize(e.dev)
+        gs = {}
+
+        def cap(name, calls):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self._run(calls)
+            gs.setdefault(name, []).append(g)
+        cap("fwd", e.fwd_calls)
+        for seg in self.segments:
+            cap("seg", seg)
+        cap("tail", self.tail + [self.emb_call])
+        cap("opt", e.opt_calls)
+        self.graphs = gs
+
+    def step(self):
+        e = self.eng
+        if self.graphs is None:
+            e.forward()
+            works = []
+            for seg, bk in zip(self.segments, self.buckets):
+                self._run(seg)
+                works += allreduce_buckets(e.G32, [bk], self.group)
+            works += gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
+            for w in works[-2:]:
+                w.wait()
+            self._run(self.tail + [self.emb_call])
+            for w in works[:-2]:
+                w.wait()
+            self._run(e.opt_calls)
+            return
+        g = self.graphs
+        g["fwd"][0].replay()
+        works = []
+        for seg, bk in zip(g["seg"], self.buckets):
+            seg.replay()
+            works += allreduce_buckets(e.G32, [bk], self.group)
+        works += gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
+        for w in works[-2:]:
+            w.wait()
+        g["tail"][0].replay()
+        for w in works[:-2]:
+            w.wait()
+        g["opt"][0].replay()

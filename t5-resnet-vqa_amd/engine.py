@@ -133,6 +133,7 @@ class VQAEngine:
         self.IMG = self._t((B, 3, H, H))
         self.IMG8 = self._t((B, H, H, 8), BF16)
         bufs = [self._t(maxel, BF16) for _ in range(5)]
+        self.res_bufs = bufs
         self.F4 = self._t((B, hh, hh, cin), BF16)
 
         # stem: conv7x7/2 + BN + ReLU, then maxpool 3x3/2
@@ -248,17 +249,24 @@ class VQAEngine:
         self.WS_SQ = t(self.SQ_PARTS, torch.float64)
 
     # ------------------------------------------------------------------ call helpers
+    # Every helper records the tensors it bakes into a call (ops.Call.keep), so no
+    # buffer can be freed while a prepared call still points at it.  Raw int
+    # addresses (sub-views made with ops.addr) must come from tensors that are
+    # passed too or are engine attributes.
     def _gemm(self, lst, a, b, m, n, k, **kw):
-        lst.append(ops.gemm_call(ops.gemm_desc(a, b, m, n, k, **kw)))
+        ts = [a, b] + [v for v in kw.values() if isinstance(v, torch.Tensor)]
+        lst.append(ops.gemm_call(ops.gemm_desc(a, b, m, n, k, **kw), [t for t in ts if isinstance(t, torch.Tensor)]))
 
     def _call(self, lst, name, *args):
-        lst.append(ops.Call(name, *[ops.addr(a) if isinstance(a, torch.Tensor) else a for a in args]))
+        ts = tuple(a for a in args if isinstance(a, torch.Tensor))
+        lst.append(ops.Call(name, *[ops.addr(a) if isinstance(a, torch.Tensor) else a for a in args], keep=ts))
 
     def _attn(self, lst, fn, **kw):
         d = L.AttnDesc()
         for k, v in kw.items():
             setattr(d, k, ops.addr(v) if isinstance(v, torch.Tensor) else v)
-        lst.append(ops.Call(fn, ctypes.byref(d), keep=d))
+        ts = tuple(v for v in kw.values() if isinstance(v, torch.Tensor))
+        lst.append(ops.Call(fn, ctypes.byref(d), keep=ts, desc=d))
 
     def _linear(self, lst, x16, wname, m, out32=None, out16=None, bias=True, relu=False, res32=None):
         w = self.p16[wname]
@@ -354,6 +362,15 @@ class VQAEngine:
         self._call(b, "vqa_head_bwd", last, self.ATT, self.POOLED, self.LOGP, self.TGT, self.p32["pool_w"],
                    self.p32["cls_w"], self.dY[(NB - 1) & 1], None, self.g32["pool_w"], self.g32["pool_b"],
                    self.g32["cls_w"], self.g32["cls_b"], self.WS_HEAD, B, Lq, D, self.A)
+        # ready marks: (number of backward calls issued, end of the gradient prefix now final).
+        # The flat layout is in backward-completion order, so finished gradients always form
+        # a prefix of G32: DP all-reduces bucket [prev_end, end) as soon as it is final.
+        self.ready_marks = []
+
+        def mark(seg):
+            sg = self.lay[seg]
+            self.ready_marks.append((len(b), sg.offset + (sg.numel + 63) // 64 * 64))
+        mark("pool_b")
         sc = 1.0 / math.sqrt(S.SGA_DHEAD)
         for n in reversed(range(NB)):
             s, p = self.sga[n], f"sga{n}."
@@ -397,15 +414,18 @@ class VQAEngine:
             self._dw(b, dq, self.TXT16, p + "qkv1_w", T, bias_from=dq)
             # text gradient accumulates over the three blocks (x is the T5 output for every block)
             self._dx(b, dq, p + "qkv1_w", T, out32=self.dTXT, res32=self.dA32, beta=0.0 if n == NB - 1 else 1.0)
+            mark(f"sga{n}.ln3_b")
         # ConvTranspose2d scaler weight/bias gradient: implicit im2col of layer4 as the B operand
         cin, fh = self.fc, self.fh
         g = ops.conv_geom(B, fh, fh, cin, fh, fh, 3, 3, 1, 1)
         self._gemm(b, self.dVIS16, self.F4, D, 9 * cin, self.V_TOK, lda=D, ldb=9 * cin, a_trans=True, b_trans=True,
                    c32=self.g32["scaler_w"], ldc32=9 * cin, gb=g)
         self._call(b, "vqa_colsum", self.dVIS32, 0, self.V_TOK, D, D, self.g32["scaler_b"], 0.0, self.WS_COL)
+        mark("scaler_b")
         # T5 encoder backward
         self._call(b, "vqa_rmsnorm_bwd", self.dTXT, self.HS[-1], self.RF, self.p32["t5.final_ln"], None, self.dH32,
                    self.dH16, self.g32["t5.final_ln"], 0.0, self.WS_NORM, T, D)
+        mark("t5.final_ln")
         for i in reversed(range(S.T5_LAYERS)):
             self._dw(b, self.dH16, self.FF[i], f"t5.{i}.wo", T)
             self._dx(b, self.dH16, f"t5.{i}.wo", T, out16=self.dF16, mask16=self.FF[i])
@@ -428,9 +448,13 @@ class VQAEngine:
             self._dx(b, dq, f"t5.{i}.qkv_w", T, out32=self.dC32)
             self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HS[i], self.R0[i], self.p32[f"t5.{i}.ln0"], self.dHM32,
                        self.dH32, self.dH16, self.g32[f"t5.{i}.ln0"], 0.0, self.WS_NORM, T, D)
-        self._call(b, "vqa_embedding_bwd", self.IDS, self.dH32, self.g32["t5.embed"], T, D, S.T5_VOCAB, self.WS_EMB)
+            mark(f"t5.{i}.ln1")
         self._call(b, "vqa_t5_relbias_bwd", self.dPB, self.bucket, self.g32["t5.relbias"], S.T5_HEADS, Lq, Lq,
                    S.T5_BUCKETS)
+        mark("t5.relbias")
+        # embedding rows last (DP replaces this call by an all-gather of (id, dH row) pairs)
+        self._call(b, "vqa_embedding_bwd", self.IDS, self.dH32, self.g32["t5.embed"], T, D, S.T5_VOCAB, self.WS_EMB)
+        self.emb_call = b[-1]
 
     # ------------------------------------------------------------------ optimizer plan
     def _plan_optimizer(self):
@@ -452,7 +476,8 @@ class VQAEngine:
         d.grad_scale = self.grad_scale
         d.state = self.opt_state.data_ptr()
         self._adam_desc = d
-        o.append(ops.Call("vqa_adamw_amsgrad", ctypes.byref(d), keep=d))
+        o.append(ops.Call("vqa_adamw_amsgrad", ctypes.byref(d), desc=d,
+                          keep=(self.P32, self.G32, self.M, self.V, self.VMAX, self.P16, self.opt_state)))
 
     def set_grad_scale(self, s):
         """DP: grads are summed over ranks; the average enters as a scale."""

@@ -89,6 +89,7 @@ def load():
         raise RuntimeError(f"libvqa_hip.so lacks exported symbols {missing}")
     lib.vqa_last_error.restype = ctypes.c_char_p
     lib.vqa_gemm.argtypes = [ctypes.POINTER(GemmDesc), c_void_p]
+    lib.vqa_gemm_select.argtypes = [ctypes.POINTER(GemmDesc)]
     lib.vqa_attn_fwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_attn_bwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_adamw_amsgrad.argtypes = [ctypes.POINTER(AdamWDesc), c_void_p]

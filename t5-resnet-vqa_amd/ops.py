@@ -59,15 +59,20 @@ def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None
 
 
 class Call:
-    """A prepared library call: fixed argument list, replayed on a stream."""
-    __slots__ = ("fn", "args", "name", "keep")
+    """A prepared library call: fixed argument list, replayed on a stream.
 
-    def __init__(self, name, *args, keep=None):
+    `keep` must reference every tensor whose device address is baked into
+    `args`: the call only stores raw addresses, and a tensor freed behind its
+    back would hand its memory to the next allocation (use-after-free)."""
+    __slots__ = ("fn", "args", "name", "keep", "desc")
+
+    def __init__(self, name, *args, keep=None, desc=None):
         lib = L.load()
         self.name = name
         self.fn = getattr(lib, name)
         self.args = args
-        self.keep = keep            # keeps ctypes structures alive
+        self.keep = keep            # tensors (and structures) that must outlive the call
+        self.desc = desc            # ctypes descriptor passed by reference, if any
 
     def __call__(self, stream_ptr):
         rc = self.fn(*self.args, stream_ptr)
@@ -75,8 +80,8 @@ class Call:
             L.check(rc, self.name)
 
 
-def gemm_call(desc):
-    return Call("vqa_gemm", ctypes.byref(desc), keep=desc)
+def gemm_call(desc, tensors=()):
+    return Call("vqa_gemm", ctypes.byref(desc), keep=tuple(tensors), desc=desc)
 
 
 def run(call_or_desc, stream=None):

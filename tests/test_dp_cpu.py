@@ -1,0 +1,120 @@
+"""Data-parallel logic on CPU with the gloo backend, world_size 2 (the GPU path
+uses the same functions over RCCL).  Covers: bucket planning over the flat
+gradient arena, bucketed all-reduce == full all-reduce, the rank-major
+(id, row) all-gather that replaces the dense embedding all-reduce, and the DP
+semantics themselves (mean-NLL per rank + gradient average == global-batch
+gradient) on the CPU oracle."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from __graft_entry__ import load_package
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _spawn(fn, world, *args):
+    port = _port()
+    mp.spawn(fn, args=(world, port) + args, nprocs=world, join=True)
+
+
+def test_plan_buckets_cover_prefix(pkg):
+    lay = pkg.layout.ParamLayout("resnet50")
+    emb = lay["t5.embed"].offset
+    # marks as the engine emits them: head, 3 SGA blocks, scaler, final LN, 12 layers, relbias
+    names = ["pool_b"] + [f"sga{n}.ln3_b" for n in (2, 1, 0)] + ["scaler_b", "t5.final_ln"] + \
+        [f"t5.{i}.ln1" for i in reversed(range(12))] + ["t5.relbias"]
+    marks = [(10 * (i + 1), lay[n].offset + (lay[n].numel + 63) // 64 * 64) for i, n in enumerate(names)]
+    bks = pkg.dp.plan_buckets(marks, emb, 24 << 20)
+    assert bks[0][1] == 0 and bks[-1][2] == emb
+    for (c0, a0, b0), (c1, a1, b1) in zip(bks, bks[1:]):
+        assert b0 == a1 and c0 < c1
+    assert all(b - a >= (24 << 20) // 4 for _, a, b in bks[:-1])
+    assert sum(b - a for _, a, b in bks) == emb
+
+
+def _allreduce_worker(rank, world, port, pkg_dir):
+    _init(rank, world, port)
+    from __graft_entry__ import load_package
+    dp = load_package().dp
+    g = torch.Generator().manual_seed(rank)
+    flat = torch.randn(1000, generator=g)
+    ref = flat.clone()
+    dist.all_reduce(ref)
+    bks = [(1, 0, 128), (2, 128, 640), (3, 640, 1000)]
+    for w in dp.allreduce_buckets(flat, bks):
+        w.wait()
+    assert torch.equal(flat, ref)
+    T, D = 6, 4
+    ids = torch.tensor([5, 7, 5, 0, 0, 9]) + rank
+    rows = torch.arange(T * D, dtype=torch.float32).reshape(T, D) + 100 * rank
+    gi, gr = torch.zeros(world * T, dtype=torch.int64), torch.zeros(world * T, D)
+    for w in dp.gather_rows(ids, rows, gi, gr):
+        w.wait()
+    for r in range(world):
+        assert torch.equal(gi[r * T:(r + 1) * T], torch.tensor([5, 7, 5, 0, 0, 9]) + r)
+        assert torch.equal(gr[r * T:(r + 1) * T], torch.arange(T * D, dtype=torch.float32).reshape(T, D) + 100 * r)
+    # gathered scatter == all-reduce of the per-rank dense scatters (what the reference computes)
+    dense = torch.zeros(20, D).index_add_(0, ids, rows)
+    dist.all_reduce(dense)
+    assert torch.equal(torch.zeros(20, D).index_add_(0, gi, gr), dense)
+    dist.destroy_process_group()
+
+
+def test_allreduce_and_gather_gloo():
+    _spawn(_allreduce_worker, 2, "")
+
+
+def _semantics_worker(rank, world, port, tmp):
+    _init(rank, world, port)
+    from __graft_entry__ import load_package
+    from oracle import vqa_oracle as orc
+    torch.set_num_threads(2)
+    pkg = load_package()
+    B, L, H = 4, 16, 64
+    sd = pkg.synthetic.make_state_dict("resnet34", seed=0)
+    nb = pkg.synthetic.make_batch(B, L, H, seed=1)
+    half = {k: (None if v is None else v[rank * B // 2:(rank + 1) * B // 2]) for k, v in nb.items()}
+    tr = orc.OracleTrainer(sd, "resnet34")
+    tr.forward_backward(orc.to_torch_batch(half))
+    grads = torch.cat([tr.sd[k].grad.reshape(-1) for k in tr.keys])
+    dist.all_reduce(grads)
+    grads /= world
+    if rank == 0:
+        np.save(os.path.join(tmp, "dp_grads.npy"), grads.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_dp_gradient_average_equals_global_batch(tmp_path):
+    """Mean-NLL per rank + all-reduce average == the reference's single-device
+    gradient of the global batch (faster_rcnn_vqa_trainer.py:391-406)."""
+    from oracle import vqa_oracle as orc
+    _spawn(_semantics_worker, 2, str(tmp_path))
+    pkg = load_package()
+    B, L, H = 4, 16, 64
+    sd = pkg.synthetic.make_state_dict("resnet34", seed=0)
+    nb = pkg.synthetic.make_batch(B, L, H, seed=1)
+    tr = orc.OracleTrainer(sd, "resnet34")
+    tr.forward_backward(orc.to_torch_batch(nb))
+    ref = torch.cat([tr.sd[k].grad.reshape(-1) for k in tr.keys]).numpy()
+    got = np.load(tmp_path / "dp_grads.npy")
+    err = np.abs(got - ref).max() / np.abs(ref).max()
+    assert err < 1e-5, err

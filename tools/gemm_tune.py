@@ -19,7 +19,7 @@ for phase, calls in (("fwd", eng.fwd_calls), ("bwd", eng.bwd_calls)):
     for c in calls:
         if c.name != "vqa_gemm":
             continue
-        d = c.keep
+        d = c.desc
         res = {}
         for cfg in (0, 1, 2, 3):
             d.config = cfg
