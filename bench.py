@@ -34,7 +34,7 @@ def cpu_baseline(pkg, batch=8, steps=3, warm=1):
     from oracle import vqa_oracle as orc
     threads = torch.get_num_threads()
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
-    tr = orc.OracleTrainer(sd, "resnet50", warmup=10, total=1000)
+    tr = orc.OracleTrainer(sd, "resnet50", warmup=10, total=1000, dropout=0.1)
     nb = orc.to_torch_batch(pkg.synthetic.make_batch(batch, 32, 224, seed=1))
     times = []
     for i in range(warm + steps):
@@ -44,7 +44,7 @@ def cpu_baseline(pkg, batch=8, steps=3, warm=1):
             times.append(time.perf_counter() - t0)
     t = float(np.median(times))
     return {"value": round(batch / t, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"oracle fp32 train step (zero_grad+fwd+bwd+clip+AdamW amsgrad), R50+T5-base+3xSGA, "
+            "sample": f"oracle fp32 train step (zero_grad+fwd+bwd+clip+AdamW amsgrad, dropout 0.1), R50+T5-base+3xSGA, "
                       f"B={batch}, 224x224, L=32, median of {steps} steps after {warm} warm-up, "
                       f"torch CPU {threads} threads"}
 
@@ -89,7 +89,7 @@ def main():
     B, L, H = args.batch, args.seq_len, args.image_size
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)       # identical init on every rank
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev,
-                               warmup=10, total=100000)
+                               warmup=10, total=100000, dropout=0.1, seed=rank)
     del sd
     pool = []
     for i in range(4):

@@ -23,12 +23,38 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 1
+#define VQA_ABI_VERSION 2
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
 int vqa_abi_version(void);
 const char* vqa_last_error(void);
+
+/* --------------------------------------------------------------- dropout ---
+ * nn.Dropout(p) in training mode at the reference's 12 dropout sites of the
+ * step (T5 encoder: embeddings, attention probabilities, attention/FF residual
+ * branches, FF inner activation, final output -- TF modeling_t5.py:86, 140,
+ * 168, 400, 725, 745; SGA: MHAtt.att probabilities, dropout1..3 and the MLP
+ * inner activation -- multi_head_vision_text_attn.py:84, 99, 146-156).
+ * Masks are counter-based, so the backward regenerates the forward mask and
+ * nothing is stored: element e (the flat row-major index of the tensor the
+ * dropout applies to) of site `site` is kept iff
+ *   mix32(e * 0x9E3779B9 + key) >= (uint32)(p * 2^32)
+ *   key = mix32(k1 ^ (site*0xC2B2AE35 + 0x27D4EB2F)),
+ *   k1  = mix32(k0 ^ (rng[1]*0x85EBCA6B + 0x632BE5AB)), k0 = mix32(rng[0] + 0x9E3779B9),
+ * mix32 = the lowbias32 finaliser; kept values are scaled by 1/(1-p).
+ * rng is a device uint32[2] {seed, counter}; vqa_rng_advance() increments the
+ * counter (once per step, first call of the forward), so a replayed hipGraph
+ * draws fresh masks.  p == 0 or rng == NULL means identity (eval mode). */
+typedef struct vqa_dropout {
+  float p;
+  unsigned site;
+  const unsigned* rng;
+} vqa_dropout;
+
+int vqa_rng_advance(unsigned* rng, hipStream_t stream);
+/* out[e] = keep(e) ? 1/(1-p) : 0 for e < n (tests / debugging) */
+int vqa_dropout_mask(const vqa_dropout* d, float* out, long long n, hipStream_t stream);
 
 /* ------------------------------------------------------------------ GEMM ---
  * C[m,n] = epilogue( alpha * sum_k A(m,k) * B(k,n) ), bf16 operands, fp32 MFMA
@@ -43,8 +69,10 @@ const char* vqa_last_error(void);
  *   (m = output pixel (img,oh,ow), k = (kh,kw,c)); requires a_trans = 0.
  * b_conv: B(k,n) is the implicit im2col with k = output pixel, n = (kh,kw,c);
  *   requires b_trans = 1 (weight-gradient of a convolution).
- * Epilogue order: v = alpha*acc; +bias[n]; +res(m,n); relu; *(mask(m,n) > 0);
+ * Epilogue: k = [mask(m,n) > 0] * dropout multiplier of element (z*m+row)*n+col
+ *   (1 when neither is given); v = k*(alpha*acc + bias[n]) + res(m,n); relu;
  *   c32 = v + beta*c32 (c32 may be NULL); c16 = bf16(v) (may be NULL).
+ *   With res, relu acts after the residual (ResNet); relu with dropout needs no res.
  * batch > 1 offsets a, b, c32, c16 by their strides and res/mask by stride_res. */
 typedef struct vqa_conv_geom {
   int n, h, w, c;          /* NHWC input */
@@ -66,6 +94,7 @@ typedef struct vqa_gemm_desc {
   int b_conv; vqa_conv_geom gb;
   int batch; long long stride_a, stride_b, stride_c32, stride_c16, stride_res;
   int config;              /* 0 auto; 1: 128x128 tile; 2: 128x64; 3: 64x64; 4: 64x64 2-stage (tuning) */
+  vqa_dropout drop;        /* dropout of the (alpha*acc + bias) branch, before the residual */
 } vqa_gemm_desc;
 
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
@@ -83,7 +112,9 @@ int vqa_gemm_select(const vqa_gemm_desc* d);
  * read in place from fused projection outputs.  p: saved P [B, H, Lq, Lk].
  * Backward: dS = P (dP - rowsum(P dP)), dQ = scale dS K, dK = scale dS^T Q,
  * dV = P^T dO; when dbias != NULL the per-sample dS is written to
- * dbias[b, h, i, j] (reduce with vqa_batch_sum; no atomics -> deterministic). */
+ * dbias[b, h, i, j] (reduce with vqa_batch_sum; no atomics -> deterministic).
+ * drop: dropout on P (element index ((b*H + h)*Lq + i)*Lk + j): O = drop(P) V;
+ * p keeps the pre-dropout P and the backward regenerates the mask. */
 typedef struct vqa_attn_desc {
   const void* q; long long ldq;
   const void* k; long long ldk;
@@ -99,6 +130,7 @@ typedef struct vqa_attn_desc {
   void* dk; long long lddk;
   void* dv; long long lddv;
   float* dbias;
+  vqa_dropout drop;
 } vqa_attn_desc;
 
 int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t stream);
@@ -110,17 +142,26 @@ int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t stream);
  * LN:  nn.LayerNorm (multi_head_vision_text_attn.py:120-126), post-LN of SGA.
  * Backward adds the residual gradient dres (may be NULL) into dx and reduces
  * the weight gradients deterministically through ws
- * (vqa_norm_bwd_workspace_floats(rows, d) floats). */
+ * (vqa_norm_bwd_workspace_floats(rows, d) floats).
+ * Dropout hooks (NULL = none; element index row*d + col):
+ *   rmsnorm_fwd drop: y = drop(norm(x))            (T5 final dropout, TF :745)
+ *   rmsnorm_bwd drop_dy: the incoming dy is masked (backward of that dropout);
+ *     drop_dx32 / drop_dx16: mask applied to that output only (the residual
+ *     branch gradient of `h + dropout(f(h))`, or the embedding dropout)
+ *   layernorm_bwd drop_dx16: mask on the bf16 output only (SGA dropout1..3);
+ *     dsum (may be NULL) = column sums of that masked branch gradient in fp32,
+ *     i.e. the bias gradient of the Linear feeding the dropout (fused). */
 int vqa_rmsnorm_fwd(const float* x, const float* w, float* y32, void* y16, float* rstd, int rows, int d, float eps,
-                    hipStream_t stream);
+                    const vqa_dropout* drop, hipStream_t stream);
 int vqa_rmsnorm_bwd(const float* dy, const float* x, const float* rstd, const float* w, const float* dres,
                     float* dx32, void* dx16, float* dw, float dw_beta, float* ws, int rows, int d,
+                    const vqa_dropout* drop_dy, const vqa_dropout* drop_dx32, const vqa_dropout* drop_dx16,
                     hipStream_t stream);
 int vqa_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y32, void* y16, float* mean,
                       float* rstd, int rows, int d, float eps, hipStream_t stream);
 int vqa_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
                       const float* dres, float* dx32, void* dx16, float* dgamma, float* dbeta, float* ws, int rows,
-                      int d, hipStream_t stream);
+                      int d, const vqa_dropout* drop_dx16, float* dsum, hipStream_t stream);
 int vqa_norm_bwd_workspace_floats(int rows, int d);
 /* out[c] = beta*out[c] + sum_p ws[p*stride + c] (fixed order) */
 int vqa_colsum_partials(const float* ws, int parts, long long stride, int cols, float* out, float beta,
@@ -142,8 +183,9 @@ int vqa_maxpool3x3s2_nhwc(const void* x, void* y, int n, int h, int w, int c, in
 int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long long ld, float* out, float beta, float* ws,
                hipStream_t stream);
 int vqa_colsum_workspace_floats(int rows, int cols);
+/* drop: T5 embedding dropout (TF :725) on out (element token*d + col); NULL = none */
 int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int tokens, int d, int vocab,
-                      hipStream_t stream);
+                      const vqa_dropout* drop, hipStream_t stream);
 /* deterministic: each touched row is written once (sorted, fixed token order); tokens <= 8192; ws = 2*tokens ints */
 int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab, int* ws,
                       hipStream_t stream);

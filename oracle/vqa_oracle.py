@@ -22,6 +22,7 @@ from __future__ import annotations
 import math
 from collections import OrderedDict
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -31,6 +32,69 @@ BN_EPS = 1e-5          # torchvision BatchNorm2d default
 SGA_HEADS, SGA_DHEAD = 8, 96     # multi_head_vision_text_attn.py:7-14
 T5_HEADS, T5_DKV = 12, 64
 T5_BUCKETS, T5_MAX_DIST = 32, 128
+
+
+# --------------------------------------------------------------------------- dropout
+# nn.Dropout(p) in train mode draws its Bernoulli(1-p) keep mask from torch's
+# RNG; a GPU path cannot reproduce that stream, so the build defines its masks
+# by a stateless counter hash (include/vqa_hip.h, "dropout") and this oracle
+# restates the same hash, which makes train-mode steps comparable element for
+# element.  The mask law (keep prob 1-p, scale 1/(1-p)) is the reference's.
+_M32 = 0xFFFFFFFF
+
+
+def _mix32(x):
+    """lowbias32 finaliser on uint64 arrays/ints holding 32-bit values."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def dropout_key(seed, counter, site):
+    k0 = _mix32((seed + 0x9E3779B9) & _M32)
+    k1 = _mix32(k0 ^ ((counter * 0x85EBCA6B + 0x632BE5AB) & _M32))
+    return _mix32(k1 ^ ((site * 0xC2B2AE35 + 0x27D4EB2F) & _M32))
+
+
+def dropout_multiplier(p, seed, counter, site, n):
+    """float32 [n]: 1/(1-p) where element e is kept, 0 where dropped."""
+    key = dropout_key(seed, counter, site)
+    e = np.arange(n, dtype=np.uint64)
+    h = _mix32(((e * np.uint64(0x9E3779B9)) + np.uint64(key)) & np.uint64(_M32))
+    thresh = int(float(np.float32(p)) * 4294967296.0)
+    scale = np.float32(1.0) / (np.float32(1.0) - np.float32(p))
+    return np.where(h >= thresh, scale, np.float32(0.0)).astype(np.float32)
+
+
+# site ids (same numbering as the engine: one per nn.Dropout application)
+SITE_EMBED, SITE_FINAL = 1, 2
+
+
+def t5_site(layer, kind):
+    return 16 + 4 * layer + kind
+
+
+def sga_site(block, kind):
+    return 128 + 8 * block + kind
+
+
+class HashDropout:
+    """drop(site, x) -> x * mask(site) for one step (seed, counter); p = 0: identity."""
+
+    def __init__(self, p, seed, counter):
+        self.p, self.seed, self.counter = float(p), int(seed), int(counter)
+
+    def __call__(self, site, x):
+        if self.p <= 0.0:
+            return x
+        m = dropout_multiplier(self.p, self.seed, self.counter, site, x.numel())
+        return x * torch.from_numpy(m).view(x.shape)
+
+
+def _nodrop(site, x):
+    return x
 
 
 # --------------------------------------------------------------------------- ResNet
@@ -99,12 +163,13 @@ def t5_rmsnorm(h, w):
     return w * (h * torch.rsqrt(var + T5_EPS))
 
 
-def t5_encoder(sd, ids, mask, prefix="lang_model."):
-    """T5Stack encoder forward, eval mode (modeling_t5.py:640-751), called from
-    resnet_vqa_model.py:137-140.  Returns last_hidden_state [B, L, 768]."""
+def t5_encoder(sd, ids, mask, prefix="lang_model.", drop=_nodrop):
+    """T5Stack encoder forward (modeling_t5.py:640-751), called from
+    resnet_vqa_model.py:137-140.  Returns last_hidden_state [B, L, 768].
+    `drop` applies the train-mode dropouts (identity = eval mode)."""
     g = lambda k: sd[prefix + k]
     B, L = ids.shape
-    h = g("embed_tokens.weight")[ids]                                  # :678
+    h = drop(SITE_EMBED, g("embed_tokens.weight")[ids])                # :678, dropout :725
     ext = (1.0 - mask[:, None, None, :].float()) * torch.finfo(torch.float32).min   # bidirectional mask
     bias = t5_position_bias(g("block.0.layer.0.SelfAttention.relative_attention_bias.weight"), L, L)
     for i in range(12):
@@ -115,13 +180,13 @@ def t5_encoder(sd, ids, mask, prefix="lang_model."):
         v = (n @ g(p + "0.SelfAttention.v.weight").T).view(B, L, T5_HEADS, T5_DKV).transpose(1, 2)
         s = q @ k.transpose(2, 3)                                      # no 1/sqrt(d) (scaling = 1.0)
         s = s + bias + ext
-        a = torch.softmax(s.float(), dim=-1)
+        a = drop(t5_site(i, 0), torch.softmax(s.float(), dim=-1))     # :168
         o = (a @ v).transpose(1, 2).reshape(B, L, T5_HEADS * T5_DKV)
-        h = h + o @ g(p + "0.SelfAttention.o.weight").T
+        h = h + drop(t5_site(i, 1), o @ g(p + "0.SelfAttention.o.weight").T)     # :400
         n = t5_rmsnorm(h, g(p + "1.layer_norm.weight"))                # T5LayerFF :126-141
-        f = F.relu(n @ g(p + "1.DenseReluDense.wi.weight").T) @ g(p + "1.DenseReluDense.wo.weight").T
-        h = h + f
-    return t5_rmsnorm(h, g("final_layer_norm.weight"))                 # :745
+        f = drop(t5_site(i, 2), F.relu(n @ g(p + "1.DenseReluDense.wi.weight").T))  # :86
+        h = h + drop(t5_site(i, 3), f @ g(p + "1.DenseReluDense.wo.weight").T)    # :140
+    return drop(SITE_FINAL, t5_rmsnorm(h, g("final_layer_norm.weight")))         # :745
 
 
 # --------------------------------------------------------------------------- SGA
@@ -129,14 +194,14 @@ def _linear(x, sd, p):
     return x @ sd[p + ".weight"].T + sd[p + ".bias"]
 
 
-def sga_mhatt(sd, p, v, k, q):
+def sga_mhatt(sd, p, v, k, q, drop=_nodrop, site=0):
     """MHAtt.forward + att (multi_head_vision_text_attn.py:38-86), mask=None."""
     B = q.shape[0]
     V = _linear(v, sd, p + ".linear_v").view(B, -1, SGA_HEADS, SGA_DHEAD).transpose(1, 2)
     K = _linear(k, sd, p + ".linear_k").view(B, -1, SGA_HEADS, SGA_DHEAD).transpose(1, 2)
     Q = _linear(q, sd, p + ".linear_q").view(B, -1, SGA_HEADS, SGA_DHEAD).transpose(1, 2)
     s = (Q @ K.transpose(-2, -1)) / math.sqrt(SGA_DHEAD)
-    a = torch.softmax(s, dim=-1)
+    a = drop(site, torch.softmax(s, dim=-1))                          # :83-84
     o = (a @ V).transpose(1, 2).contiguous().view(B, -1, SGA_HEADS * SGA_DHEAD)
     return _linear(o, sd, p + ".linear_merge")
 
@@ -145,27 +210,29 @@ def _layernorm(x, sd, p):
     return F.layer_norm(x, (x.shape[-1],), sd[p + ".norm.weight"], sd[p + ".norm.bias"], LN_EPS)
 
 
-def sga_block(sd, p, x, y):
-    """SGA.forward (multi_head_vision_text_attn.py:145-158): post-LN, dropout off."""
-    x = _layernorm(x + sga_mhatt(sd, p + ".mhatt1", x, x, x), sd, p + ".norm1")
-    x = _layernorm(x + sga_mhatt(sd, p + ".mhatt2", y, y, x), sd, p + ".norm2")
-    f = _linear(F.relu(_linear(x, sd, p + ".ffn.mlp.fc1")), sd, p + ".ffn.mlp.fc2")
-    return _layernorm(x + f, sd, p + ".norm3")
+def sga_block(sd, p, x, y, drop=_nodrop, block=0):
+    """SGA.forward (multi_head_vision_text_attn.py:145-158): post-LN; `drop` = train-mode dropouts."""
+    st = lambda kind: sga_site(block, kind)
+    x = _layernorm(x + drop(st(1), sga_mhatt(sd, p + ".mhatt1", x, x, x, drop, st(0))), sd, p + ".norm1")
+    x = _layernorm(x + drop(st(3), sga_mhatt(sd, p + ".mhatt2", y, y, x, drop, st(2))), sd, p + ".norm2")
+    f = _linear(drop(st(4), F.relu(_linear(x, sd, p + ".ffn.mlp.fc1"))), sd, p + ".ffn.mlp.fc2")   # MLP :97-101
+    return _layernorm(x + drop(st(5), f), sd, p + ".norm3")
 
 
 # --------------------------------------------------------------------------- full model
-def model_forward(sd, batch, vision="resnet50", num_blocks=3, return_features=False):
-    """ResnetVQAModel.forward (resnet_vqa_model.py:101-165) in eval mode.
+def model_forward(sd, batch, vision="resnet50", num_blocks=3, return_features=False, drop=_nodrop):
+    """ResnetVQAModel.forward (resnet_vqa_model.py:101-165); eval mode unless
+    `drop` (a HashDropout) supplies train-mode dropout.
     Returns (log_probs [B, A], loss scalar or None)."""
     with torch.no_grad():
         feat = resnet_features(sd, batch["image_tensors"], vision)
     scaler = "downscale_layer" if vision == "resnet50" else "upscale_layer"
     vis = F.conv_transpose2d(feat, sd[scaler + ".weight"], sd[scaler + ".bias"], stride=1, padding=1)
-    txt = t5_encoder(sd, batch["question_input_ids"], batch["question_attention_masks"])
+    txt = t5_encoder(sd, batch["question_input_ids"], batch["question_attention_masks"], drop=drop)
     y = vis.view(vis.shape[0], vis.shape[1], -1).permute(0, 2, 1)      # :142-143
     fused = None
     for n in range(num_blocks):                                        # :147-149 (Q4)
-        fused = sga_block(sd, f"sga_modules.{n}", txt, y)
+        fused = sga_block(sd, f"sga_modules.{n}", txt, y, drop, n)
         y = fused
     w = sd["attention_pooler.attention.0.weight"]                      # AttentionPooler :14-26
     a = torch.softmax(fused @ w.T + sd["attention_pooler.attention.0.bias"], dim=1)
@@ -213,8 +280,9 @@ class OracleTrainer:
     """zero_grad -> fwd -> bwd -> clip_grad_norm_(1.0) -> AdamW(amsgrad) -> sched
     (faster_rcnn_vqa_trainer.py:391-406), all restated in fp32 on the CPU."""
 
-    def __init__(self, sd, vision="resnet50", warmup=10, total=100, num_blocks=3):
+    def __init__(self, sd, vision="resnet50", warmup=10, total=100, num_blocks=3, dropout=0.0, seed=0):
         self.vision, self.warmup, self.total, self.num_blocks = vision, warmup, total, num_blocks
+        self.dropout, self.seed, self.rng_counter = float(dropout), int(seed), 0
         self.sd = OrderedDict((k, torch.as_tensor(v).clone()) for k, v in sd.items())
         self.keys = trainable_keys(self.sd, vision)
         for k in self.keys:
@@ -227,7 +295,11 @@ class OracleTrainer:
     def forward_backward(self, batch):
         for k in self.keys:
             self.sd[k].grad = None
-        lp, loss = model_forward(self.sd, batch, self.vision, self.num_blocks)
+        drop = _nodrop
+        if self.dropout > 0.0:                     # one draw per forward, like the engine's rng advance
+            self.rng_counter += 1
+            drop = HashDropout(self.dropout, self.seed, self.rng_counter)
+        lp, loss = model_forward(self.sd, batch, self.vision, self.num_blocks, drop=drop)
         loss.backward()
         return lp.detach(), loss.detach()
 

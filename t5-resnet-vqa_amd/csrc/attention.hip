@@ -25,6 +25,7 @@ struct AttnP {
   const bf16_t* dout; long lddo;
   bf16_t *dq, *dk, *dv; long lddq, lddk, lddv;
   float* dbias;
+  vqa_dropout drop;        // attention-probability dropout (MHAtt.att :84, T5 :168)
 };
 
 __device__ __forceinline__ float2 unpack(uint32_t u) {
@@ -74,6 +75,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnP P) {
   }
   __syncthreads();
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const DropK dk = drop_init(P.drop);
   for (int i = wv; i < lq; i += 4) {
     const float s = l < lk ? S[i * sst + l] : -INFINITY;
     const float m = wave_max(s);
@@ -81,8 +83,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnP P) {
     const float z = wave_sum(e);
     const float pr = e / z;
     if (l < lk) {
-      S[i * sst + l] = pr;
-      if (P.p) P.p[(((long)b * P.heads + h) * lq + i) * lk + l] = pr;
+      const long idx = (((long)b * P.heads + h) * lq + i) * lk + l;
+      S[i * sst + l] = dk.on ? pr * drop_mul(dk, (uint32_t)idx) : pr;      // O uses dropout(P)
+      if (P.p) P.p[idx] = pr;                                               // saved pre-dropout
     }
   }
   __syncthreads();
@@ -126,16 +129,20 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnP P) {
     dS[i * sst + j] = rowdot(Os + i * st, Vs + j * st, w2);
   }
   __syncthreads();
-  // dS = P (dP - sum_j P dP)
+  // with dropout: dP = mask * dP(dropped);  dS = P (dP - sum_j P dP);  Ps <- dropout(P) for dV
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const DropK dk = drop_init(P.drop);
   for (int i = wv; i < lq; i += 4) {
+    const long idx = (((long)b * P.heads + h) * lq + i) * lk + l;
+    const float km = (dk.on && l < lk) ? drop_mul(dk, (uint32_t)idx) : 1.f;
     const float pr = l < lk ? Ps[i * sst + l] : 0.f;
-    const float dp = l < lk ? dS[i * sst + l] : 0.f;
+    const float dp = l < lk ? dS[i * sst + l] * km : 0.f;
     const float di = wave_sum(pr * dp);
     if (l < lk) {
       const float ds = pr * (dp - di);
       dS[i * sst + l] = ds;
-      if (P.dbias) P.dbias[(((long)b * P.heads + h) * lq + i) * lk + l] = ds;   // per-sample dS
+      if (dk.on) Ps[i * sst + l] = pr * km;
+      if (P.dbias) P.dbias[idx] = ds;                                       // per-sample dS
     }
   }
   __syncthreads();
@@ -151,7 +158,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnP P) {
     }
     reinterpret_cast<uint32_t*>(P.dq + ((long)b * lq + i) * P.lddq + h * dh)[e] = pack(a0 * P.scale, a1 * P.scale);
   }
-  // dK = scale * dS^T Q ; dV = P^T dO
+  // dK = scale * dS^T Q ; dV = dropout(P)^T dO
   for (int idx = threadIdx.x; idx < lk * w2; idx += blockDim.x) {
     const int j = idx / w2, e = idx - j * w2;
     float k0 = 0.f, k1 = 0.f, v0 = 0.f, v1 = 0.f;
@@ -188,6 +195,8 @@ int fill(AttnP& P, const vqa_attn_desc* d) {
   P.dq = (bf16_t*)d->dq; P.dk = (bf16_t*)d->dk; P.dv = (bf16_t*)d->dv;
   P.lddq = d->lddq; P.lddk = d->lddk; P.lddv = d->lddv;
   P.dbias = d->dbias;
+  P.drop = d->drop;
+  VQA_REQUIRE(d->drop.p >= 0.f && d->drop.p < 1.f, "attention: dropout p must be in [0, 1)");
   return VQA_OK;
 }
 

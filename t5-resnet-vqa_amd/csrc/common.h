@@ -48,6 +48,39 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// ---------------------------------------------------------------- dropout
+// Counter-based keep masks (include/vqa_hip.h, "dropout"): stateless, so a
+// kernel regenerates exactly the forward mask in backward from (rng, site, e).
+__host__ __device__ __forceinline__ uint32_t vqa_mix32(uint32_t x) {     // lowbias32 finaliser
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+struct DropK {
+  uint32_t key, thresh;
+  float scale;
+  bool on;
+};
+__device__ __forceinline__ DropK drop_init(const vqa_dropout& d) {
+  DropK k;
+  k.on = d.p > 0.f && d.rng != nullptr;
+  k.key = 0; k.thresh = 0; k.scale = 1.f;
+  if (k.on) {
+    const uint32_t k0 = vqa_mix32(d.rng[0] + 0x9E3779B9u);
+    const uint32_t k1 = vqa_mix32(k0 ^ (d.rng[1] * 0x85EBCA6Bu + 0x632BE5ABu));
+    k.key = vqa_mix32(k1 ^ (d.site * 0xC2B2AE35u + 0x27D4EB2Fu));
+    k.thresh = (uint32_t)((double)d.p * 4294967296.0);
+    k.scale = 1.f / (1.f - d.p);
+  }
+  return k;
+}
+__device__ __forceinline__ bool drop_keep(const DropK& k, uint32_t e) {
+  return vqa_mix32(e * 0x9E3779B9u + k.key) >= k.thresh;
+}
+// multiplier for element e: scale if kept, 0 if dropped, 1 when dropout is off
+__device__ __forceinline__ float drop_mul(const DropK& k, uint32_t e) {
+  return k.on ? (drop_keep(k, e) ? k.scale : 0.f) : 1.f;
+}
+
 // ---------------------------------------------------------------- host side
 namespace vqa {
 int fail(int code, const char* fmt, ...);

@@ -91,13 +91,28 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const void* __restrict
 // h[t, :] = table[ids[t], :]  (T5Stack embed_tokens, modeling_t5.py:678)
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(const long long* __restrict__ ids,
                                                             const float* __restrict__ table, float* __restrict__ out,
-                                                            int tokens, int d4, int vocab) {
+                                                            int tokens, int d4, int vocab, vqa_dropout drop) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)tokens * d4) return;
   const int t = (int)(i / d4), j = (int)(i - (long)t * d4);
   long long id = ids[t];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);     // clamp (reference raises; ids validated on host)
-  reinterpret_cast<float4*>(out)[i] = reinterpret_cast<const float4*>(table + id * (long)d4 * 4)[j];
+  float4 v = reinterpret_cast<const float4*>(table + id * (long)d4 * 4)[j];
+  const DropK dk = drop_init(drop);                       // T5 embedding dropout (TF modeling_t5.py:725)
+  if (dk.on) {
+    const uint32_t e = (uint32_t)i * 4u;
+    v.x *= drop_mul(dk, e); v.y *= drop_mul(dk, e + 1); v.z *= drop_mul(dk, e + 2); v.w *= drop_mul(dk, e + 3);
+  }
+  reinterpret_cast<float4*>(out)[i] = v;
+}
+
+__global__ void rng_advance_kernel(unsigned* rng) { rng[1] += 1u; }
+
+__global__ __launch_bounds__(256) void dropout_mask_kernel(vqa_dropout d, float* __restrict__ out, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const DropK dk = drop_init(d);
+  out[i] = drop_mul(dk, (uint32_t)i);
 }
 
 // Deterministic dense embedding gradient (nn.Embedding sparse=False), no atomics:
@@ -141,20 +156,45 @@ __global__ __launch_bounds__(1024) void embedding_sort_kernel(const long long* _
   }
 }
 
-__global__ __launch_bounds__(256) void embedding_bwd_kernel(const float* __restrict__ dh, float* __restrict__ dtable,
-                                                            const int* __restrict__ ws, int tokens, int d) {
+// One workgroup per (sorted slot, 128-column slab); only the first slot of an
+// id-run works.  Long runs (the pad id covers ~40% of a batch) are split over
+// 16 row-lanes that each sum a fixed stride of the run; the 16 partials are
+// then added in lane order through LDS, so the result is still bit-identical
+// run to run.
+constexpr int EMB_RL = 16, EMB_CL = 32;                // row-lanes x float4 column-lanes
+__global__ __launch_bounds__(EMB_RL * EMB_CL) void embedding_bwd_kernel(const float* __restrict__ dh,
+                                                                        float* __restrict__ dtable,
+                                                                        const int* __restrict__ ws, int tokens,
+                                                                        int d) {
   const int s0 = blockIdx.x;
   const int* pos = ws;
   const int* sid = ws + tokens;
   const int id = sid[s0];
-  if (s0 > 0 && sid[s0 - 1] == id) return;           // not the first slot of its run
+  if (s0 > 0 && sid[s0 - 1] == id) return;           // not the first slot of its run (uniform per block)
   int s1 = s0 + 1;
   while (s1 < tokens && sid[s1] == id) ++s1;
-  for (int c = threadIdx.x; c < d; c += 256) {
-    float s = 0.f;
+  const int tx = threadIdx.x % EMB_CL, ty = threadIdx.x / EMB_CL;
+  const int c4 = blockIdx.y * EMB_CL + tx;             // float4 column
+  const bool act = c4 * 4 < d;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (act) {
 #pragma unroll 4
-    for (int u = s0; u < s1; ++u) s += dh[(long)pos[u] * d + c];
-    dtable[(long)id * d + c] = s;
+    for (int u = s0 + ty; u < s1; u += EMB_RL) {
+      const float4 v = reinterpret_cast<const float4*>(dh + (long)pos[u] * d)[c4];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  __shared__ float4 red[EMB_RL][EMB_CL];
+  red[ty][tx] = acc;
+  __syncthreads();
+  if (ty == 0 && act) {
+    float4 t = red[0][tx];
+#pragma unroll
+    for (int r = 1; r < EMB_RL; ++r) {
+      const float4 v = red[r][tx];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    reinterpret_cast<float4*>(dtable + (long)id * d)[c4] = t;
   }
 }
 
@@ -235,24 +275,41 @@ extern "C" int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long lo
 }
 
 extern "C" int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int tokens, int d, int vocab,
-                                 hipStream_t s) {
+                                 const vqa_dropout* drop, hipStream_t s) {
   VQA_REQUIRE(ids && table && out && d % 4 == 0, "vqa_embedding_fwd: bad arguments");
+  VQA_REQUIRE(!drop || (drop->p >= 0.f && drop->p < 1.f), "vqa_embedding_fwd: dropout p must be in [0, 1)");
+  const vqa_dropout dr = drop ? *drop : vqa_dropout{0.f, 0u, nullptr};
   const long total = (long)tokens * (d / 4);
   hipLaunchKernelGGL(embedding_fwd_kernel, dim3(vqa::cdiv(total, 256)), dim3(256), 0, s, ids, table, out, tokens,
-                     d / 4, vocab);
+                     d / 4, vocab, dr);
   return vqa::check_launch("vqa_embedding_fwd");
+}
+
+extern "C" int vqa_rng_advance(unsigned* rng, hipStream_t s) {
+  VQA_REQUIRE(rng, "vqa_rng_advance: null state");
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, s, rng);
+  return vqa::check_launch("vqa_rng_advance");
+}
+
+extern "C" int vqa_dropout_mask(const vqa_dropout* d, float* out, long long n, hipStream_t s) {
+  VQA_REQUIRE(d && out && n > 0 && n <= (1ll << 32), "vqa_dropout_mask: bad arguments");
+  VQA_REQUIRE(d->p >= 0.f && d->p < 1.f, "vqa_dropout_mask: p must be in [0, 1)");
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(vqa::cdiv(n, 256)), dim3(256), 0, s, *d, out, (long)n);
+  return vqa::check_launch("vqa_dropout_mask");
 }
 
 extern "C" int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab,
                                  int* ws, hipStream_t s) {
   // keys hold the position in 16 bits and the padded sort buffer lives in LDS (<= 64 KiB)
-  VQA_REQUIRE(ids && dh && dtable && ws && tokens > 0 && tokens <= 8192, "vqa_embedding_bwd: bad arguments");
+  VQA_REQUIRE(ids && dh && dtable && ws && tokens > 0 && tokens <= 8192 && d % 4 == 0,
+              "vqa_embedding_bwd: bad arguments");
   int n = 1;
   while (n < tokens) n <<= 1;
   hipLaunchKernelGGL(embedding_sort_kernel, dim3(1), dim3(1024), n * sizeof(unsigned long long), s, ids, tokens, vocab,
                      ws);
   if (int rc = vqa::check_launch("vqa_embedding_bwd/sort")) return rc;
-  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(tokens), dim3(256), 0, s, dh, dtable, ws, tokens, d);
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(tokens, vqa::cdiv(d, 4 * EMB_CL)), dim3(EMB_RL * EMB_CL), 0, s, dh,
+                     dtable, ws, tokens, d);
   return vqa::check_launch("vqa_embedding_bwd");
 }
 

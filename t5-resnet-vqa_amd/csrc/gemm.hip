@@ -46,6 +46,7 @@ struct GemmParams {
   long sa, sb, sc32, sc16, sres;
   int tiles_m, tiles_n;
   int vec;                 // 4-wide vector epilogue legal (N, ld*, pointers aligned)
+  vqa_dropout drop;        // dropout of the (alpha*acc + bias) branch
 };
 
 // byte offset of 16-B chunk `ch` of row `row` in a k-contig image ([rows][64 bf16])
@@ -328,18 +329,25 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
   }
 
   // epilogue: acc[i][j][4g+t] -> row m0+wm*WM+i*32+(l&31), col n0+wn*WN+j*32+8g+4(l>>5)+t.
-  // All inputs (bias, residual, mask, old C) are loaded before any store so the
-  // compiler can keep them in flight (C may alias them as far as it knows).
+  // Per element: k = [mask > 0] * dropout multiplier (1 if neither), then
+  //   v = k*(alpha*acc + bias) + res ; relu ; c32 = v + beta*c32 ; c16 = bf16(v).
+  // (relu(k*t) == k*relu(t) for k >= 0, and with a residual relu acts after it.)
+  // All inputs (bias, residual, mask, old C) are loaded and the keep factors
+  // computed before any store so the loads stay in flight (C may alias them as
+  // far as the compiler knows); keep factors travel as a 4-bit mask per group.
   float* C32 = P.c32 ? P.c32 + (long)z * P.sc32 : nullptr;
   bf16_t* C16 = P.c16 ? P.c16 + (long)z * P.sc16 : nullptr;
   const float* R32 = P.res32 ? P.res32 + (long)z * P.sres : nullptr;
   const bf16_t* R16 = P.res16 ? P.res16 + (long)z * P.sres : nullptr;
   const bf16_t* MK = P.mask16 ? P.mask16 + (long)z * P.sres : nullptr;
   const bool beta = P.beta != 0.f && C32;
+  const DropK dk = drop_init(P.drop);
+  const float kscale = dk.on ? dk.scale : 1.f;       // multiplier of a kept element
+  const uint32_t ebase = (uint32_t)z * (uint32_t)P.m;  // dropout element index = (z*m + row)*n + col
   const int rl = l & 31, ch = l >> 5;
   if (P.vec) {
     float4 add[TM][TN][4];
-    uint2 msk[TM][TN][4];
+    uint32_t kb[TM][TN][4];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -349,9 +357,24 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
           const int row = m0 + wm * WM + i * 32 + rl;
           const int col = n0 + wn * WN + j * 32 + 8 * g + 4 * ch;
           float4 a4 = make_float4(0.f, 0.f, 0.f, 0.f);
-          uint2 m2 = make_uint2(0x3f803f80u, 0x3f803f80u);       // bf16 1.0 x4 (no mask)
+          uint32_t bits = 0xf;
           if (row < P.m && col < P.n) {
-            if (P.bias) a4 = *reinterpret_cast<const float4*>(P.bias + col);
+            if (MK) {
+              const uint2 m2 = *reinterpret_cast<const uint2*>(MK + (long)row * P.ldmask + col);
+              bits = (bf2f(m2.x & 0xffff) > 0.f ? 1u : 0u) | (bf2f(m2.x >> 16) > 0.f ? 2u : 0u) |
+                     (bf2f(m2.y & 0xffff) > 0.f ? 4u : 0u) | (bf2f(m2.y >> 16) > 0.f ? 8u : 0u);
+            }
+            if (dk.on) {
+              const uint32_t e = (ebase + (uint32_t)row) * (uint32_t)P.n + (uint32_t)col;
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+                if (!drop_keep(dk, e + t)) bits &= ~(1u << t);
+            }
+            if (P.bias) {
+              a4 = *reinterpret_cast<const float4*>(P.bias + col);
+              a4.x *= (bits & 1) ? kscale : 0.f; a4.y *= (bits & 2) ? kscale : 0.f;
+              a4.z *= (bits & 4) ? kscale : 0.f; a4.w *= (bits & 8) ? kscale : 0.f;
+            }
             if (R32) {
               const float4 r = *reinterpret_cast<const float4*>(R32 + (long)row * P.ldres + col);
               a4.x += r.x; a4.y += r.y; a4.z += r.z; a4.w += r.w;
@@ -360,10 +383,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
               const uint2 r = *reinterpret_cast<const uint2*>(R16 + (long)row * P.ldres + col);
               a4.x += bf2f(r.x & 0xffff); a4.y += bf2f(r.x >> 16); a4.z += bf2f(r.y & 0xffff); a4.w += bf2f(r.y >> 16);
             }
-            if (MK) m2 = *reinterpret_cast<const uint2*>(MK + (long)row * P.ldmask + col);
           }
           add[i][j][g] = a4;
-          msk[i][j][g] = m2;
+          kb[i][j][g] = bits;
         }
     float4 old[TM][TN][4];
     if (beta) {
@@ -379,6 +401,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
           }
     }
+    const float ak = P.alpha * kscale;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -389,14 +412,14 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
           const int col = n0 + wn * WN + j * 32 + 8 * g + 4 * ch;
           if (row >= P.m || col >= P.n) continue;
           const float4 a4 = add[i][j][g];
-          const uint2 m2 = msk[i][j][g];
-          float v[4] = {acc[i][j][4 * g] * P.alpha + a4.x, acc[i][j][4 * g + 1] * P.alpha + a4.y,
-                        acc[i][j][4 * g + 2] * P.alpha + a4.z, acc[i][j][4 * g + 3] * P.alpha + a4.w};
-          const float mk[4] = {bf2f(m2.x & 0xffff), bf2f(m2.x >> 16), bf2f(m2.y & 0xffff), bf2f(m2.y >> 16)};
+          const uint32_t bits = kb[i][j][g];
+          float v[4] = {acc[i][j][4 * g] * ((bits & 1) ? ak : 0.f) + a4.x,
+                        acc[i][j][4 * g + 1] * ((bits & 2) ? ak : 0.f) + a4.y,
+                        acc[i][j][4 * g + 2] * ((bits & 4) ? ak : 0.f) + a4.z,
+                        acc[i][j][4 * g + 3] * ((bits & 8) ? ak : 0.f) + a4.w};
+          if (P.relu) {
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (P.relu) v[t] = fmaxf(v[t], 0.f);
-            if (!(mk[t] > 0.f)) v[t] = 0.f;
+            for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
           }
           if (C32) {
             float4 o = make_float4(v[0], v[1], v[2], v[3]);
@@ -424,11 +447,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
           const int row = m0 + wm * WM + i * 32 + rl;
           const int col = n0 + wn * WN + j * 32 + 8 * (e >> 2) + 4 * ch + (e & 3);
           if (row >= P.m || col >= P.n) continue;
-          float v = acc[i][j][e] * P.alpha + (P.bias ? P.bias[col] : 0.f);
+          float kf = 1.f;
+          if (MK && !(bf2f(MK[(long)row * P.ldmask + col]) > 0.f)) kf = 0.f;
+          if (dk.on) kf *= drop_mul(dk, (ebase + (uint32_t)row) * (uint32_t)P.n + (uint32_t)col);
+          float v = kf * (acc[i][j][e] * P.alpha + (P.bias ? P.bias[col] : 0.f));
           if (R32) v += R32[(long)row * P.ldres + col];
           if (R16) v += bf2f(R16[(long)row * P.ldres + col]);
           if (P.relu) v = fmaxf(v, 0.f);
-          if (MK && !(bf2f(MK[(long)row * P.ldmask + col]) > 0.f)) v = 0.f;
           if (C32) {
             float* cp = C32 + (long)row * P.ldc32 + col;
             *cp = beta ? v + P.beta * *cp : v;
@@ -497,6 +522,9 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   VQA_REQUIRE(!d->b_conv || d->gb.c % 8 == 0, "vqa_gemm: conv input channels must be a multiple of 8");
   VQA_REQUIRE(d->batch >= 1, "vqa_gemm: batch must be >= 1");
   VQA_REQUIRE(d->config >= 0 && d->config <= 4, "vqa_gemm: config must be 0..4");
+  VQA_REQUIRE(d->drop.p >= 0.f && d->drop.p < 1.f, "vqa_gemm: dropout p must be in [0, 1)");
+  VQA_REQUIRE(!(d->drop.p > 0.f && d->drop.rng && d->relu && (d->res32 || d->res16)),
+              "vqa_gemm: relu + residual + dropout is not a supported epilogue");
   GemmParams P;
   P.a = (const bf16_t*)d->a; P.lda = d->lda;
   P.b = (const bf16_t*)d->b; P.ldb = d->ldb;
@@ -508,6 +536,7 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   P.alpha = d->alpha; P.beta = d->beta; P.relu = d->relu;
   P.ga = d->ga; P.gb = d->gb;
   P.sa = d->stride_a; P.sb = d->stride_b; P.sc32 = d->stride_c32; P.sc16 = d->stride_c16; P.sres = d->stride_res;
+  P.drop = d->drop;
   const int batch = d->batch, cfg = d->config;
   auto al = [](const void* p, int bytes) { return p == nullptr || ((uintptr_t)p % bytes) == 0; };
   P.vec = d->n % 4 == 0 && (!d->c32 || (d->ldc32 % 4 == 0 && al(d->c32, 16) && d->stride_c32 % 4 == 0)) &&

@@ -42,14 +42,52 @@ __device__ __forceinline__ void store_row16(bf16_t* __restrict__ p, const float 
 template <int NV>
 __device__ __forceinline__ void load_vec(const float* __restrict__ p, float (&x)[NV][4]) { load_row<NV>(p, x); }
 
+// multiply a row held as [NV][4] per lane by the dropout factors of row `row`
+template <int NV>
+__device__ __forceinline__ void drop_row(const DropK& k, int row, float (&x)[NV][4]) {
+  if (!k.on) return;
+  const int l = threadIdx.x & 63;
+  const uint32_t base = (uint32_t)row * (uint32_t)(NV * 256);
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[i][j] *= drop_mul(k, base + (uint32_t)((i * 64 + l) * 4 + j));
+}
+template <int NV>
+__device__ __forceinline__ void store_row16_drop(bf16_t* __restrict__ p, const DropK& k, int row,
+                                                 const float (&x)[NV][4]) {
+  if (!k.on) { store_row16<NV>(p, x); return; }
+  float y[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[i][j] = x[i][j];
+  drop_row<NV>(k, row, y);
+  store_row16<NV>(p, y);
+}
+template <int NV>
+__device__ __forceinline__ void store_row32_drop(float* __restrict__ p, const DropK& k, int row,
+                                                 const float (&x)[NV][4]) {
+  if (!k.on) { store_row32<NV>(p, x); return; }
+  float y[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[i][j] = x[i][j];
+  drop_row<NV>(k, row, y);
+  store_row32<NV>(p, y);
+}
+
 // ------------------------------------------------------------------ RMSNorm
 template <int NV>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           float* __restrict__ y32, bf16_t* __restrict__ y16,
-                                                          float* __restrict__ rstd, int rows, float eps) {
+                                                          float* __restrict__ rstd, int rows, float eps,
+                                                          vqa_dropout drop) {
   const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
   if (row >= rows) return;
   constexpr int D = NV * 256;
+  const DropK dk = drop_init(drop);
   float v[NV][4], g[NV][4];
   load_row<NV>(x + (long)row * D, v);
   load_vec<NV>(w, g);
@@ -64,6 +102,7 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const float* __restric
   for (int i = 0; i < NV; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[i][j] = g[i][j] * (v[i][j] * r);
+  drop_row<NV>(dk, row, v);
   if (y32) store_row32<NV>(y32 + (long)row * D, v);
   if (y16) store_row16<NV>(y16 + (long)row * D, v);
   if (rstd && (threadIdx.x & 63) == 0) rstd[row] = r;
@@ -75,9 +114,11 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* __restric
                                                           const float* __restrict__ rstd, const float* __restrict__ w,
                                                           const float* __restrict__ dres, float* __restrict__ dx32,
                                                           bf16_t* __restrict__ dx16, float* __restrict__ dw_ws,
-                                                          int rows, int rows_per_block) {
+                                                          int rows, int rows_per_block, vqa_dropout drop_dy,
+                                                          vqa_dropout drop_dx32, vqa_dropout drop_dx16) {
   constexpr int D = NV * 256;
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const DropK kdy = drop_init(drop_dy), k32 = drop_init(drop_dx32), k16 = drop_init(drop_dx16);
   float g[NV][4];
   load_vec<NV>(w, g);
   float dwacc[NV][4] = {};
@@ -87,6 +128,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* __restric
     float d[NV][4], v[NV][4];
     load_row<NV>(dy + (long)row * D, d);
     load_row<NV>(x + (long)row * D, v);
+    drop_row<NV>(kdy, row, d);
     const float r = rstd[row];
     float s = 0.f;
 #pragma unroll
@@ -107,8 +149,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* __restric
         float t = r * g[i][j] * d[i][j] - c * v[i][j];
         o[i][j] = dres ? o[i][j] + t : t;
       }
-    if (dx32) store_row32<NV>(dx32 + (long)row * D, o);
-    if (dx16) store_row16<NV>(dx16 + (long)row * D, o);
+    if (dx32) store_row32_drop<NV>(dx32 + (long)row * D, k32, row, o);
+    if (dx16) store_row16_drop<NV>(dx16 + (long)row * D, k16, row, o);
   }
   // reduce the 4 waves' dw partials through LDS, write one row per block
   __shared__ float red[ROWS_PER_BLOCK][NV * 256];
@@ -164,12 +206,14 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
                                                             const float* __restrict__ mean, const float* __restrict__ rstd,
                                                             const float* __restrict__ gam, const float* __restrict__ dres,
                                                             float* __restrict__ dx32, bf16_t* __restrict__ dx16,
-                                                            float* __restrict__ ws, int rows, int rows_per_block) {
+                                                            float* __restrict__ ws, int rows, int rows_per_block,
+                                                            vqa_dropout drop_dx16, int with_dsum) {
   constexpr int D = NV * 256;
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const DropK k16 = drop_init(drop_dx16);
   float g[NV][4];
   load_vec<NV>(gam, g);
-  float dga[NV][4] = {}, dba[NV][4] = {};
+  float dga[NV][4] = {}, dba[NV][4] = {}, dsa[NV][4] = {};
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   for (int row = r0 + wv; row < r1; row += ROWS_PER_BLOCK) {
@@ -201,18 +245,26 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
         o[i][j] = dres ? o[i][j] + t : t;
       }
     if (dx32) store_row32<NV>(dx32 + (long)row * D, o);
-    if (dx16) store_row16<NV>(dx16 + (long)row * D, o);
+    if (dx16 || with_dsum) {
+      drop_row<NV>(k16, row, o);                           // the branch gradient (masked)
+      if (dx16) store_row16<NV>(dx16 + (long)row * D, o);
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dsa[i][j] += o[i][j];
+    }
   }
   __shared__ float red[ROWS_PER_BLOCK][NV * 256];
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
+  const int npass = with_dsum ? 3 : 2;
+  for (int pass = 0; pass < npass; ++pass) {
 #pragma unroll
     for (int i = 0; i < NV; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) red[wv][(i * 64 + l) * 4 + j] = pass == 0 ? dga[i][j] : dba[i][j];
+      for (int j = 0; j < 4; ++j)
+        red[wv][(i * 64 + l) * 4 + j] = pass == 0 ? dga[i][j] : (pass == 1 ? dba[i][j] : dsa[i][j]);
     __syncthreads();
     for (int c = threadIdx.x; c < D; c += 256)
-      ws[((long)blockIdx.x * 2 + pass) * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+      ws[((long)blockIdx.x * 3 + pass) * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
     __syncthreads();
   }
 }
@@ -240,7 +292,37 @@ __global__ __launch_bounds__(1024) void colsum_partials_kernel(const float* __re
   }
 }
 
+// the LayerNorm backward's up to three column sums in one launch: blockIdx.y picks
+// the output (0 dgamma, 1 dbeta, 2 branch-gradient sum) from ws[p][3][cols]
+__global__ __launch_bounds__(1024) void colsum3_partials_kernel(const float* __restrict__ ws, int parts, long stride,
+                                                                int cols, float* __restrict__ o0,
+                                                                float* __restrict__ o1, float* __restrict__ o2) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx, which = blockIdx.y;
+  const float* w = ws + (long)which * cols;
+  float s = 0.f;
+  if (c < cols) {
+#pragma unroll 4
+    for (int p = ty; p < parts; p += 16) s += w[(long)p * stride + c];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][tx];
+    (which == 0 ? o0 : (which == 1 ? o1 : o2))[c] = t;
+  }
+}
+
 constexpr int NORM_BWD_ROWS = 16;      // rows per block in the backward kernels
+
+vqa_dropout dr(const vqa_dropout* d) {
+  vqa_dropout o{0.f, 0u, nullptr};
+  return d ? *d : o;
+}
+bool dr_ok(const vqa_dropout* d) { return !d || (d->p >= 0.f && d->p < 1.f); }
 
 }  // namespace
 
@@ -254,24 +336,28 @@ constexpr int NORM_BWD_ROWS = 16;      // rows per block in the backward kernels
   }
 
 extern "C" int vqa_rmsnorm_fwd(const float* x, const float* w, float* y32, void* y16, float* rstd, int rows, int d,
-                               float eps, hipStream_t s) {
+                               float eps, const vqa_dropout* drop, hipStream_t s) {
   VQA_REQUIRE(x && w && (y32 || y16) && rows > 0 && d % 256 == 0, "vqa_rmsnorm_fwd: bad arguments");
+  VQA_REQUIRE(dr_ok(drop), "vqa_rmsnorm_fwd: dropout p must be in [0, 1)");
   dim3 grid(vqa::cdiv(rows, ROWS_PER_BLOCK));
   DISPATCH_NV(d, hipLaunchKernelGGL(rmsnorm_fwd_kernel<NV>, grid, dim3(256), 0, s, x, w, y32, (bf16_t*)y16, rstd,
-                                    rows, eps));
+                                    rows, eps, dr(drop)));
   return vqa::check_launch("vqa_rmsnorm_fwd");
 }
 
 int vqa_norm_bwd_parts(int rows) { return vqa::cdiv(rows, NORM_BWD_ROWS); }
-extern "C" int vqa_norm_bwd_workspace_floats(int rows, int d) { return 2 * vqa_norm_bwd_parts(rows) * d; }
+extern "C" int vqa_norm_bwd_workspace_floats(int rows, int d) { return 3 * vqa_norm_bwd_parts(rows) * d; }
 
 extern "C" int vqa_rmsnorm_bwd(const float* dy, const float* x, const float* rstd, const float* w, const float* dres,
                                float* dx32, void* dx16, float* dw, float dw_beta, float* ws, int rows, int d,
+                               const vqa_dropout* drop_dy, const vqa_dropout* drop_dx32, const vqa_dropout* drop_dx16,
                                hipStream_t s) {
   VQA_REQUIRE(dy && x && rstd && w && dw && ws && (dx32 || dx16) && d % 256 == 0, "vqa_rmsnorm_bwd: bad arguments");
+  VQA_REQUIRE(dr_ok(drop_dy) && dr_ok(drop_dx32) && dr_ok(drop_dx16), "vqa_rmsnorm_bwd: dropout p must be in [0, 1)");
   const int parts = vqa_norm_bwd_parts(rows);
   DISPATCH_NV(d, hipLaunchKernelGGL(rmsnorm_bwd_kernel<NV>, dim3(parts), dim3(256), 0, s, dy, x, rstd, w, dres, dx32,
-                                    (bf16_t*)dx16, ws, rows, NORM_BWD_ROWS));
+                                    (bf16_t*)dx16, ws, rows, NORM_BWD_ROWS, dr(drop_dy), dr(drop_dx32),
+                                    dr(drop_dx16)));
   if (int rc = vqa::check_launch("vqa_rmsnorm_bwd")) return rc;
   hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 64)), dim3(1024), 0, s, ws, parts, (long)d, d, dw,
                      dw_beta);
@@ -289,17 +375,18 @@ extern "C" int vqa_layernorm_fwd(const float* x, const float* gamma, const float
 
 extern "C" int vqa_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
                                  const float* gamma, const float* dres, float* dx32, void* dx16, float* dgamma,
-                                 float* dbeta, float* ws, int rows, int d, hipStream_t s) {
+                                 float* dbeta, float* ws, int rows, int d, const vqa_dropout* drop_dx16,
+                                 float* dsum, hipStream_t s) {
   VQA_REQUIRE(dy && x && mean && rstd && gamma && dgamma && dbeta && ws && (dx32 || dx16) && d % 256 == 0,
               "vqa_layernorm_bwd: bad arguments");
+  VQA_REQUIRE(dr_ok(drop_dx16), "vqa_layernorm_bwd: dropout p must be in [0, 1)");
   const int parts = vqa_norm_bwd_parts(rows);
   DISPATCH_NV(d, hipLaunchKernelGGL(layernorm_bwd_kernel<NV>, dim3(parts), dim3(256), 0, s, dy, x, mean, rstd, gamma,
-                                    dres, dx32, (bf16_t*)dx16, ws, rows, NORM_BWD_ROWS));
+                                    dres, dx32, (bf16_t*)dx16, ws, rows, NORM_BWD_ROWS, dr(drop_dx16),
+                                    dsum != nullptr ? 1 : 0));
   if (int rc = vqa::check_launch("vqa_layernorm_bwd")) return rc;
-  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 64)), dim3(1024), 0, s, ws, parts, (long)2 * d, d,
-                     dgamma, 0.f);
-  hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 64)), dim3(1024), 0, s, ws + d, parts, (long)2 * d, d,
-                     dbeta, 0.f);
+  hipLaunchKernelGGL(colsum3_partials_kernel, dim3(vqa::cdiv(d, 64), dsum ? 3 : 2), dim3(1024), 0, s, ws, parts,
+                     (long)3 * d, d, dgamma, dbeta, dsum);
   return vqa::check_launch("vqa_layernorm_bwd/colsum");
 }
 

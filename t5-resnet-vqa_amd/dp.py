@@ -96,11 +96,13 @@ class DataParallelStep:
         e = self.eng
         s = torch.cuda.Stream(e.dev)
         s.wait_stream(torch.cuda.current_stream(e.dev))
+        saved_rng = e.RNG.clone()
         with torch.cuda.stream(s):                          # warm-up outside capture
             e.forward()
             e.backward()
         torch.cuda.current_stream(e.dev).wait_stream(s)
         torch.cuda.synchronize(e.dev)
+        e.RNG.copy_(saved_rng)                              # the warm-up must not consume a dropout draw
         gs = {}
 
         def cap(name, calls):

@@ -20,7 +20,10 @@ Design (MI355X-first, not a translation of eager PyTorch):
   * activations/workspaces are allocated once for a fixed (B, L, H), every
     kernel call is prepared once with fixed device addresses, and the whole
     step is replayed as one hipGraph (torch.cuda.CUDAGraph capture);
-  * dropout is off (eval-mode numerics); parity is defined there.
+  * dropout (p = 0.1 at the reference's 12 sites per step) is
+    applied inside the producing kernels from a stateless counter hash
+    (include/vqa_hip.h "dropout"); the backward regenerates the masks, nothing
+    is stored.  dropout=0 gives eval-mode numerics (golden-vector parity).
 """
 from __future__ import annotations
 
@@ -38,12 +41,27 @@ from .layout import ParamLayout, fold_bn, t5_bucket_map
 BF16, F32, I64 = torch.bfloat16, torch.float32, torch.int64
 D = S.D_MODEL
 
+# dropout site ids (the hash key of each nn.Dropout application of the step)
+SITE_EMBED, SITE_FINAL = 1, 2                  # T5Stack: dropout(inputs_embeds) :725, dropout(final_ln) :745
+
+
+def t5_site(layer, kind):
+    """kind 0 attention probs (:168), 1 attention residual branch (:400), 2 FF inner (:86), 3 FF residual (:140)"""
+    return 16 + 4 * layer + kind
+
+
+def sga_site(block, kind):
+    """kind 0 mhatt1 probs, 1 dropout1, 2 mhatt2 probs, 3 dropout2, 4 MLP inner, 5 dropout3
+    (multi_head_vision_text_attn.py:84, 146, 84, 150, 99, 154)"""
+    return 128 + 8 * block + kind
+
 
 class VQAEngine:
     def __init__(self, state_dict, vision="resnet50", batch=64, seq_len=32, image_size=224, device="cuda:0",
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
-                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1):
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0):
         L.load()
+        self.p_drop, self.seed = float(dropout), int(seed)
         self.dev = torch.device(device)
         self.vision, self.B, self.L, self.H = vision, batch, seq_len, image_size
         self.NB, self.A = num_blocks, answer_spaces
@@ -90,6 +108,8 @@ class VQAEngine:
             self.p16[s.name] = self.P16[sl].view(s.shape)
             self.g32[s.name] = self.G32[sl].view(s.shape)
         self.opt_state = self._t(8, zero=True)
+        # dropout RNG state {seed, counter}; the forward's first call advances the counter
+        self.RNG = torch.from_numpy(np.array([self.seed & 0xFFFFFFFF, 0], np.uint32).view(np.int32)).to(self.dev)
         self.bucket = torch.from_numpy(t5_bucket_map(self.L, self.L)).reshape(-1).to(self.dev)
 
     def _plan_resnet(self, sd):
@@ -257,29 +277,57 @@ class VQAEngine:
         ts = [a, b] + [v for v in kw.values() if isinstance(v, torch.Tensor)]
         lst.append(ops.gemm_call(ops.gemm_desc(a, b, m, n, k, **kw), [t for t in ts if isinstance(t, torch.Tensor)]))
 
-    def _call(self, lst, name, *args):
-        ts = tuple(a for a in args if isinstance(a, torch.Tensor))
+    def _call(self, lst, name, *args, extra=()):
+        ts = tuple(a for a in args if isinstance(a, torch.Tensor)) + tuple(extra)
         lst.append(ops.Call(name, *[ops.addr(a) if isinstance(a, torch.Tensor) else a for a in args], keep=ts))
 
-    def _attn(self, lst, fn, **kw):
+    def _attn(self, lst, fn, drop=None, **kw):
         d = L.AttnDesc()
         for k, v in kw.items():
             setattr(d, k, ops.addr(v) if isinstance(v, torch.Tensor) else v)
         ts = tuple(v for v in kw.values() if isinstance(v, torch.Tensor))
+        dd = self._drop(drop) if drop is not None else None
+        if dd is not None:
+            d.drop = dd
+            ts = ts + (self.RNG,)
         lst.append(ops.Call(fn, ctypes.byref(d), keep=ts, desc=d))
 
-    def _linear(self, lst, x16, wname, m, out32=None, out16=None, bias=True, relu=False, res32=None):
+    def _drop(self, site):
+        """vqa_dropout for `site` (None when dropout is off)."""
+        if self.p_drop <= 0.0:
+            return None
+        return L.Dropout(self.p_drop, site, self.RNG.data_ptr())
+
+    def _dptr(self, site, keep):
+        """`const vqa_dropout*` argument (0 = none); the struct is kept alive through `keep`."""
+        d = self._drop(site)
+        if d is None:
+            return None
+        keep.append(d)
+        return ctypes.addressof(d)
+
+    @property
+    def drop_scale(self):
+        """1/(1-p) in fp32, the multiplier of a kept element (as the kernels compute it)."""
+        p = np.float32(self.p_drop)
+        return float(np.float32(1.0) / (np.float32(1.0) - p))
+
+    def _linear(self, lst, x16, wname, m, out32=None, out16=None, bias=True, relu=False, res32=None, drop=None):
         w = self.p16[wname]
         n, k = w.shape
         self._gemm(lst, x16, w, m, n, k, lda=k, ldb=k, c32=out32, ldc32=n, c16=out16, ldc16=n,
                    bias=self.p32[wname[:-1] + "b"] if bias else None, relu=relu, res32=res32, ldres=n)
+        d = self._drop(drop) if drop is not None else None
+        if d is not None:
+            lst[-1].desc.drop = d
+            lst[-1].keep = lst[-1].keep + (self.RNG,)
 
-    def _dx(self, lst, dy16, wname, m, out32=None, out16=None, res32=None, mask16=None, beta=0.0):
-        """dX[m, k] = dY[m, n] W[n, k]  (+res) (*mask>0) (+beta*out32)"""
+    def _dx(self, lst, dy16, wname, m, out32=None, out16=None, res32=None, mask16=None, beta=0.0, alpha=1.0):
+        """dX[m, k] = alpha * dY[m, n] W[n, k]  (+res) (*mask>0) (+beta*out32)"""
         w = self.p16[wname]
         n, k = w.shape
         self._gemm(lst, dy16, w, m, k, n, lda=n, ldb=k, b_trans=True, c32=out32, ldc32=k, c16=out16, ldc16=k,
-                   res32=res32, ldres=k, mask16=mask16, ldmask=k, beta=beta)
+                   res32=res32, ldres=k, mask16=mask16, ldmask=k, beta=beta, alpha=alpha)
 
     def _dw(self, lst, dy16, x16, wname, rows, bias_from=None, bias_bf16=True):
         """dW[n, k] = dY[rows, n]^T X[rows, k]; optional bias grad = colsum(dY)."""
@@ -294,6 +342,8 @@ class VQAEngine:
     def _plan_forward(self):
         f = self.fwd_calls
         B, Lq, T = self.B, self.L, self.T
+        if self.p_drop > 0.0:                                # fresh dropout masks every step
+            self._call(f, "vqa_rng_advance", self.RNG)
         f += self.res_calls
         # ConvTranspose2d scaler as implicit GEMM over the layer4 map (+bias) -> vision tokens
         cin, fh = self.fc, self.fh
@@ -301,23 +351,30 @@ class VQAEngine:
         self._gemm(f, self.F4, self.p16["scaler_w"], self.V_TOK, D, 9 * cin, lda=9 * cin, ldb=9 * cin, ga=g,
                    c32=self.VIS32, ldc32=D, c16=self.VIS16, ldc16=D, bias=self.p32["scaler_b"])
         # T5 encoder
-        self._call(f, "vqa_embedding_fwd", self.IDS, self.p32["t5.embed"], self.HS[0], T, D, S.T5_VOCAB)
+        kp = []
+        self._call(f, "vqa_embedding_fwd", self.IDS, self.p32["t5.embed"], self.HS[0], T, D, S.T5_VOCAB,
+                   self._dptr(SITE_EMBED, kp), extra=kp + [self.RNG])
         self._call(f, "vqa_t5_relbias_fwd", self.p32["t5.relbias"], self.bucket, self.PB, S.T5_HEADS, Lq, Lq)
         for i in range(S.T5_LAYERS):
             self._call(f, "vqa_rmsnorm_fwd", self.HS[i], self.p32[f"t5.{i}.ln0"], None, self.N0[i], self.R0[i], T, D,
-                       1e-6)
+                       1e-6, None)
             self._linear(f, self.N0[i], f"t5.{i}.qkv_w", T, out16=self.QKV[i], bias=False)
             q = self.QKV[i]
             self._attn(f, "vqa_attn_fwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, o=self.O[i], ldo=D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B,
-                       heads=S.T5_HEADS, lq=Lq, lk=Lq, dh=S.T5_DKV, scale=1.0)
-            self._linear(f, self.O[i], f"t5.{i}.o_w", T, out32=self.HM[i], bias=False, res32=self.HS[i])
+                       heads=S.T5_HEADS, lq=Lq, lk=Lq, dh=S.T5_DKV, scale=1.0, drop=t5_site(i, 0))
+            # h + dropout(attention output)   (T5LayerSelfAttention :400)
+            self._linear(f, self.O[i], f"t5.{i}.o_w", T, out32=self.HM[i], bias=False, res32=self.HS[i],
+                         drop=t5_site(i, 1))
             self._call(f, "vqa_rmsnorm_fwd", self.HM[i], self.p32[f"t5.{i}.ln1"], None, self.N1[i], self.R1[i], T, D,
-                       1e-6)
-            self._linear(f, self.N1[i], f"t5.{i}.wi", T, out16=self.FF[i], bias=False, relu=True)
-            self._linear(f, self.FF[i], f"t5.{i}.wo", T, out32=self.HS[i + 1], bias=False, res32=self.HM[i])
+                       1e-6, None)
+            # dropout(relu(wi h)) (T5DenseActDense :86), then h + dropout(wo .) (T5LayerFF :140)
+            self._linear(f, self.N1[i], f"t5.{i}.wi", T, out16=self.FF[i], bias=False, relu=True, drop=t5_site(i, 2))
+            self._linear(f, self.FF[i], f"t5.{i}.wo", T, out32=self.HS[i + 1], bias=False, res32=self.HM[i],
+                         drop=t5_site(i, 3))
+        kp = []
         self._call(f, "vqa_rmsnorm_fwd", self.HS[-1], self.p32["t5.final_ln"], self.TXT32, self.TXT16, self.RF, T, D,
-                   1e-6)
+                   1e-6, self._dptr(SITE_FINAL, kp), extra=kp + [self.RNG])
         # SGA blocks: x = text always, y chained
         y16 = self.VIS16
         sc = 1.0 / math.sqrt(S.SGA_DHEAD)
@@ -327,8 +384,8 @@ class VQAEngine:
             q = s["QKV1"]
             self._attn(f, "vqa_attn_fwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, o=s["O1"], ldo=D, p=s["P1"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=Lq,
-                       dh=S.SGA_DHEAD, scale=sc)
-            self._linear(f, s["O1"], p + "m1_w", T, out32=s["S1"], res32=self.TXT32)
+                       dh=S.SGA_DHEAD, scale=sc, drop=sga_site(n, 0))
+            self._linear(f, s["O1"], p + "m1_w", T, out32=s["S1"], res32=self.TXT32, drop=sga_site(n, 1))
             self._call(f, "vqa_layernorm_fwd", s["S1"], self.p32[p + "ln1_g"], self.p32[p + "ln1_b"], s["X1"],
                        s["X1h"], s["MU1"], s["RS1"], T, D, 1e-5)
             self._linear(f, s["X1h"], p + "q2_w", T, out16=s["Q2"])
@@ -336,12 +393,12 @@ class VQAEngine:
             kv = s["KV2"]
             self._attn(f, "vqa_attn_fwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
                        o=s["O2"], ldo=D, p=s["P2"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=s["lk"], dh=S.SGA_DHEAD,
-                       scale=sc)
-            self._linear(f, s["O2"], p + "m2_w", T, out32=s["S2"], res32=s["X1"])
+                       scale=sc, drop=sga_site(n, 2))
+            self._linear(f, s["O2"], p + "m2_w", T, out32=s["S2"], res32=s["X1"], drop=sga_site(n, 3))
             self._call(f, "vqa_layernorm_fwd", s["S2"], self.p32[p + "ln2_g"], self.p32[p + "ln2_b"], s["X2"],
                        s["X2h"], s["MU2"], s["RS2"], T, D, 1e-5)
-            self._linear(f, s["X2h"], p + "fc1_w", T, out16=s["FFh"], relu=True)
-            self._linear(f, s["FFh"], p + "fc2_w", T, out32=s["S3"], res32=s["X2"])
+            self._linear(f, s["X2h"], p + "fc1_w", T, out16=s["FFh"], relu=True, drop=sga_site(n, 4))
+            self._linear(f, s["FFh"], p + "fc2_w", T, out32=s["S3"], res32=s["X2"], drop=sga_site(n, 5))
             self._call(f, "vqa_layernorm_fwd", s["S3"], self.p32[p + "ln3_g"], self.p32[p + "ln3_b"], s["OUT"],
                        s["OUTh"], s["MU3"], s["RS3"], T, D, 1e-5)
             y16 = s["OUTh"]
@@ -372,27 +429,33 @@ class VQAEngine:
             self.ready_marks.append((len(b), sg.offset + (sg.numel + 63) // 64 * 64))
         mark("pool_b")
         sc = 1.0 / math.sqrt(S.SGA_DHEAD)
+        ks = self.drop_scale if self.p_drop > 0.0 else 1.0      # relu-mask dX: kept elements carry 1/(1-p)
         for n in reversed(range(NB)):
             s, p = self.sga[n], f"sga{n}."
             dy = self.dY[n & 1]
             y16 = self.VIS16 if n == 0 else self.sga[n - 1]["OUTh"]
-            # norm3 + FFN
+            # norm3 + FFN: dA32 = grad of x + dropout3(ffn(x)) (the residual), dA16 = its dropout3 branch;
+            # the fc2 bias gradient (column sums of the branch) is fused into the LayerNorm backward
+            kp = []
             self._call(b, "vqa_layernorm_bwd", dy, s["S3"], s["MU3"], s["RS3"], self.p32[p + "ln3_g"], None,
-                       self.dA32, self.dA16, self.g32[p + "ln3_g"], self.g32[p + "ln3_b"], self.WS_NORM, T, D)
-            self._dw(b, self.dA16, s["FFh"], p + "fc2_w", T, bias_from=self.dA32, bias_bf16=False)
-            self._dx(b, self.dA16, p + "fc2_w", T, out16=self.dB16, mask16=s["FFh"])
+                       self.dA32, self.dA16, self.g32[p + "ln3_g"], self.g32[p + "ln3_b"], self.WS_NORM, T, D,
+                       self._dptr(sga_site(n, 5), kp), self.g32[p + "fc2_b"], extra=kp + [self.RNG])
+            self._dw(b, self.dA16, s["FFh"], p + "fc2_w", T)
+            self._dx(b, self.dA16, p + "fc2_w", T, out16=self.dB16, mask16=s["FFh"], alpha=ks)
             self._dw(b, self.dB16, s["X2h"], p + "fc1_w", T, bias_from=self.dB16)
             self._dx(b, self.dB16, p + "fc1_w", T, out32=self.dC32, res32=self.dA32)
             # norm2 + cross attention (q from x, k/v from y)
+            kp = []
             self._call(b, "vqa_layernorm_bwd", self.dC32, s["S2"], s["MU2"], s["RS2"], self.p32[p + "ln2_g"], None,
-                       self.dA32, self.dA16, self.g32[p + "ln2_g"], self.g32[p + "ln2_b"], self.WS_NORM, T, D)
-            self._dw(b, self.dA16, s["O2"], p + "m2_w", T, bias_from=self.dA32, bias_bf16=False)
+                       self.dA32, self.dA16, self.g32[p + "ln2_g"], self.g32[p + "ln2_b"], self.WS_NORM, T, D,
+                       self._dptr(sga_site(n, 3), kp), self.g32[p + "m2_b"], extra=kp + [self.RNG])
+            self._dw(b, self.dA16, s["O2"], p + "m2_w", T)
             self._dx(b, self.dA16, p + "m2_w", T, out16=self.dO16)
             kv = s["KV2"]
             self._attn(b, "vqa_attn_bwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
                        p=s["P2"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=s["lk"], dh=S.SGA_DHEAD, scale=sc,
                        dout=self.dO16, lddo=D, dq=self.dQ16, lddq=D, dk=self.dKV16, lddk=2 * D,
-                       dv=ops.addr(self.dKV16, D), lddv=2 * D)
+                       dv=ops.addr(self.dKV16, D), lddv=2 * D, drop=sga_site(n, 2))
             self._dw(b, self.dQ16, s["X1h"], p + "q2_w", T, bias_from=self.dQ16)
             self._dx(b, self.dQ16, p + "q2_w", T, out32=self.dC32, res32=self.dA32)
             self._dw(b, self.dKV16, y16, p + "kv2_w", s["ly"], bias_from=self.dKV16)
@@ -401,16 +464,18 @@ class VQAEngine:
             else:
                 self._dx(b, self.dKV16, p + "kv2_w", s["ly"], out32=self.dY[(n - 1) & 1])
             # norm1 + self attention
+            kp = []
             self._call(b, "vqa_layernorm_bwd", self.dC32, s["S1"], s["MU1"], s["RS1"], self.p32[p + "ln1_g"], None,
-                       self.dA32, self.dA16, self.g32[p + "ln1_g"], self.g32[p + "ln1_b"], self.WS_NORM, T, D)
-            self._dw(b, self.dA16, s["O1"], p + "m1_w", T, bias_from=self.dA32, bias_bf16=False)
+                       self.dA32, self.dA16, self.g32[p + "ln1_g"], self.g32[p + "ln1_b"], self.WS_NORM, T, D,
+                       self._dptr(sga_site(n, 1), kp), self.g32[p + "m1_b"], extra=kp + [self.RNG])
+            self._dw(b, self.dA16, s["O1"], p + "m1_w", T)
             self._dx(b, self.dA16, p + "m1_w", T, out16=self.dO16)
             q = s["QKV1"]
             dq = self.dQKV16
             self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, p=s["P1"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=Lq, dh=S.SGA_DHEAD, scale=sc,
                        dout=self.dO16, lddo=D, dq=dq, lddq=3 * D, dk=ops.addr(dq, D), lddk=3 * D,
-                       dv=ops.addr(dq, 2 * D), lddv=3 * D)
+                       dv=ops.addr(dq, 2 * D), lddv=3 * D, drop=sga_site(n, 0))
             self._dw(b, dq, self.TXT16, p + "qkv1_w", T, bias_from=dq)
             # text gradient accumulates over the three blocks (x is the T5 output for every block)
             self._dx(b, dq, p + "qkv1_w", T, out32=self.dTXT, res32=self.dA32, beta=0.0 if n == NB - 1 else 1.0)
@@ -422,17 +487,23 @@ class VQAEngine:
                    c32=self.g32["scaler_w"], ldc32=9 * cin, gb=g)
         self._call(b, "vqa_colsum", self.dVIS32, 0, self.V_TOK, D, D, self.g32["scaler_b"], 0.0, self.WS_COL)
         mark("scaler_b")
-        # T5 encoder backward
+        # T5 encoder backward.  dH32 is the gradient of the residual stream h_i; dH16 the
+        # dropout-masked gradient of the FF branch that produced it (T5LayerFF :140).
+        kp = []
         self._call(b, "vqa_rmsnorm_bwd", self.dTXT, self.HS[-1], self.RF, self.p32["t5.final_ln"], None, self.dH32,
-                   self.dH16, self.g32["t5.final_ln"], 0.0, self.WS_NORM, T, D)
+                   self.dH16, self.g32["t5.final_ln"], 0.0, self.WS_NORM, T, D,
+                   self._dptr(SITE_FINAL, kp), None, self._dptr(t5_site(S.T5_LAYERS - 1, 3), kp),
+                   extra=kp + [self.RNG])
         mark("t5.final_ln")
         for i in reversed(range(S.T5_LAYERS)):
             self._dw(b, self.dH16, self.FF[i], f"t5.{i}.wo", T)
-            self._dx(b, self.dH16, f"t5.{i}.wo", T, out16=self.dF16, mask16=self.FF[i])
+            self._dx(b, self.dH16, f"t5.{i}.wo", T, out16=self.dF16, mask16=self.FF[i], alpha=ks)
             self._dw(b, self.dF16, self.N1[i], f"t5.{i}.wi", T)
             self._dx(b, self.dF16, f"t5.{i}.wi", T, out32=self.dC32)
+            kp = []
             self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HM[i], self.R1[i], self.p32[f"t5.{i}.ln1"], self.dH32,
-                       self.dHM32, self.dHM16, self.g32[f"t5.{i}.ln1"], 0.0, self.WS_NORM, T, D)
+                       self.dHM32, self.dHM16, self.g32[f"t5.{i}.ln1"], 0.0, self.WS_NORM, T, D,
+                       None, None, self._dptr(t5_site(i, 1), kp), extra=kp + [self.RNG])
             self._dw(b, self.dHM16, self.O[i], f"t5.{i}.o_w", T)
             self._dx(b, self.dHM16, f"t5.{i}.o_w", T, out16=self.dO16)
             q = self.QKV[i]
@@ -440,14 +511,21 @@ class VQAEngine:
             self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B, heads=S.T5_HEADS, lq=Lq,
                        lk=Lq, dh=S.T5_DKV, scale=1.0, dout=self.dO16, lddo=D, dq=dq, lddq=3 * D,
-                       dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dSB)
+                       dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dSB,
+                       drop=t5_site(i, 0))
             # relative-position bias is shared by all 12 layers: dPB = sum_layers sum_b dS
             self._call(b, "vqa_batch_sum", self.dSB, B, S.T5_HEADS * Lq * Lq, self.dPB,
                        0.0 if i == S.T5_LAYERS - 1 else 1.0)
             self._dw(b, dq, self.N0[i], f"t5.{i}.qkv_w", T)
             self._dx(b, dq, f"t5.{i}.qkv_w", T, out32=self.dC32)
+            # layer 0: dH32 becomes the embedding gradient (masked by the embedding dropout :725);
+            # otherwise dH16 is the FF branch gradient of layer i-1
+            kp = []
+            d32 = self._dptr(SITE_EMBED, kp) if i == 0 else None
+            d16 = self._dptr(t5_site(i - 1, 3), kp) if i > 0 else None
             self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HS[i], self.R0[i], self.p32[f"t5.{i}.ln0"], self.dHM32,
-                       self.dH32, self.dH16, self.g32[f"t5.{i}.ln0"], 0.0, self.WS_NORM, T, D)
+                       self.dH32, self.dH16 if i > 0 else None, self.g32[f"t5.{i}.ln0"], 0.0, self.WS_NORM, T, D,
+                       None, d32, d16, extra=kp + [self.RNG])
             mark(f"t5.{i}.ln1")
         self._call(b, "vqa_t5_relbias_bwd", self.dPB, self.bucket, self.g32["t5.relbias"], S.T5_HEADS, Lq, Lq,
                    S.T5_BUCKETS)
@@ -533,7 +611,7 @@ class VQAEngine:
         all-reduce hook, graph(fwd+bwd) -> eager collective -> graph(optimizer)."""
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
-        saved = self.opt_state.clone()
+        saved, saved_rng = self.opt_state.clone(), self.RNG.clone()
         with torch.cuda.stream(s):
             if warm:                                    # warm-up launch outside capture
                 self.forward()
@@ -558,6 +636,7 @@ class VQAEngine:
             ar = self.allreduce
             parts = [g1, lambda: ar(self.G32), g2]
         self.opt_state.copy_(saved)
+        self.RNG.copy_(saved_rng)                       # the warm-up launch must not consume a dropout draw
         self.graph = parts
 
     # ------------------------------------------------------------------ readouts (tests / API)

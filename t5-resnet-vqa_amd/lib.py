@@ -25,6 +25,11 @@ class ConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("n", "h", "w", "c", "oh", "ow", "kh", "kw", "stride", "pad")]
 
 
+class Dropout(ctypes.Structure):
+    """vqa_dropout: p (0 = off), site id, device uint32[2] {seed, counter}."""
+    _fields_ = [("p", c_float), ("site", ctypes.c_uint), ("rng", c_void_p)]
+
+
 class GemmDesc(ctypes.Structure):
     _fields_ = [
         ("a", c_void_p), ("lda", c_ll), ("a_trans", c_int),
@@ -40,6 +45,7 @@ class GemmDesc(ctypes.Structure):
         ("b_conv", c_int), ("gb", ConvGeom),
         ("batch", c_int), ("stride_a", c_ll), ("stride_b", c_ll), ("stride_c32", c_ll),
         ("stride_c16", c_ll), ("stride_res", c_ll), ("config", c_int),
+        ("drop", Dropout),
     ]
 
 
@@ -50,6 +56,7 @@ class AttnDesc(ctypes.Structure):
         ("batch", c_int), ("heads", c_int), ("lq", c_int), ("lk", c_int), ("dh", c_int), ("scale", c_float),
         ("dout", c_void_p), ("lddo", c_ll), ("dq", c_void_p), ("lddq", c_ll), ("dk", c_void_p), ("lddk", c_ll),
         ("dv", c_void_p), ("lddv", c_ll), ("dbias", c_void_p),
+        ("drop", Dropout),
     ]
 
 
@@ -76,6 +83,10 @@ def header_symbols():
     return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(vqa_\w+)\s*\(", txt, re.M)))
 
 
+def abi_version():
+    return int(re.search(r"#define VQA_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+
+
 def load():
     global _lib
     if _lib is not None:
@@ -88,6 +99,8 @@ def load():
     if missing:
         raise RuntimeError(f"libvqa_hip.so lacks exported symbols {missing}")
     lib.vqa_last_error.restype = ctypes.c_char_p
+    if lib.vqa_abi_version() != abi_version():
+        raise RuntimeError(f"libvqa_hip.so ABI {lib.vqa_abi_version()} != header ABI {abi_version()}: rebuild it")
     lib.vqa_gemm.argtypes = [ctypes.POINTER(GemmDesc), c_void_p]
     lib.vqa_gemm_select.argtypes = [ctypes.POINTER(GemmDesc)]
     lib.vqa_attn_fwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
@@ -112,15 +125,17 @@ def register(name, *argtypes):
 
 
 P = c_void_p
-register("vqa_rmsnorm_fwd", P, P, P, P, P, c_int, c_int, c_float)
-register("vqa_rmsnorm_bwd", P, P, P, P, P, P, P, P, c_float, P, c_int, c_int)
+register("vqa_rmsnorm_fwd", P, P, P, P, P, c_int, c_int, c_float, P)
+register("vqa_rmsnorm_bwd", P, P, P, P, P, P, P, P, c_float, P, c_int, c_int, P, P, P)
 register("vqa_layernorm_fwd", P, P, P, P, P, P, P, c_int, c_int, c_float)
-register("vqa_layernorm_bwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int)
+register("vqa_layernorm_bwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P, P)
+register("vqa_rng_advance", P)
+register("vqa_dropout_mask", P, P, c_ll)
 register("vqa_colsum_partials", P, c_int, c_ll, c_int, P, c_float)
 register("vqa_image_to_nhwc8", P, P, c_int, c_int, c_int)
 register("vqa_maxpool3x3s2_nhwc", P, P, c_int, c_int, c_int, c_int, c_int, c_int)
 register("vqa_colsum", P, c_int, c_int, c_int, c_ll, P, c_float, P)
-register("vqa_embedding_fwd", P, P, P, c_int, c_int, c_int)
+register("vqa_embedding_fwd", P, P, P, c_int, c_int, c_int, P)
 register("vqa_embedding_bwd", P, P, P, c_int, c_int, c_int, P)
 register("vqa_t5_relbias_fwd", P, P, P, c_int, c_int, c_int)
 register("vqa_t5_relbias_bwd", P, P, P, c_int, c_int, c_int, c_int)

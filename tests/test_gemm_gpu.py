@@ -94,9 +94,33 @@ def test_beta_mask_bf16_residual_batched(ops):
                           alpha=0.5, beta=1.0, batch=Bt, stride_a=M * K, stride_b=N * K, stride_c32=M * N,
                           stride_res=M * N))
     torch.cuda.synchronize()
-    v = 0.5 * torch.bmm(a.float(), b.float().transpose(1, 2)) + res.float()
-    v = torch.where(mask.float() > 0, v, torch.zeros_like(v))
+    v = 0.5 * torch.bmm(a.float(), b.float().transpose(1, 2))
+    v = torch.where(mask.float() > 0, v, torch.zeros_like(v)) + res.float()     # the mask gates the product only
     close(c, v + c0, (a.float().abs() @ b.float().abs().transpose(1, 2)).max().item() + 10)
+
+
+@pytest.mark.parametrize("vec", [True, False])
+@pytest.mark.parametrize("relu", [False, True])
+def test_dropout_epilogue(ops, pkg, vec, relu):
+    """c = drop(alpha*A B^T + bias) + res (or relu(drop(.)) without res), masks = the oracle's hash."""
+    from oracle import vqa_oracle as orc
+    Bt, M, K = 2, 96, 128
+    N = 200 if vec else 198                      # odd-ish N takes the scalar epilogue
+    a, b = bf((Bt, M, K), seed=21), bf((Bt, N, K), seed=22)
+    bias = torch.randn(N, device="cuda")
+    res = None if relu else torch.randn(Bt, M, N, device="cuda")
+    rng = torch.tensor([5, 9], dtype=torch.int32, device="cuda")
+    c = torch.empty(Bt, M, N, device="cuda")
+    d = ops.gemm_desc(a, b, M, N, K, lda=K, ldb=K, c32=c, ldc32=N, bias=bias, res32=res, ldres=N, relu=relu,
+                      alpha=0.75, batch=Bt, stride_a=M * K, stride_b=N * K, stride_c32=M * N, stride_res=M * N)
+    d.drop = pkg.lib.Dropout(0.1, 33, rng.data_ptr())
+    ops.run(d)
+    torch.cuda.synchronize()
+    mult = torch.from_numpy(orc.dropout_multiplier(0.1, 5, 9, 33, Bt * M * N)).cuda().view(Bt, M, N)
+    v = (0.75 * torch.bmm(a.float(), b.float().transpose(1, 2)) + bias) * mult
+    v = torch.relu(v) if relu else v + res
+    close(c, v, (a.float().abs() @ b.float().abs().transpose(1, 2)).max().item() + 10)
+    assert ((c == 0) == (v == 0)).float().mean() > 0.999
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 3])

@@ -35,7 +35,7 @@ def test_rmsnorm_fwd_bwd(k, rows):
     dy, dres = rnd((rows, D), 3), rnd((rows, D), 4)
     y32, y16, rstd = torch.empty_like(x), torch.empty(rows, D, device="cuda", dtype=torch.bfloat16), \
         torch.empty(rows, device="cuda")
-    run(k, "vqa_rmsnorm_fwd", x, w, y32, y16, rstd, rows, D, 1e-6)
+    run(k, "vqa_rmsnorm_fwd", x, w, y32, y16, rstd, rows, D, 1e-6, None)
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     ref = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6))
@@ -43,7 +43,7 @@ def test_rmsnorm_fwd_bwd(k, rows):
     torch.testing.assert_close(y32, ref.detach(), rtol=1e-5, atol=1e-5)
     dx32, dx16, dw = torch.empty_like(x), torch.empty_like(y16), torch.empty(D, device="cuda")
     ws = torch.empty(k.lib.load().vqa_norm_bwd_workspace_floats(rows, D), device="cuda")
-    run(k, "vqa_rmsnorm_bwd", dy, x, rstd, w, dres, dx32, dx16, dw, 0.0, ws, rows, D)
+    run(k, "vqa_rmsnorm_bwd", dy, x, rstd, w, dres, dx32, dx16, dw, 0.0, ws, rows, D, None, None, None)
     torch.cuda.synchronize()
     torch.testing.assert_close(dx32, xr.grad + dres, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dw, wr.grad, rtol=1e-4, atol=1e-3)
@@ -63,26 +63,28 @@ def test_layernorm_fwd_bwd(k, rows):
     torch.testing.assert_close(y32, ref.detach(), rtol=1e-5, atol=1e-5)
     dx, dg, db = torch.empty_like(x), torch.empty(D, device="cuda"), torch.empty(D, device="cuda")
     ws = torch.empty(k.lib.load().vqa_norm_bwd_workspace_floats(rows, D), device="cuda")
-    run(k, "vqa_layernorm_bwd", dy, x, mu, rs, g, None, dx, None, dg, db, ws, rows, D)
+    run(k, "vqa_layernorm_bwd", dy, x, mu, rs, g, None, dx, None, dg, db, ws, rows, D, None, None)
     torch.cuda.synchronize()
     torch.testing.assert_close(dx, xr.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dg, gr.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-3)
 
 
-def attn_ref(q, kk, v, scale, bias, mask):
+def attn_ref(q, kk, v, scale, bias, mask, mult=None):
     s = q @ kk.transpose(-1, -2) * scale
     if bias is not None:
         s = s + bias
     if mask is not None:
         s = s + (1.0 - mask[:, None, None, :].float()) * torch.finfo(torch.float32).min
-    return torch.softmax(s, -1) @ v
+    p = torch.softmax(s, -1)
+    return (p if mult is None else p * mult) @ v
 
 
-@pytest.mark.parametrize("B,H,Lq,Lk,dh,t5", [(4, 8, 32, 49, 96, False), (4, 8, 32, 32, 96, False),
-                                              (3, 12, 32, 32, 64, True), (2, 8, 16, 64, 96, False),
-                                              (2, 12, 16, 16, 64, True)])
-def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5):
+@pytest.mark.parametrize("B,H,Lq,Lk,dh,t5,pd", [(4, 8, 32, 49, 96, False, 0.0), (4, 8, 32, 32, 96, False, 0.0),
+                                                 (3, 12, 32, 32, 64, True, 0.0), (2, 8, 16, 64, 96, False, 0.0),
+                                                 (2, 12, 16, 16, 64, True, 0.0), (4, 8, 32, 49, 96, False, 0.1),
+                                                 (3, 12, 32, 32, 64, True, 0.1)])
+def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5, pd):
     D = H * dh
     q16 = rnd((B * Lq, 3 * D), 10, dtype=torch.bfloat16)                   # fused qkv-like layout
     kv16 = rnd((B * Lk, 2 * D), 11, dtype=torch.bfloat16)
@@ -102,12 +104,18 @@ def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5):
     d.o, d.ldo, d.p = A(o), D, A(p)
     d.bias, d.key_mask = A(bias), A(mask)
     d.batch, d.heads, d.lq, d.lk, d.dh, d.scale = B, H, Lq, Lk, dh, scale
+    mult = None
+    if pd > 0:
+        from oracle import vqa_oracle as orc
+        rng = torch.tensor([11, 4], dtype=torch.int32, device="cuda")
+        d.drop = L.Dropout(pd, 77, rng.data_ptr())
+        mult = torch.from_numpy(orc.dropout_multiplier(pd, 11, 4, 77, B * H * Lq * Lk)).cuda().view(B, H, Lq, Lk)
     L.check(L.load().vqa_attn_fwd(ctypes.byref(d), L.stream_handle()), "fwd")
     qf = q16[:, :D].float().view(B, Lq, H, dh).transpose(1, 2).requires_grad_(True)
     kf = kv16[:, :D].float().view(B, Lk, H, dh).transpose(1, 2).requires_grad_(True)
     vf = kv16[:, D:].float().view(B, Lk, H, dh).transpose(1, 2).requires_grad_(True)
     bf = bias.clone().requires_grad_(True) if t5 else None
-    ref = attn_ref(qf, kf, vf, scale, bf, mask)
+    ref = attn_ref(qf, kf, vf, scale, bf, mask, mult)
     ref_o = ref.transpose(1, 2).reshape(B * Lq, D)
     torch.testing.assert_close(o.float(), ref_o.detach(), rtol=1e-2, atol=1e-2)
     ref_o.backward(do16.float())
@@ -167,7 +175,7 @@ def test_embedding_relbias_colsum_cast(k):
     ids[:50] = 7                                               # heavy duplicates
     table = rnd((Vv, D), 30)
     out = torch.empty(T, D, device="cuda")
-    run(k, "vqa_embedding_fwd", ids, table, out, T, D, Vv)
+    run(k, "vqa_embedding_fwd", ids, table, out, T, D, Vv, None)
     torch.testing.assert_close(out, table[ids])
     dh = rnd((T, D), 31)
     dt = torch.zeros(Vv, D, device="cuda")
@@ -256,3 +264,86 @@ def test_adamw_amsgrad_matches_torch(k):
         assert abs(st[1].item() - norm.item()) <= 1e-5 * norm.item()
         torch.testing.assert_close(p, torch.cat([t.detach() for t in ref_params]), rtol=1e-6, atol=1e-7)
     assert torch.equal(p16, p.to(torch.bfloat16))
+
+
+def test_dropout_mask_matches_oracle_hash(k):
+    """vqa_dropout_mask == the oracle's restatement of the counter hash, bit for bit."""
+    from oracle import vqa_oracle as orc
+    L = k.lib
+    for seed, ctr, site, p, n in [(0, 1, 1, 0.1, 100003), (123456789, 77, 150, 0.1, 4096),
+                                  (0xFFFFFFFF, 2**31 + 5, 16, 0.5, 5000), (3, 3, 3, 0.0, 64)]:
+        rng = torch.from_numpy(np.array([seed, ctr], np.uint32).view(np.int32)).cuda()
+        d = L.Dropout(p, site, rng.data_ptr())
+        out = torch.empty(n, device="cuda")
+        L.check(L.load().vqa_dropout_mask(ctypes.byref(d), ctypes.c_void_p(out.data_ptr()), n, L.stream_handle()),
+                "mask")
+        torch.cuda.synchronize()
+        ref = orc.dropout_multiplier(p, seed, ctr, site, n) if p > 0 else np.ones(n, np.float32)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    # law: keep rate 1-p, scale 1/(1-p); advancing the counter changes the mask
+    rng = torch.tensor([0, 0], dtype=torch.int32, device="cuda")
+    d = L.Dropout(0.1, 5, rng.data_ptr())
+    m0, m1 = torch.empty(1 << 20, device="cuda"), torch.empty(1 << 20, device="cuda")
+    L.load().vqa_dropout_mask(ctypes.byref(d), ctypes.c_void_p(m0.data_ptr()), 1 << 20, L.stream_handle())
+    run(k, "vqa_rng_advance", rng)
+    L.load().vqa_dropout_mask(ctypes.byref(d), ctypes.c_void_p(m1.data_ptr()), 1 << 20, L.stream_handle())
+    torch.cuda.synchronize()
+    assert int(rng[1]) == 1
+    keep0 = (m0 > 0).float().mean().item()
+    assert abs(keep0 - 0.9) < 2e-3, keep0
+    assert torch.all((m0 == 0) | (m0 == np.float32(1) / (np.float32(1) - np.float32(0.1))))
+    both = ((m0 > 0) & (m1 > 0)).float().mean().item()
+    assert abs(both - 0.81) < 3e-3, both                                # independent draws
+
+
+def test_norm_and_embedding_dropout_hooks(k):
+    from oracle import vqa_oracle as orc
+    L = k.lib
+    rows, D = 256, 768
+    rng = torch.tensor([9, 2], dtype=torch.int32, device="cuda")
+    mk = lambda site: L.Dropout(0.1, site, rng.data_ptr())
+    mult = lambda site: torch.from_numpy(orc.dropout_multiplier(0.1, 9, 2, site, rows * D)).cuda().view(rows, D)
+    dA, dB, dC = mk(40), mk(41), mk(42)
+    pa = lambda d: ctypes.addressof(d)
+    x, w = rnd((rows, D), 1), 1 + 0.1 * rnd(D, 2)
+    dy, dres = rnd((rows, D), 3), rnd((rows, D), 4)
+    y32, rstd = torch.empty_like(x), torch.empty(rows, device="cuda")
+    run(k, "vqa_rmsnorm_fwd", x, w, y32, None, rstd, rows, D, 1e-6, pa(dA))
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    ref = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6)) * mult(40)
+    ref.backward(dy)
+    torch.testing.assert_close(y32, ref.detach(), rtol=1e-5, atol=1e-5)
+    # backward of that dropout (drop_dy) + residual; masks on the two outputs
+    dx32, dx16, dw = torch.empty_like(x), torch.empty(rows, D, device="cuda", dtype=torch.bfloat16), \
+        torch.empty(D, device="cuda")
+    ws = torch.empty(L.load().vqa_norm_bwd_workspace_floats(rows, D), device="cuda")
+    run(k, "vqa_rmsnorm_bwd", dy, x, rstd, w, dres, dx32, dx16, dw, 0.0, ws, rows, D, pa(dA), pa(dB), pa(dC))
+    torch.cuda.synchronize()
+    full = xr.grad + dres
+    torch.testing.assert_close(dx32, full * mult(41), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dx16.float(), (full * mult(42)).to(torch.bfloat16).float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dw, wr.grad, rtol=1e-4, atol=1e-3)
+    # LayerNorm backward: branch gradient masked in bf16 + its fp32 column sums (fused bias grad)
+    g, b = 1 + 0.1 * rnd(D, 6), 0.1 * rnd(D, 7)
+    mu, rs = torch.empty(rows, device="cuda"), torch.empty(rows, device="cuda")
+    y = torch.empty_like(x)
+    run(k, "vqa_layernorm_fwd", x, g, b, y, None, mu, rs, rows, D, 1e-5)
+    xr, gr, br = (t.clone().requires_grad_(True) for t in (x, g, b))
+    F.layer_norm(xr, (D,), gr, br, 1e-5).backward(dy)
+    dx, dg, db, dsum = (torch.empty_like(x), torch.empty(D, device="cuda"), torch.empty(D, device="cuda"),
+                        torch.empty(D, device="cuda"))
+    run(k, "vqa_layernorm_bwd", dy, x, mu, rs, g, None, dx, dx16, dg, db, ws, rows, D, pa(dB), dsum)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dx, xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dx16.float(), (xr.grad * mult(41)).to(torch.bfloat16).float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dsum, (xr.grad * mult(41)).sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(dg, gr.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-3)
+    # embedding dropout
+    T, Vv = rows, 1000
+    ids = torch.randint(0, Vv, (T,), device="cuda")
+    table = rnd((Vv, D), 30)
+    out = torch.empty(T, D, device="cuda")
+    run(k, "vqa_embedding_fwd", ids, table, out, T, D, Vv, pa(dC))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, table[ids] * mult(42))

@@ -29,8 +29,9 @@ def test_engine_matches_reference_golden(cuda, pkg, golden, case, vision):
     B, L, H = int(g["B"]), int(g["L"]), int(g["H"])
     sd = pkg.synthetic.make_state_dict(vision, seed=0)
     nb = pkg.synthetic.make_batch(B, L, H, seed=1)
+    # the fixtures are eval-mode (dropout off): the reference's train-mode masks come from torch's RNG
     eng = pkg.engine.VQAEngine(sd, vision=vision, batch=B, seq_len=L, image_size=H, warmup=int(g["warmup"]),
-                               total=int(g["total"]))
+                               total=int(g["total"]), dropout=0.0)
     losses, norms = [], []
     for s in range(len(g["losses"])):
         lp, loss = eng.forward_backward(nb)
@@ -54,12 +55,15 @@ def test_engine_matches_reference_golden(cuda, pkg, golden, case, vision):
     assert (nrel <= 5e-2).all(), nrel
 
 
-def test_engine_vs_oracle_multistep(cuda, pkg):
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_engine_vs_oracle_multistep(cuda, pkg, p):
+    """Train-mode steps (p=0.1: the reference's dropout, masks from the shared
+    counter hash, restated in the oracle) and eval-mode steps (p=0)."""
     from oracle import vqa_oracle as orc
     B, L, H = 6, 32, 96
     sd = pkg.synthetic.make_state_dict("resnet50", seed=5)
-    eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=50)
-    ot = orc.OracleTrainer(sd, "resnet50", warmup=1, total=50)
+    eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=50, dropout=p, seed=7)
+    ot = orc.OracleTrainer(sd, "resnet50", warmup=1, total=50, dropout=p, seed=7)
     for step in range(3):
         nb = pkg.synthetic.make_batch(B, L, H, seed=10 + step)
         lp, loss = eng.forward_backward(nb)
@@ -74,7 +78,7 @@ def test_engine_vs_oracle_multistep(cuda, pkg):
 def test_state_dict_roundtrip_and_graph_replay(cuda, pkg):
     B, L, H = 2, 32, 64
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
-    eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=10)
+    eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=10, dropout=0.1, seed=3)
     out = eng.state_dict()
     assert list(out) == list(pkg.synthetic.model_specs("resnet50"))
     for kk in ("lang_model.block.3.layer.0.SelfAttention.k.weight", "downscale_layer.weight",
@@ -83,7 +87,7 @@ def test_state_dict_roundtrip_and_graph_replay(cuda, pkg):
     nb = pkg.synthetic.make_batch(B, L, H, seed=1)
     eng.load_batch(nb)
     # eager reference of two steps
-    eng2 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=10)
+    eng2 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=10, dropout=0.1, seed=3)
     eng2.load_batch(nb)
     for _ in range(3):
         eng2.train_step()
@@ -96,3 +100,19 @@ def test_state_dict_roundtrip_and_graph_replay(cuda, pkg):
     assert torch.equal(eng.M, eng2.M) and torch.equal(eng.VMAX, eng2.VMAX)
     assert float(eng.LOSS) == float(eng2.LOSS)
     assert float(eng.opt_state[0]) == 3.0
+    assert int(eng.RNG[1]) == 3 and int(eng2.RNG[1]) == 3          # one dropout draw per step
+
+
+def test_dropout_changes_step_to_step(cuda, pkg):
+    """Fresh masks every replayed step: the same batch gives a different loss in train mode."""
+    B, L, H = 2, 16, 64
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=5, total=10, dropout=0.1)
+    nb = pkg.synthetic.make_batch(B, L, H, seed=1)
+    _, l1 = eng.forward_backward(nb)
+    _, l2 = eng.forward_backward(nb)        # lr is 0 before any optimizer step: only the masks differ
+    assert l1 != l2
+    e0 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=5, total=10, dropout=0.0)
+    _, a = e0.forward_backward(nb)
+    _, b = e0.forward_backward(nb)
+    assert a == b
