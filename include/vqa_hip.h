@@ -93,12 +93,13 @@ typedef struct vqa_gemm_desc {
   int a_conv; vqa_conv_geom ga;
   int b_conv; vqa_conv_geom gb;
   int batch; long long stride_a, stride_b, stride_c32, stride_c16, stride_res;
-  int config;              /* 0 auto; 1: 128x128 tile; 2: 128x64; 3: 64x64; 4: 64x64 2-stage (tuning) */
+  int config;              /* 0 auto, else a tile config 1..VQA_GEMM_CONFIGS (speed only: results are identical) */
   vqa_dropout drop;        /* dropout of the (alpha*acc + bias) branch, before the residual */
 } vqa_gemm_desc;
 
+#define VQA_GEMM_CONFIGS 8
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
-/* tile configuration (1..4) that vqa_gemm would run for this descriptor */
+/* tile configuration (1..VQA_GEMM_CONFIGS) that vqa_gemm would run for this descriptor */
 int vqa_gemm_select(const vqa_gemm_desc* d);
 
 /* ------------------------------------------------------------- attention ---
@@ -186,7 +187,7 @@ int vqa_colsum_workspace_floats(int rows, int cols);
 /* drop: T5 embedding dropout (TF :725) on out (element token*d + col); NULL = none */
 int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int tokens, int d, int vocab,
                       const vqa_dropout* drop, hipStream_t stream);
-/* deterministic: each touched row is written once (sorted, fixed token order); tokens <= 8192; ws = 2*tokens ints */
+/* deterministic: each touched row is written once (sorted, fixed token order); tokens <= 8192; ws = 3*tokens ints */
 int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab, int* ws,
                       hipStream_t stream);
 int vqa_t5_relbias_fwd(const float* table, const int* bucket, float* out, int heads, int lq, int lk,

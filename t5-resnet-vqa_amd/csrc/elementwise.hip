@@ -117,11 +117,13 @@ __global__ __launch_bounds__(256) void dropout_mask_kernel(vqa_dropout d, float*
 
 // Deterministic dense embedding gradient (nn.Embedding sparse=False), no atomics:
 //   1. one workgroup bitonic-sorts the keys (id << 16 | position) in LDS, which
-//      groups equal ids with their positions in token order;
-//   2. one workgroup per sorted slot: the first slot of each id-run sums the
-//      run's dh rows in that fixed order and writes the table row once.
+//      groups equal ids with their positions in token order, and finds each
+//      id-run's end with a max-scan of the run starts (no serial run walks);
+//   2. one workgroup per (run start, column slab) sums the run's dh rows in
+//      that fixed order and writes the table row once.
 // Bit-identical run to run (DP ranks stay in lockstep, graph replay == eager).
-// ws: [0, T) sorted positions, [T, 2T) sorted ids (clamped).
+// ws: [0, T) sorted positions, [T, 2T) sorted ids (clamped), [2T, 3T) run end
+// (valid at run starts).
 __global__ __launch_bounds__(1024) void embedding_sort_kernel(const long long* __restrict__ ids, int tokens, int vocab,
                                                               int* __restrict__ ws) {
   extern __shared__ unsigned long long key[];
@@ -150,9 +152,38 @@ __global__ __launch_bounds__(1024) void embedding_sort_kernel(const long long* _
       __syncthreads();
     }
   }
+  // run starts: flag[t] = t if id(t) != id(t-1) else 0 (t = 0 always starts)
+  constexpr int MAXT = 8192 / 1024;
+  int st[MAXT];
+#pragma unroll
+  for (int q = 0; q < MAXT; ++q) {
+    const int t = threadIdx.x + q * 1024;
+    st[q] = 0;
+    if (t < tokens) {
+      const unsigned long long kt = key[t];
+      ws[t] = (int)(kt & 0xffff);
+      ws[tokens + t] = (int)(kt >> 16);
+      st[q] = (t == 0 || (key[t - 1] >> 16) != (kt >> 16)) ? t : 0;
+    }
+  }
+  __syncthreads();                                      // keys are dead from here: reuse LDS as 2 int arrays
+  int* s0 = reinterpret_cast<int*>(key);
+  int* s1 = s0 + n;
+#pragma unroll
+  for (int q = 0; q < MAXT; ++q) {
+    const int t = threadIdx.x + q * 1024;
+    if (t < n) s0[t] = st[q];
+  }
+  __syncthreads();
+  // inclusive max-scan: start(t) = the last run start <= t
+  for (int off = 1; off < n; off <<= 1) {
+    for (int t = threadIdx.x; t < n; t += blockDim.x) s1[t] = t >= off ? max(s0[t], s0[t - off]) : s0[t];
+    __syncthreads();
+    int* tmp = s0; s0 = s1; s1 = tmp;
+  }
   for (int t = threadIdx.x; t < tokens; t += blockDim.x) {
-    ws[t] = (int)(key[t] & 0xffff);
-    ws[tokens + t] = (int)(key[t] >> 16);
+    const int a = s0[t];
+    if (t == tokens - 1 || s0[t + 1] != a) ws[2 * tokens + a] = t + 1;      // t is the last of its run
   }
 }
 
@@ -171,17 +202,28 @@ __global__ __launch_bounds__(EMB_RL * EMB_CL) void embedding_bwd_kernel(const fl
   const int* sid = ws + tokens;
   const int id = sid[s0];
   if (s0 > 0 && sid[s0 - 1] == id) return;           // not the first slot of its run (uniform per block)
-  int s1 = s0 + 1;
-  while (s1 < tokens && sid[s1] == id) ++s1;
+  const int s1 = ws[2 * tokens + s0];                   // run end from the sort kernel's scan
   const int tx = threadIdx.x % EMB_CL, ty = threadIdx.x / EMB_CL;
   const int c4 = blockIdx.y * EMB_CL + tx;             // float4 column
   const bool act = c4 * 4 < d;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (act) {
-#pragma unroll 4
-    for (int u = s0 + ty; u < s1; u += EMB_RL) {
-      const float4 v = reinterpret_cast<const float4*>(dh + (long)pos[u] * d)[c4];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    // 8 rows per batch: all position loads, then all row loads, are issued before
+    // the first add, so a long run costs ~len/128 round trips, not len/16
+    constexpr int U = 8;
+    for (int u0 = s0 + ty; u0 < s1; u0 += EMB_RL * U) {
+      // unconditional loads (index clamped into the run), the tail masked on the values:
+      // a per-load branch would serialise the round trips
+      int pp[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) pp[q] = pos[min(u0 + q * EMB_RL, s1 - 1)];
+      float4 v[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) v[q] = reinterpret_cast<const float4*>(dh + (long)pp[q] * d)[c4];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        if (u0 + q * EMB_RL < s1) { acc.x += v[q].x; acc.y += v[q].y; acc.z += v[q].z; acc.w += v[q].w; }
+      }
     }
   }
   __shared__ float4 red[EMB_RL][EMB_CL];

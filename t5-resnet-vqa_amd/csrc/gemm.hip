@@ -472,18 +472,20 @@ int launch(GemmParams& P, int batch, hipStream_t s) {
   return vqa::check_launch("vqa_gemm");
 }
 
-// config: 0 = auto; 1 = 128x128 (3 stages); 2 = 128x64 (4); 3 = 64x64 (4); 4 = 64x64 (2)
-// Auto (measured on MI355X, tools/gemm_tune.py): the LDS-DMA fill rate per CU
-// grows with resident waves, so 64x64 tiles at 2 blocks/CU win almost
-// everywhere at this model's sizes; 128x128 only pays for narrow-N, long-K
-// convolutions (half the operand re-reads); with <= 2 K-tiles the ring is
-// useless and a 2-stage ring doubles the resident blocks.
+// config: 0 = auto; 1 = 128x128 (3 stages); 2 = 128x64 (4); 3 = 64x64 (4); 4 = 64x64 (2);
+//         5 = 64x64 (3); 6 = 128x64 (2); 7 = 64x128 (2); 8 = 128x128 (2).
+// Every config accumulates each output element in the same K order (BK = 64
+// k-tiles, 16-deep MFMA steps), so the choice changes speed, never the bits.
+// Auto (measured on MI355X, tools/callprof.py): fewer stages = less LDS = more
+// resident blocks, which beats a deep ring at this model's sizes; 128-wide
+// tiles only pay for narrow-N, long-K convolutions.  Engines autotune per call.
 int auto_config(int m, int n, int k, int batch) {
   const long t128 = (long)vqa::cdiv(m, 128) * vqa::cdiv(n, 128) * batch;
   const int nk = vqa::cdiv(k, BK);
   if (nk <= 2) return 4;
   if (n <= 256 && k >= 1024 && t128 >= 128) return 1;
-  return 3;
+  if (k >= 2048) return 3;
+  return 4;
 }
 
 template <bool AKC, bool BKC, bool GA, bool GB>
@@ -493,6 +495,10 @@ int dispatch_tile(GemmParams& P, int batch, int config, hipStream_t s) {
     case 1: return launch<128, 128, 3, AKC, BKC, GA, GB>(P, batch, s);
     case 2: return launch<128, 64, 4, AKC, BKC, GA, GB>(P, batch, s);
     case 4: return launch<64, 64, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 5: return launch<64, 64, 3, AKC, BKC, GA, GB>(P, batch, s);
+    case 6: return launch<128, 64, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 7: return launch<64, 128, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 8: return launch<128, 128, 2, AKC, BKC, GA, GB>(P, batch, s);
     default: return launch<64, 64, 4, AKC, BKC, GA, GB>(P, batch, s);
   }
 }
@@ -521,7 +527,7 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   VQA_REQUIRE(!d->a_conv || d->ga.c % 8 == 0, "vqa_gemm: conv input channels must be a multiple of 8");
   VQA_REQUIRE(!d->b_conv || d->gb.c % 8 == 0, "vqa_gemm: conv input channels must be a multiple of 8");
   VQA_REQUIRE(d->batch >= 1, "vqa_gemm: batch must be >= 1");
-  VQA_REQUIRE(d->config >= 0 && d->config <= 4, "vqa_gemm: config must be 0..4");
+  VQA_REQUIRE(d->config >= 0 && d->config <= VQA_GEMM_CONFIGS, "vqa_gemm: config must be 0..%d", VQA_GEMM_CONFIGS);
   VQA_REQUIRE(d->drop.p >= 0.f && d->drop.p < 1.f, "vqa_gemm: dropout p must be in [0, 1)");
   VQA_REQUIRE(!(d->drop.p > 0.f && d->drop.rng && d->relu && (d->res32 || d->res16)),
               "vqa_gemm: relu + residual + dropout is not a supported epilogue");

@@ -79,7 +79,7 @@ class DataParallelStep:
         dev = e.dev
         self.GIDS = torch.zeros(self.world * T, dtype=torch.int64, device=dev)
         self.GDH = torch.zeros(self.world * T, D, dtype=torch.float32, device=dev)
-        self.WS = torch.empty(2 * self.world * T, dtype=torch.int32, device=dev)
+        self.WS = torch.empty(3 * self.world * T, dtype=torch.int32, device=dev)
         self.emb_call = ops.Call("vqa_embedding_bwd", self.GIDS.data_ptr(), self.GDH.data_ptr(),
                                  e.g32["t5.embed"].data_ptr(), self.world * T, D, S.T5_VOCAB, self.WS.data_ptr(),
                                  keep=(self.GIDS, self.GDH, self.WS, e.g32["t5.embed"]))

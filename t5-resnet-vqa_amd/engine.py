@@ -56,6 +56,22 @@ def sga_site(block, kind):
     return 128 + 8 * block + kind
 
 
+_TUNE_CACHE = {}
+
+
+def lib_gemm_configs():
+    import re
+    return int(re.search(r"#define VQA_GEMM_CONFIGS (\d+)", open(L.HEADER).read()).group(1))
+
+
+def _gemm_key(d):
+    geo = lambda g: (g.n, g.h, g.w, g.c, g.oh, g.ow, g.kh, g.kw, g.stride, g.pad)
+    return (d.m, d.n, d.k, d.batch, d.a_trans, d.b_trans, d.a_conv, d.b_conv,
+            geo(d.ga) if d.a_conv else None, geo(d.gb) if d.b_conv else None,
+            bool(d.c32), bool(d.c16), bool(d.bias), bool(d.res32), bool(d.res16), bool(d.mask16), d.relu,
+            d.beta != 0.0, d.drop.p > 0.0)
+
+
 class VQAEngine:
     def __init__(self, state_dict, vision="resnet50", batch=64, seq_len=32, image_size=224, device="cuda:0",
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
@@ -82,6 +98,7 @@ class VQAEngine:
             self._plan_optimizer()
         self.graph = None
         self.allreduce = None            # set by the DP trainer: fn(G32 tensor) on the current stream
+        self._side = torch.cuda.Stream(self.dev)
 
     @classmethod
     def from_state_dict(cls, sd, **kw):
@@ -260,10 +277,11 @@ class VQAEngine:
         self.dHM32, self.dHM16 = t((T, D)), t((T, D), BF16)
         self.dPB = t((S.T5_HEADS, Lq, Lq), zero=True)
         self.dSB = t((B, S.T5_HEADS, Lq, Lq))             # per-sample attention dS (rel-bias grad)
-        self.WS_EMB = t(2 * T, torch.int32)
+        self.WS_EMB = t(3 * T, torch.int32)
         lib = L.load()
         self.WS_NORM = t(lib.vqa_norm_bwd_workspace_floats(T, D))
         self.WS_COL = t(lib.vqa_colsum_workspace_floats(mx, 3 * D))
+        self.WS_COL2 = t(lib.vqa_colsum_workspace_floats(V, D))
         self.WS_HEAD = t(lib.vqa_head_workspace_floats(B, Lq, D, self.A))
         self.SQ_PARTS = 1024
         self.WS_SQ = t(self.SQ_PARTS, torch.float64)
@@ -344,13 +362,15 @@ class VQAEngine:
         B, Lq, T = self.B, self.L, self.T
         if self.p_drop > 0.0:                                # fresh dropout masks every step
             self._call(f, "vqa_rng_advance", self.RNG)
+        self._fsplit = [len(f)]                              # [pre | vision | text | fusion]
         f += self.res_calls
         # ConvTranspose2d scaler as implicit GEMM over the layer4 map (+bias) -> vision tokens
         cin, fh = self.fc, self.fh
         g = ops.conv_geom(B, fh, fh, cin, fh, fh, 3, 3, 1, 1)
         self._gemm(f, self.F4, self.p16["scaler_w"], self.V_TOK, D, 9 * cin, lda=9 * cin, ldb=9 * cin, ga=g,
                    c32=self.VIS32, ldc32=D, c16=self.VIS16, ldc16=D, bias=self.p32["scaler_b"])
-        # T5 encoder
+        # T5 encoder (independent of the vision branch until the SGA blocks)
+        self._fsplit.append(len(f))
         kp = []
         self._call(f, "vqa_embedding_fwd", self.IDS, self.p32["t5.embed"], self.HS[0], T, D, S.T5_VOCAB,
                    self._dptr(SITE_EMBED, kp), extra=kp + [self.RNG])
@@ -375,6 +395,7 @@ class VQAEngine:
         kp = []
         self._call(f, "vqa_rmsnorm_fwd", self.HS[-1], self.p32["t5.final_ln"], self.TXT32, self.TXT16, self.RF, T, D,
                    1e-6, self._dptr(SITE_FINAL, kp), extra=kp + [self.RNG])
+        self._fsplit.append(len(f))
         # SGA blocks: x = text always, y chained
         y16 = self.VIS16
         sc = 1.0 / math.sqrt(S.SGA_DHEAD)
@@ -481,12 +502,15 @@ class VQAEngine:
             self._dx(b, dq, p + "qkv1_w", T, out32=self.dTXT, res32=self.dA32, beta=0.0 if n == NB - 1 else 1.0)
             mark(f"sga{n}.ln3_b")
         # ConvTranspose2d scaler weight/bias gradient: implicit im2col of layer4 as the B operand
+        # (vision branch: independent of the T5 backward below; its own colsum workspace)
+        self._bsplit = [len(b)]
         cin, fh = self.fc, self.fh
         g = ops.conv_geom(B, fh, fh, cin, fh, fh, 3, 3, 1, 1)
         self._gemm(b, self.dVIS16, self.F4, D, 9 * cin, self.V_TOK, lda=D, ldb=9 * cin, a_trans=True, b_trans=True,
                    c32=self.g32["scaler_w"], ldc32=9 * cin, gb=g)
-        self._call(b, "vqa_colsum", self.dVIS32, 0, self.V_TOK, D, D, self.g32["scaler_b"], 0.0, self.WS_COL)
+        self._call(b, "vqa_colsum", self.dVIS32, 0, self.V_TOK, D, D, self.g32["scaler_b"], 0.0, self.WS_COL2)
         mark("scaler_b")
+        self._bsplit.append(len(b))
         # T5 encoder backward.  dH32 is the gradient of the residual stream h_i; dH16 the
         # dropout-masked gradient of the FF branch that produced it (T5LayerFF :140).
         kp = []
@@ -591,6 +615,41 @@ class VQAEngine:
     def optimizer_step(self):
         self._run(self.opt_calls)
 
+    def _run_step_streams(self, optimizer=True):
+        """One step with graph-level concurrency: the frozen-ResNet + ConvTranspose2d
+        branch and the T5 encoder run on two streams in the forward (they meet at
+        SGA block 0), and the scaler weight gradient overlaps the T5 backward.
+        Buffers of the two branches are disjoint, so the result is the same as
+        the sequential order (and bit-identical: no cross-branch reductions)."""
+        main = torch.cuda.current_stream(self.dev)
+        side = self._side
+        f, b = self.fwd_calls, self.bwd_calls
+        p0, p1, p2 = self._fsplit
+        q0, q1 = self._bsplit
+        self._run(f[:p0])                                  # rng advance
+        fork = torch.cuda.Event()
+        fork.record(main)
+        side.wait_event(fork)
+        with torch.cuda.stream(side):
+            self._run(f[p1:p2])                            # T5 encoder
+        self._run(f[p0:p1])                                # ResNet + ConvTranspose2d
+        join = torch.cuda.Event()
+        join.record(side)
+        main.wait_event(join)
+        self._run(f[p2:])                                  # SGA + head
+        self._run(b[:q0])                                  # head + SGA backward
+        fork2 = torch.cuda.Event()
+        fork2.record(main)
+        side.wait_event(fork2)
+        with torch.cuda.stream(side):
+            self._run(b[q0:q1])                            # scaler dW / db
+        self._run(b[q1:])                                  # T5 backward + embedding
+        join2 = torch.cuda.Event()
+        join2.record(side)
+        main.wait_event(join2)
+        if optimizer:
+            self._run(self.opt_calls)
+
     def train_step(self):
         """zero_grad -> forward -> backward -> (all-reduce) -> clip -> AdamW -> sched, all on-device."""
         if self.graph is not None:
@@ -622,9 +681,7 @@ class VQAEngine:
         if self.allreduce is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
-                self.forward()
-                self.backward()
-                self.optimizer_step()
+                self._run_step_streams()
             parts = [g]
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -638,6 +695,43 @@ class VQAEngine:
         self.opt_state.copy_(saved)
         self.RNG.copy_(saved_rng)                       # the warm-up launch must not consume a dropout draw
         self.graph = parts
+
+    # ------------------------------------------------------------------ GEMM autotuning
+    def autotune(self, reps=5):
+        """Pick the fastest tile config for every prepared GEMM by timing them in
+        place (HIP events).  Configs differ only in speed: each output element is
+        accumulated in the same K order whatever the tile, so results (and DP
+        rank agreement) do not depend on the choice.  Run after a batch is
+        loaded and one forward/backward has filled the activations; it
+        scribbles only on buffers the next step recomputes."""
+        s = L.stream_handle()
+        lib = L.load()
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        chosen = {}
+        for c in self.fwd_calls + self.bwd_calls:
+            if c.name != "vqa_gemm":
+                continue
+            d = c.desc
+            key = _gemm_key(d)
+            if key not in _TUNE_CACHE:
+                best = None
+                for cfg in range(1, lib_gemm_configs() + 1):
+                    d.config = cfg
+                    c(s)
+                    st.record()
+                    for _ in range(reps):
+                        c(s)
+                    en.record()
+                    en.synchronize()
+                    t = st.elapsed_time(en)
+                    if best is None or t < best[0]:
+                        best = (t, cfg)
+                _TUNE_CACHE[key] = best[1]
+            d.config = _TUNE_CACHE[key]
+            chosen[key] = d.config
+        torch.cuda.synchronize(self.dev)
+        self.graph = None
+        return chosen
 
     # ------------------------------------------------------------------ readouts (tests / API)
     def forward_backward(self, batch):

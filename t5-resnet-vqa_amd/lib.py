@@ -60,6 +60,10 @@ class AttnDesc(ctypes.Structure):
     ]
 
 
+# vqa_gemm tile configs (gemm.hip dispatch_tile): config -> (BM, BN, LDS stages)
+GEMM_TILES = {1: (128, 128, 3), 2: (128, 64, 4), 3: (64, 64, 4), 4: (64, 64, 2), 5: (64, 64, 3), 6: (128, 64, 2),
+              7: (64, 128, 2), 8: (128, 128, 2)}
+
 MAX_GROUPS = 8
 ST_STEP, ST_GRAD_NORM, ST_CLIP_COEF, ST_LR_SCALE, ST_BC1, ST_BC2_SQRT = range(6)
 

@@ -164,3 +164,48 @@ def test_conv_weight_grad_gather(ops, n, h, c, co, cfg):
     cols = cols.view(n, c, 9, h * h).permute(0, 3, 2, 1).reshape(n * h * h, K9)   # [(n,h,w), (tap, c)]
     ref = dy.float().T @ cols
     close(out, ref, (dy.float().abs().T @ cols.abs()).max().item())
+
+
+@pytest.mark.parametrize("layout", ["AB", "ABt", "AtBt", "AtB", "conv", "convw"])
+def test_all_tile_configs_bitwise_identical(ops, pkg, layout):
+    """Tile configs are a speed choice only: every config accumulates each output
+    element in the same K order, so outputs are bit-identical (engines autotune
+    per call and DP ranks may pick differently without diverging)."""
+    n_cfg = max(pkg.lib.GEMM_TILES)
+    rng = torch.tensor([1, 2], dtype=torch.int32, device="cuda")
+    if layout in ("conv", "convw"):
+        nb, h, c, co = 2, 14, 64, 96
+        x = bf((nb, h, h, c), seed=31)
+        g = ops.conv_geom(nb, h, h, c, h, h, 3, 3, 1, 1)
+        if layout == "conv":
+            wt = bf((co, 3, 3, c), 0.05, seed=32)
+            M, N, K = nb * h * h, co, 9 * c
+            mk = lambda out: ops.gemm_desc(x, wt, M, N, K, lda=K, ldb=K, c32=out, ldc32=N, relu=True, ga=g)
+        else:
+            dy = bf((nb * h * h, co), seed=33)
+            M, N, K = co, 9 * c, nb * h * h
+            mk = lambda out: ops.gemm_desc(dy, x, M, N, K, lda=co, ldb=9 * c, a_trans=True, b_trans=True, c32=out,
+                                           ldc32=N, gb=g)
+    else:
+        M, N, K = 328, 264, 776
+        at, bt = layout in ("AtBt", "AtB"), layout in ("ABt", "AtBt")
+        a = bf((K, M) if at else (M, K), seed=34)
+        b = bf((K, N) if bt else (N, K), seed=35)
+        bias = torch.randn(N, device="cuda")
+        res = torch.randn(M, N, device="cuda")
+
+        def mk(out):
+            d = ops.gemm_desc(a, b, M, N, K, lda=M if at else K, ldb=N if bt else K, a_trans=at, b_trans=bt,
+                              c32=out, ldc32=N, bias=bias, res32=res, ldres=N)
+            d.drop = pkg.lib.Dropout(0.1, 3, rng.data_ptr())
+            return d
+    outs = []
+    for cfg in range(1, n_cfg + 1):
+        out = torch.empty(M, N, device="cuda")
+        d = mk(out)
+        d.config = cfg
+        ops.run(d)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for cfg, o in enumerate(outs[1:], start=2):
+        assert torch.equal(o, outs[0]), f"config {cfg} differs from config 1"

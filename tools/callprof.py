@@ -29,6 +29,8 @@ eng.load_batch(pkg.synthetic.make_batch(B, 32, 224, seed=1))
 eng.forward()
 eng.backward()
 torch.cuda.synchronize()
+if "--autotune" in sys.argv:
+    eng.autotune()
 s = L.stream_handle()
 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
