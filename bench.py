@@ -74,6 +74,9 @@ def main():
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--tune-table", default=os.path.join(ROOT, "t5-resnet-vqa_amd", "tuning", "gemm_gfx950.json"),
+                    help="measured GEMM tile choices (missing shapes are timed at start-up)")
+    ap.add_argument("--tune-save", default=None, help="write the tile choices used to this file")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -99,7 +102,7 @@ def main():
     eng.load_batch(pool[0])
     eng.forward()
     eng.backward()
-    eng.autotune()                                               # per-call GEMM tile choice (speed only)
+    eng.autotune(table=args.tune_table, save=args.tune_save if rank == 0 else None)   # tile choice: speed only
     if world > 1:
         dps = pkg.dp.DataParallelStep(eng, use_graph=not args.no_graph)
         run_step = dps.step

@@ -45,7 +45,7 @@ struct GemmParams {
   vqa_conv_geom ga, gb;
   long sa, sb, sc32, sc16, sres;
   int tiles_m, tiles_n;
-  int vec;                 // 4-wide vector epilogue legal (N, ld*, pointers aligned)
+  int vec;                 // LDS-staged 8-wide epilogue legal (N, ld*, pointers 16-B aligned)
   vqa_dropout drop;        // dropout of the (alpha*acc + bias) branch
 };
 
@@ -332,9 +332,6 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
   // Per element: k = [mask > 0] * dropout multiplier (1 if neither), then
   //   v = k*(alpha*acc + bias) + res ; relu ; c32 = v + beta*c32 ; c16 = bf16(v).
   // (relu(k*t) == k*relu(t) for k >= 0, and with a residual relu acts after it.)
-  // All inputs (bias, residual, mask, old C) are loaded and the keep factors
-  // computed before any store so the loads stay in flight (C may alias them as
-  // far as the compiler knows); keep factors travel as a 4-bit mask per group.
   float* C32 = P.c32 ? P.c32 + (long)z * P.sc32 : nullptr;
   bf16_t* C16 = P.c16 ? P.c16 + (long)z * P.sc16 : nullptr;
   const float* R32 = P.res32 ? P.res32 + (long)z * P.sres : nullptr;
@@ -342,100 +339,109 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
   const bf16_t* MK = P.mask16 ? P.mask16 + (long)z * P.sres : nullptr;
   const bool beta = P.beta != 0.f && C32;
   const DropK dk = drop_init(P.drop);
-  const float kscale = dk.on ? dk.scale : 1.f;       // multiplier of a kept element
   const uint32_t ebase = (uint32_t)z * (uint32_t)P.m;  // dropout element index = (z*m + row)*n + col
   const int rl = l & 31, ch = l >> 5;
   if (P.vec) {
-    float4 add[TM][TN][4];
-    uint32_t kb[TM][TN][4];
+    // Staged through LDS (the ring is idle now): each wave parks alpha*acc of its
+    // fragments as fp32 rows, then all 256 threads walk the tile row-major, 8
+    // columns (16-32 B) per thread, so every global access -- bias, residual,
+    // mask, old C, the stores -- is a full coalesced line instead of 16-B
+    // pieces of 32 rows.  Two passes of BM/2 rows keep the image <= 64 KiB.
+    constexpr int LDR = BN + 4;                         // fp32 row stride (+16 B: spreads the banks)
+    constexpr int HALF = BM / 2;
+    static_assert(HALF * LDR * 4 <= STAGES * ST_BYTES, "epilogue image must fit the ring");
+    float* img = reinterpret_cast<float*>(smem);
+    constexpr int TPR = BN / 8;                         // threads per row
+    constexpr int RPP = NT / TPR;                       // rows per sweep
+    // __syncthreads (waits for this wave's LDS ops, then barriers); no LDS-DMA is in flight now
+    __syncthreads();                                    // every wave is done with the ring
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int pass = 0; pass < 2; ++pass) {
+      if (wm == pass) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int row = m0 + wm * WM + i * 32 + rl;
-          const int col = n0 + wn * WN + j * 32 + 8 * g + 4 * ch;
-          float4 a4 = make_float4(0.f, 0.f, 0.f, 0.f);
-          uint32_t bits = 0xf;
-          if (row < P.m && col < P.n) {
-            if (MK) {
-              const uint2 m2 = *reinterpret_cast<const uint2*>(MK + (long)row * P.ldmask + col);
-              bits = (bf2f(m2.x & 0xffff) > 0.f ? 1u : 0u) | (bf2f(m2.x >> 16) > 0.f ? 2u : 0u) |
-                     (bf2f(m2.y & 0xffff) > 0.f ? 4u : 0u) | (bf2f(m2.y >> 16) > 0.f ? 8u : 0u);
-            }
-            if (dk.on) {
-              const uint32_t e = (ebase + (uint32_t)row) * (uint32_t)P.n + (uint32_t)col;
+          for (int j = 0; j < TN; ++j)
 #pragma unroll
-              for (int t = 0; t < 4; ++t)
-                if (!drop_keep(dk, e + t)) bits &= ~(1u << t);
+            for (int g = 0; g < 4; ++g) {
+              const int r = i * 32 + rl, c = wn * WN + j * 32 + 8 * g + 4 * ch;
+              *reinterpret_cast<float4*>(img + r * LDR + c) =
+                  make_float4(acc[i][j][4 * g] * P.alpha, acc[i][j][4 * g + 1] * P.alpha,
+                              acc[i][j][4 * g + 2] * P.alpha, acc[i][j][4 * g + 3] * P.alpha);
             }
-            if (P.bias) {
-              a4 = *reinterpret_cast<const float4*>(P.bias + col);
-              a4.x *= (bits & 1) ? kscale : 0.f; a4.y *= (bits & 2) ? kscale : 0.f;
-              a4.z *= (bits & 4) ? kscale : 0.f; a4.w *= (bits & 8) ? kscale : 0.f;
-            }
-            if (R32) {
-              const float4 r = *reinterpret_cast<const float4*>(R32 + (long)row * P.ldres + col);
-              a4.x += r.x; a4.y += r.y; a4.z += r.z; a4.w += r.w;
-            }
-            if (R16) {
-              const uint2 r = *reinterpret_cast<const uint2*>(R16 + (long)row * P.ldres + col);
-              a4.x += bf2f(r.x & 0xffff); a4.y += bf2f(r.x >> 16); a4.z += bf2f(r.y & 0xffff); a4.w += bf2f(r.y >> 16);
-            }
-          }
-          add[i][j][g] = a4;
-          kb[i][j][g] = bits;
+      }
+      __syncthreads();                                  // the fragment writes have landed
+      const int c = (tid % TPR) * 8, col = n0 + c;
+#pragma unroll
+      for (int r0 = 0; r0 < HALF; r0 += RPP) {
+        const int r = r0 + tid / TPR, row = m0 + pass * HALF + r;
+        if (HALF % RPP != 0 && r >= HALF) continue;
+        if (row >= P.m || col >= P.n) continue;
+        const float4 x0 = *reinterpret_cast<const float4*>(img + r * LDR + c);
+        const float4 x1 = *reinterpret_cast<const float4*>(img + r * LDR + c + 4);
+        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        float kf[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) kf[t] = 1.f;
+        if (MK) {
+          const uint4 m4 = *reinterpret_cast<const uint4*>(MK + (long)row * P.ldmask + col);
+          const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            if (!(bf2f((t & 1) ? (mw[t >> 1] >> 16) : (mw[t >> 1] & 0xffff)) > 0.f)) kf[t] = 0.f;
         }
-    float4 old[TM][TN][4];
-    if (beta) {
+        if (dk.on) {
+          const uint32_t e = (ebase + (uint32_t)row) * (uint32_t)P.n + (uint32_t)col;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+          for (int t = 0; t < 8; ++t) kf[t] *= drop_mul(dk, e + t);
+        }
+        if (P.bias) {
+          const float4 b0 = *reinterpret_cast<const float4*>(P.bias + col);
+          const float4 b1 = *reinterpret_cast<const float4*>(P.bias + col + 4);
+          const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+          for (int t = 0; t < 8; ++t) v[t] += bb[t];
+        }
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int row = m0 + wm * WM + i * 32 + rl;
-            const int col = n0 + wn * WN + j * 32 + 8 * g + 4 * ch;
-            old[i][j][g] = (row < P.m && col < P.n) ? *reinterpret_cast<const float4*>(C32 + (long)row * P.ldc32 + col)
-                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int t = 0; t < 8; ++t) v[t] *= kf[t];
+        if (R32) {
+          const float4 a0 = *reinterpret_cast<const float4*>(R32 + (long)row * P.ldres + col);
+          const float4 a1 = *reinterpret_cast<const float4*>(R32 + (long)row * P.ldres + col + 4);
+          v[0] += a0.x; v[1] += a0.y; v[2] += a0.z; v[3] += a0.w;
+          v[4] += a1.x; v[5] += a1.y; v[6] += a1.z; v[7] += a1.w;
+        }
+        if (R16) {
+          const uint4 q = *reinterpret_cast<const uint4*>(R16 + (long)row * P.ldres + col);
+          const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int t = 0; t < 8; ++t) v[t] += bf2f((t & 1) ? (qw[t >> 1] >> 16) : (qw[t >> 1] & 0xffff));
+        }
+        if (P.relu) {
+#pragma unroll
+          for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+        }
+        if (C32) {
+          float4* cp = reinterpret_cast<float4*>(C32 + (long)row * P.ldc32 + col);
+          float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
+          if (beta) {
+            const float4 c0 = cp[0], c1 = cp[1];
+            o0.x += P.beta * c0.x; o0.y += P.beta * c0.y; o0.z += P.beta * c0.z; o0.w += P.beta * c0.w;
+            o1.x += P.beta * c1.x; o1.y += P.beta * c1.y; o1.z += P.beta * c1.z; o1.w += P.beta * c1.w;
           }
+          cp[0] = o0;
+          cp[1] = o1;
+        }
+        if (C16) {
+          uint4 u;
+          u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+          u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+          *reinterpret_cast<uint4*>(C16 + (long)row * P.ldc16 + col) = u;
+        }
+      }
+      if (pass == 0) __syncthreads();                   // image reused by the second half
     }
-    const float ak = P.alpha * kscale;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int row = m0 + wm * WM + i * 32 + rl;
-          const int col = n0 + wn * WN + j * 32 + 8 * g + 4 * ch;
-          if (row >= P.m || col >= P.n) continue;
-          const float4 a4 = add[i][j][g];
-          const uint32_t bits = kb[i][j][g];
-          float v[4] = {acc[i][j][4 * g] * ((bits & 1) ? ak : 0.f) + a4.x,
-                        acc[i][j][4 * g + 1] * ((bits & 2) ? ak : 0.f) + a4.y,
-                        acc[i][j][4 * g + 2] * ((bits & 4) ? ak : 0.f) + a4.z,
-                        acc[i][j][4 * g + 3] * ((bits & 8) ? ak : 0.f) + a4.w};
-          if (P.relu) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
-          }
-          if (C32) {
-            float4 o = make_float4(v[0], v[1], v[2], v[3]);
-            if (beta) {
-              const float4 c = old[i][j][g];
-              o.x += P.beta * c.x; o.y += P.beta * c.y; o.z += P.beta * c.z; o.w += P.beta * c.w;
-            }
-            *reinterpret_cast<float4*>(C32 + (long)row * P.ldc32 + col) = o;
-          }
-          if (C16) {
-            uint2 u;
-            u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-            u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-            *reinterpret_cast<uint2*>(C16 + (long)row * P.ldc16 + col) = u;
-          }
-        }
   } else {
     // generic scalar path (odd N or leading dimensions)
 #pragma unroll
@@ -545,11 +551,11 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   P.drop = d->drop;
   const int batch = d->batch, cfg = d->config;
   auto al = [](const void* p, int bytes) { return p == nullptr || ((uintptr_t)p % bytes) == 0; };
-  P.vec = d->n % 4 == 0 && (!d->c32 || (d->ldc32 % 4 == 0 && al(d->c32, 16) && d->stride_c32 % 4 == 0)) &&
-          (!d->c16 || (d->ldc16 % 4 == 0 && al(d->c16, 8) && d->stride_c16 % 4 == 0)) &&
-          (!d->res32 || (d->ldres % 4 == 0 && al(d->res32, 16))) && (!d->res16 || (d->ldres % 4 == 0 && al(d->res16, 8))) &&
-          (!d->mask16 || (d->ldmask % 4 == 0 && al(d->mask16, 8))) && (!(d->res32 || d->res16 || d->mask16) || d->stride_res % 4 == 0) &&
-          al(d->bias, 16);
+  P.vec = d->n % 8 == 0 && (!d->c32 || (d->ldc32 % 8 == 0 && al(d->c32, 16) && d->stride_c32 % 8 == 0)) &&
+          (!d->c16 || (d->ldc16 % 8 == 0 && al(d->c16, 16) && d->stride_c16 % 8 == 0)) &&
+          (!d->res32 || (d->ldres % 8 == 0 && al(d->res32, 16))) && (!d->res16 || (d->ldres % 8 == 0 && al(d->res16, 16))) &&
+          (!d->mask16 || (d->ldmask % 8 == 0 && al(d->mask16, 16))) &&
+          (!(d->res32 || d->res16 || d->mask16) || d->stride_res % 8 == 0) && al(d->bias, 16);
   const bool akc = !d->a_trans, bkc = !d->b_trans;
   if (akc && bkc && !d->a_conv) return dispatch_tile<true, true, false, false>(P, batch, cfg, stream);
   if (akc && bkc && d->a_conv) return dispatch_tile<true, true, true, false>(P, batch, cfg, stream);

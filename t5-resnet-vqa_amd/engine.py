@@ -99,6 +99,8 @@ class VQAEngine:
         self.graph = None
         self.allreduce = None            # set by the DP trainer: fn(G32 tensor) on the current stream
         self._side = torch.cuda.Stream(self.dev)
+        self._wside = torch.cuda.Stream(self.dev)
+        self.dw_stream = False
 
     @classmethod
     def from_state_dict(cls, sd, **kw):
@@ -263,18 +265,14 @@ class VQAEngine:
         # backward temporaries (reused layer to layer)
         mx = max(T, V)
         self.dY = [t((T, D)), t((T, D))]
-        self.dA32, self.dA16 = t((T, D)), t((T, D), BF16)
-        self.dB32, self.dB16 = t((T, D)), t((T, D), BF16)
+        self.dA32 = t((T, D))
+        self._gbufs = {}
         self.dC32 = t((T, D))
         self.dO16 = t((T, D), BF16)
-        self.dQKV16 = t((T, 3 * D), BF16)
-        self.dQ16 = t((T, D), BF16)
-        self.dKV16 = t((mx, 2 * D), BF16)
-        self.dF16 = t((T, S.T5_DFF), BF16)
         self.dTXT = t((T, D))
         self.dVIS32, self.dVIS16 = t((V, D)), t((V, D), BF16)
-        self.dH32, self.dH16 = t((T, D)), t((T, D), BF16)
-        self.dHM32, self.dHM16 = t((T, D)), t((T, D), BF16)
+        self.dH32 = t((T, D))
+        self.dHM32 = t((T, D))
         self.dPB = t((S.T5_HEADS, Lq, Lq), zero=True)
         self.dSB = t((B, S.T5_HEADS, Lq, Lq))             # per-sample attention dS (rel-bias grad)
         self.WS_EMB = t(3 * T, torch.int32)
@@ -347,14 +345,24 @@ class VQAEngine:
         self._gemm(lst, dy16, w, m, k, n, lda=n, ldb=k, b_trans=True, c32=out32, ldc32=k, c16=out16, ldc16=k,
                    res32=res32, ldres=k, mask16=mask16, ldmask=k, beta=beta, alpha=alpha)
 
+    def _gbuf(self, name, shape):
+        """A bf16 backward buffer private to one use (see _plan_backward)."""
+        if name not in self._gbufs:
+            self._gbufs[name] = self._t(shape, BF16)
+        return self._gbufs[name]
+
     def _dw(self, lst, dy16, x16, wname, rows, bias_from=None, bias_bf16=True):
-        """dW[n, k] = dY[rows, n]^T X[rows, k]; optional bias grad = colsum(dY)."""
+        """dW[n, k] = dY[rows, n]^T X[rows, k]; optional bias grad = colsum(dY).
+        Tagged `side`: nothing on the dX chain reads them, so the step graph runs
+        them on a third stream beside the chain (joined before the optimizer)."""
         g = self.g32[wname]
         n, k = g.shape
         self._gemm(lst, dy16, x16, n, k, rows, lda=n, ldb=k, a_trans=True, b_trans=True, c32=g, ldc32=k)
+        lst[-1].side = True
         if bias_from is not None:
             self._call(lst, "vqa_colsum", bias_from, int(bias_bf16), rows, n, n, self.g32[wname[:-1] + "b"], 0.0,
                        self.WS_COL)
+            lst[-1].side = True
 
     # ------------------------------------------------------------------ forward plan
     def _plan_forward(self):
@@ -455,44 +463,50 @@ class VQAEngine:
             s, p = self.sga[n], f"sga{n}."
             dy = self.dY[n & 1]
             y16 = self.VIS16 if n == 0 else self.sga[n - 1]["OUTh"]
+            # every bf16 gradient a weight-gradient GEMM reads gets its own buffer, so the dW
+            # GEMMs can trail the dX chain on another stream without write-after-read hazards
+            g = lambda nm, shape: self._gbuf(f"{p}{nm}", shape)
+            dA3, dA2, dA1 = g("dA3", (T, D)), g("dA2", (T, D)), g("dA1", (T, D))
+            dB, dQ = g("dB", (T, D)), g("dQ", (T, D))
+            dKV, dQKV = g("dKV", (s["ly"], 2 * D)), g("dQKV", (T, 3 * D))
             # norm3 + FFN: dA32 = grad of x + dropout3(ffn(x)) (the residual), dA16 = its dropout3 branch;
             # the fc2 bias gradient (column sums of the branch) is fused into the LayerNorm backward
             kp = []
             self._call(b, "vqa_layernorm_bwd", dy, s["S3"], s["MU3"], s["RS3"], self.p32[p + "ln3_g"], None,
-                       self.dA32, self.dA16, self.g32[p + "ln3_g"], self.g32[p + "ln3_b"], self.WS_NORM, T, D,
+                       self.dA32, dA3, self.g32[p + "ln3_g"], self.g32[p + "ln3_b"], self.WS_NORM, T, D,
                        self._dptr(sga_site(n, 5), kp), self.g32[p + "fc2_b"], extra=kp + [self.RNG])
-            self._dw(b, self.dA16, s["FFh"], p + "fc2_w", T)
-            self._dx(b, self.dA16, p + "fc2_w", T, out16=self.dB16, mask16=s["FFh"], alpha=ks)
-            self._dw(b, self.dB16, s["X2h"], p + "fc1_w", T, bias_from=self.dB16)
-            self._dx(b, self.dB16, p + "fc1_w", T, out32=self.dC32, res32=self.dA32)
+            self._dw(b, dA3, s["FFh"], p + "fc2_w", T)
+            self._dx(b, dA3, p + "fc2_w", T, out16=dB, mask16=s["FFh"], alpha=ks)
+            self._dw(b, dB, s["X2h"], p + "fc1_w", T, bias_from=dB)
+            self._dx(b, dB, p + "fc1_w", T, out32=self.dC32, res32=self.dA32)
             # norm2 + cross attention (q from x, k/v from y)
             kp = []
             self._call(b, "vqa_layernorm_bwd", self.dC32, s["S2"], s["MU2"], s["RS2"], self.p32[p + "ln2_g"], None,
-                       self.dA32, self.dA16, self.g32[p + "ln2_g"], self.g32[p + "ln2_b"], self.WS_NORM, T, D,
+                       self.dA32, dA2, self.g32[p + "ln2_g"], self.g32[p + "ln2_b"], self.WS_NORM, T, D,
                        self._dptr(sga_site(n, 3), kp), self.g32[p + "m2_b"], extra=kp + [self.RNG])
-            self._dw(b, self.dA16, s["O2"], p + "m2_w", T)
-            self._dx(b, self.dA16, p + "m2_w", T, out16=self.dO16)
+            self._dw(b, dA2, s["O2"], p + "m2_w", T)
+            self._dx(b, dA2, p + "m2_w", T, out16=self.dO16)
             kv = s["KV2"]
             self._attn(b, "vqa_attn_bwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
                        p=s["P2"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=s["lk"], dh=S.SGA_DHEAD, scale=sc,
-                       dout=self.dO16, lddo=D, dq=self.dQ16, lddq=D, dk=self.dKV16, lddk=2 * D,
-                       dv=ops.addr(self.dKV16, D), lddv=2 * D, drop=sga_site(n, 2))
-            self._dw(b, self.dQ16, s["X1h"], p + "q2_w", T, bias_from=self.dQ16)
-            self._dx(b, self.dQ16, p + "q2_w", T, out32=self.dC32, res32=self.dA32)
-            self._dw(b, self.dKV16, y16, p + "kv2_w", s["ly"], bias_from=self.dKV16)
+                       dout=self.dO16, lddo=D, dq=dQ, lddq=D, dk=dKV, lddk=2 * D,
+                       dv=ops.addr(dKV, D), lddv=2 * D, drop=sga_site(n, 2))
+            self._dw(b, dQ, s["X1h"], p + "q2_w", T, bias_from=dQ)
+            self._dx(b, dQ, p + "q2_w", T, out32=self.dC32, res32=self.dA32)
+            self._dw(b, dKV, y16, p + "kv2_w", s["ly"], bias_from=dKV)
             if n == 0:
-                self._dx(b, self.dKV16, p + "kv2_w", s["ly"], out32=self.dVIS32, out16=self.dVIS16)
+                self._dx(b, dKV, p + "kv2_w", s["ly"], out32=self.dVIS32, out16=self.dVIS16)
             else:
-                self._dx(b, self.dKV16, p + "kv2_w", s["ly"], out32=self.dY[(n - 1) & 1])
+                self._dx(b, dKV, p + "kv2_w", s["ly"], out32=self.dY[(n - 1) & 1])
             # norm1 + self attention
             kp = []
             self._call(b, "vqa_layernorm_bwd", self.dC32, s["S1"], s["MU1"], s["RS1"], self.p32[p + "ln1_g"], None,
-                       self.dA32, self.dA16, self.g32[p + "ln1_g"], self.g32[p + "ln1_b"], self.WS_NORM, T, D,
+                       self.dA32, dA1, self.g32[p + "ln1_g"], self.g32[p + "ln1_b"], self.WS_NORM, T, D,
                        self._dptr(sga_site(n, 1), kp), self.g32[p + "m1_b"], extra=kp + [self.RNG])
-            self._dw(b, self.dA16, s["O1"], p + "m1_w", T)
-            self._dx(b, self.dA16, p + "m1_w", T, out16=self.dO16)
+            self._dw(b, dA1, s["O1"], p + "m1_w", T)
+            self._dx(b, dA1, p + "m1_w", T, out16=self.dO16)
             q = s["QKV1"]
-            dq = self.dQKV16
+            dq = dQKV
             self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, p=s["P1"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=Lq, dh=S.SGA_DHEAD, scale=sc,
                        dout=self.dO16, lddo=D, dq=dq, lddq=3 * D, dk=ops.addr(dq, D), lddk=3 * D,
@@ -513,25 +527,28 @@ class VQAEngine:
         self._bsplit.append(len(b))
         # T5 encoder backward.  dH32 is the gradient of the residual stream h_i; dH16 the
         # dropout-masked gradient of the FF branch that produced it (T5LayerFF :140).
+        g = lambda nm, shape: self._gbuf(nm, shape)
+        dH16 = [g(f"t5.{i}.dH", (T, D)) for i in range(S.T5_LAYERS)]     # FF-branch grad of layer i
         kp = []
         self._call(b, "vqa_rmsnorm_bwd", self.dTXT, self.HS[-1], self.RF, self.p32["t5.final_ln"], None, self.dH32,
-                   self.dH16, self.g32["t5.final_ln"], 0.0, self.WS_NORM, T, D,
+                   dH16[-1], self.g32["t5.final_ln"], 0.0, self.WS_NORM, T, D,
                    self._dptr(SITE_FINAL, kp), None, self._dptr(t5_site(S.T5_LAYERS - 1, 3), kp),
                    extra=kp + [self.RNG])
         mark("t5.final_ln")
         for i in reversed(range(S.T5_LAYERS)):
-            self._dw(b, self.dH16, self.FF[i], f"t5.{i}.wo", T)
-            self._dx(b, self.dH16, f"t5.{i}.wo", T, out16=self.dF16, mask16=self.FF[i], alpha=ks)
-            self._dw(b, self.dF16, self.N1[i], f"t5.{i}.wi", T)
-            self._dx(b, self.dF16, f"t5.{i}.wi", T, out32=self.dC32)
+            dF, dHM, dQKV = g(f"t5.{i}.dF", (T, S.T5_DFF)), g(f"t5.{i}.dHM", (T, D)), g(f"t5.{i}.dQKV", (T, 3 * D))
+            self._dw(b, dH16[i], self.FF[i], f"t5.{i}.wo", T)
+            self._dx(b, dH16[i], f"t5.{i}.wo", T, out16=dF, mask16=self.FF[i], alpha=ks)
+            self._dw(b, dF, self.N1[i], f"t5.{i}.wi", T)
+            self._dx(b, dF, f"t5.{i}.wi", T, out32=self.dC32)
             kp = []
             self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HM[i], self.R1[i], self.p32[f"t5.{i}.ln1"], self.dH32,
-                       self.dHM32, self.dHM16, self.g32[f"t5.{i}.ln1"], 0.0, self.WS_NORM, T, D,
+                       self.dHM32, dHM, self.g32[f"t5.{i}.ln1"], 0.0, self.WS_NORM, T, D,
                        None, None, self._dptr(t5_site(i, 1), kp), extra=kp + [self.RNG])
-            self._dw(b, self.dHM16, self.O[i], f"t5.{i}.o_w", T)
-            self._dx(b, self.dHM16, f"t5.{i}.o_w", T, out16=self.dO16)
+            self._dw(b, dHM, self.O[i], f"t5.{i}.o_w", T)
+            self._dx(b, dHM, f"t5.{i}.o_w", T, out16=self.dO16)
             q = self.QKV[i]
-            dq = self.dQKV16
+            dq = dQKV
             self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B, heads=S.T5_HEADS, lq=Lq,
                        lk=Lq, dh=S.T5_DKV, scale=1.0, dout=self.dO16, lddo=D, dq=dq, lddq=3 * D,
@@ -548,7 +565,7 @@ class VQAEngine:
             d32 = self._dptr(SITE_EMBED, kp) if i == 0 else None
             d16 = self._dptr(t5_site(i - 1, 3), kp) if i > 0 else None
             self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HS[i], self.R0[i], self.p32[f"t5.{i}.ln0"], self.dHM32,
-                       self.dH32, self.dH16 if i > 0 else None, self.g32[f"t5.{i}.ln0"], 0.0, self.WS_NORM, T, D,
+                       self.dH32, dH16[i - 1] if i > 0 else None, self.g32[f"t5.{i}.ln0"], 0.0, self.WS_NORM, T, D,
                        None, d32, d16, extra=kp + [self.RNG])
             mark(f"t5.{i}.ln1")
         self._call(b, "vqa_t5_relbias_bwd", self.dPB, self.bucket, self.g32["t5.relbias"], S.T5_HEADS, Lq, Lq,
@@ -637,18 +654,44 @@ class VQAEngine:
         join.record(side)
         main.wait_event(join)
         self._run(f[p2:])                                  # SGA + head
-        self._run(b[:q0])                                  # head + SGA backward
+        wside = self._wside
+        self._run_tagged(b[:q0], main, wside)              # head + SGA backward (dW beside the chain)
         fork2 = torch.cuda.Event()
         fork2.record(main)
         side.wait_event(fork2)
         with torch.cuda.stream(side):
             self._run(b[q0:q1])                            # scaler dW / db
-        self._run(b[q1:])                                  # T5 backward + embedding
-        join2 = torch.cuda.Event()
-        join2.record(side)
-        main.wait_event(join2)
+        self._run_tagged(b[q1:], main, wside)              # T5 backward + embedding
+        for st in (side, wside):
+            join2 = torch.cuda.Event()
+            join2.record(st)
+            main.wait_event(join2)
         if optimizer:
             self._run(self.opt_calls)
+
+    def _run_tagged(self, calls, main, wside):
+        """Run `calls` in order on `main`, except runs of side-tagged calls (weight
+        gradients), which go to `wside` after an event on `main` at that point.
+        Off by default (`dw_stream`): measured on MI355X, each cross-stream edge
+        inside the graph costs ~10-20 us of idle time on the chain, more than
+        the overlap gains at this model's sizes."""
+        if not self.dw_stream:
+            self._run(calls)
+            return
+        i, n = 0, len(calls)
+        while i < n:
+            j = i
+            while j < n and calls[j].side == calls[i].side:
+                j += 1
+            if calls[i].side:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                wside.wait_event(ev)
+                with torch.cuda.stream(wside):
+                    self._run(calls[i:j])
+            else:
+                self._run(calls[i:j])
+            i = j
 
     def train_step(self):
         """zero_grad -> forward -> backward -> (all-reduce) -> clip -> AdamW -> sched, all on-device."""
@@ -697,13 +740,18 @@ class VQAEngine:
         self.graph = parts
 
     # ------------------------------------------------------------------ GEMM autotuning
-    def autotune(self, reps=5):
+    def autotune(self, reps=5, table=None, save=None):
         """Pick the fastest tile config for every prepared GEMM by timing them in
         place (HIP events).  Configs differ only in speed: each output element is
         accumulated in the same K order whatever the tile, so results (and DP
         rank agreement) do not depend on the choice.  Run after a batch is
         loaded and one forward/backward has filled the activations; it
         scribbles only on buffers the next step recomputes."""
+        import json
+        import os
+        if table and os.path.exists(table):                # measured table (tools: bench --tune-save)
+            for k, v in json.load(open(table)).items():
+                _TUNE_CACHE.setdefault(k, int(v))
         s = L.stream_handle()
         lib = L.load()
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -712,7 +760,7 @@ class VQAEngine:
             if c.name != "vqa_gemm":
                 continue
             d = c.desc
-            key = _gemm_key(d)
+            key = repr(_gemm_key(d))
             if key not in _TUNE_CACHE:
                 best = None
                 for cfg in range(1, lib_gemm_configs() + 1):
@@ -731,6 +779,8 @@ class VQAEngine:
             chosen[key] = d.config
         torch.cuda.synchronize(self.dev)
         self.graph = None
+        if save:
+            json.dump(dict(sorted(chosen.items())), open(save, "w"), indent=0)
         return chosen
 
     # ------------------------------------------------------------------ readouts (tests / API)

@@ -64,7 +64,7 @@ class Call:
     `keep` must reference every tensor whose device address is baked into
     `args`: the call only stores raw addresses, and a tensor freed behind its
     back would hand its memory to the next allocation (use-after-free)."""
-    __slots__ = ("fn", "args", "name", "keep", "desc")
+    __slots__ = ("fn", "args", "name", "keep", "desc", "side")
 
     def __init__(self, name, *args, keep=None, desc=None):
         lib = L.load()
@@ -73,6 +73,7 @@ class Call:
         self.args = args
         self.keep = keep            # tensors (and structures) that must outlive the call
         self.desc = desc            # ctypes descriptor passed by reference, if any
+        self.side = False           # may run on a side stream (off the critical chain), see engine
 
     def __call__(self, stream_ptr):
         rc = self.fn(*self.args, stream_ptr)

@@ -42,3 +42,13 @@ for g, n in gaps[:12]:
 import collections
 hist = collections.Counter(min(int(g / 1000), 10) for g, _ in gaps)
 print("gap histogram (us bucket: count):", dict(sorted(hist.items())))
+
+# per-kernel-family time inside the step window
+fam = collections.defaultdict(lambda: [0, 0])
+for s, e, n, q in win:
+    key = n.replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "")[:70]
+    fam[key][0] += e - s
+    fam[key][1] += 1
+print("\nper kernel (one step):")
+for k, (t, c) in sorted(fam.items(), key=lambda kv: -kv[1][0])[:30]:
+    print(f"  {t / 1e3:8.1f} us  {c:4d}x  {k}")
