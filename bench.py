@@ -136,14 +136,31 @@ def main():
     loss = float(eng.LOSS.item())
     gnorm = eng.last_grad_norm()
 
-    # dominant single launch: the ConvTranspose2d weight-gradient implicit GEMM (its gather-B
-    # instantiation is used by no other call): M=768, N=9*2048, K=B*49, 2*M*N*K FLOP per launch
+    # Roofline of the dominant single launch: the fused AdamW-amsgrad pass (HBM-bound; the
+    # longest kernel of the step).  Algorithmic bytes per launch: read p, g, m, v, vmax (20 B)
+    # + write p, m, v, vmax (16 B) + the bf16 shadow (2 B) per parameter.  Timed with HIP
+    # events on its launch stream; re-running it after the timed region only re-applies
+    # the last update.  HBM traffic comes from the committed rocprofv3 PMC passes
+    # (tools/pmc_traffic.py) when present.
     from vqa_amd import lib as VL
+    stream = torch.cuda.current_stream(dev)
+    adam_call = eng.opt_calls[-1]
+    assert adam_call.name == "vqa_adamw_amsgrad"
+    n_par = eng.lay.total
+    adam_bytes = 38.0 * n_par
+    adam_dur = time_kernel(adam_call, 10, stream)
+    adam_gbs = adam_bytes / adam_dur / 1e9
+    pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        pmc = json.load(open(pmc_path))
+    # second roofline: the largest MFMA launch, the ConvTranspose2d weight-gradient implicit
+    # GEMM (M=768, N=9*2048, K=B*49; 2*M*N*K FLOP)
     wg_call = next(c for c in eng.bwd_calls if c.name == "vqa_gemm" and c.desc.b_conv == 1)
     cfg = VL.load().vqa_gemm_select(wg_call.desc)
     bm, bn, st = VL.GEMM_TILES[cfg]
     kname = f"gemm_kernel<{bm}, {bn}, {st}, false, false, false, true> (ConvTranspose2d dW implicit GEMM)"
-    kdur = time_kernel(wg_call, 20, torch.cuda.current_stream(dev))
+    kdur = time_kernel(wg_call, 20, stream)
     kflop = 2.0 * wg_call.desc.m * wg_call.desc.n * wg_call.desc.k
     k_tflops = kflop / kdur / 1e12
 
@@ -158,11 +175,18 @@ def main():
                    "model": "resnet50+t5-base+3xSGA", "global_batch": world * B, "per_gpu_batch": B,
                    "seq_len": L, "image_size": H, "answers": 170, "parallelism": f"dp{world}",
                    "graph": not args.no_graph},
-        "roofline": {"bound": "mfma", "kernel": kname,
-                     "achieved": round(k_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(k_tflops / MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel_avg_us": round(kdur * 1e6, 2), "flop_per_launch": kflop,
-                     "step_mfma_frac": round(value / world * FLOP_PER_PAIR / (MFMA_PEAK_TFLOPS * 1e12), 4)},
+        "roofline": {"bound": "hbm", "kernel": "adamw_kernel (fused clip-scaled AdamW-amsgrad + bf16 shadow)",
+                     "achieved": round(adam_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(adam_gbs / HBM_PEAK_GBS, 4),
+                     "traffic": (round(pmc["adamw_kernel"]["traffic_bytes"]) if "adamw_kernel" in pmc else None),
+                     "algorithmic_bytes": adam_bytes, "kernel_avg_us": round(adam_dur * 1e6, 2),
+                     "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"},
+        "roofline_mfma": {"bound": "mfma", "kernel": kname,
+                          "achieved": round(k_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": round(k_tflops / MFMA_PEAK_TFLOPS, 4),
+                          "traffic": (round(pmc["convT_dW"]["traffic_bytes"]) if "convT_dW" in pmc else None),
+                          "kernel_avg_us": round(kdur * 1e6, 2), "flop_per_launch": kflop,
+                          "step_mfma_frac": round(value / world * FLOP_PER_PAIR / (MFMA_PEAK_TFLOPS * 1e12), 4)},
         "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

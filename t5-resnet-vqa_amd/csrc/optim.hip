@@ -62,43 +62,46 @@ struct AdamArgs {
   const float* st;
 };
 
+// One float4 of every stream per thread, no grid-stride loop: 138k blocks of
+// 256 keep ~2k threads x 5 x 16 B of loads in flight per CU.  Every stream is
+// touched once per step (5.4 GB >> the 256 MiB Infinity Cache), so loads and
+// stores are non-temporal.
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs A) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= A.n4) return;
   const float coef = A.st[VQA_ST_CLIP_COEF], lam = A.st[VQA_ST_LR_SCALE];
   const float bc1 = A.st[VQA_ST_BC1], bc2s = A.st[VQA_ST_BC2_SQRT];
   const float gmul = A.gscale * coef;
   const float omb1 = 1.f - A.b1, omb2 = 1.f - A.b2;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < A.n4; i += (long)gridDim.x * 256) {
-    int gi = 0;
+  int gi = 0;
 #pragma unroll
-    for (int k = 0; k < VQA_MAX_GROUPS - 1; ++k) gi += (k < A.ngroups - 1 && i >= A.gend4[k]) ? 1 : 0;
-    const float lr = A.glr[gi] * lam;
-    const float decay = 1.f - lr * A.wd, step_size = lr / bc1;
-    float4 p = reinterpret_cast<float4*>(A.p)[i];
-    const float4 g4 = reinterpret_cast<const float4*>(A.g)[i];
-    float4 m = reinterpret_cast<float4*>(A.m)[i];
-    float4 v = reinterpret_cast<float4*>(A.v)[i];
-    float4 vm = reinterpret_cast<float4*>(A.vm)[i];
-    float* pp = &p.x; const float* gg = &g4.x; float* mm = &m.x; float* vv = &v.x; float* ww = &vm.x;
+  for (int k = 0; k < VQA_MAX_GROUPS - 1; ++k) gi += (k < A.ngroups - 1 && i >= A.gend4[k]) ? 1 : 0;
+  const float lr = A.glr[gi] * lam;
+  const float decay = 1.f - lr * A.wd, step_size = lr / bc1;
+  f32x4_t p = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.p) + i);
+  const f32x4_t g4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.g) + i);
+  f32x4_t m = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.m) + i);
+  f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.v) + i);
+  f32x4_t vm = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.vm) + i);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float gr = gg[j] * gmul;
-      pp[j] *= decay;                                   // decoupled weight decay
-      mm[j] = mm[j] + omb1 * (gr - mm[j]);              // exp_avg.lerp_(grad, 1-beta1)
-      vv[j] = vv[j] * A.b2 + omb2 * gr * gr;            // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-      ww[j] = fmaxf(ww[j], vv[j]);                      // amsgrad running max
-      const float denom = sqrtf(ww[j]) / bc2s + A.eps;
-      pp[j] = pp[j] - step_size * (mm[j] / denom);
-    }
-    reinterpret_cast<float4*>(A.p)[i] = p;
-    reinterpret_cast<float4*>(A.m)[i] = m;
-    reinterpret_cast<float4*>(A.v)[i] = v;
-    reinterpret_cast<float4*>(A.vm)[i] = vm;
-    if (A.p16) {
-      uint2 u;
-      u.x = (uint32_t)f2bf(p.x) | ((uint32_t)f2bf(p.y) << 16);
-      u.y = (uint32_t)f2bf(p.z) | ((uint32_t)f2bf(p.w) << 16);
-      reinterpret_cast<uint2*>(A.p16)[i] = u;
-    }
+  for (int j = 0; j < 4; ++j) {
+    const float gr = g4[j] * gmul;
+    p[j] *= decay;                                      // decoupled weight decay
+    m[j] = m[j] + omb1 * (gr - m[j]);                   // exp_avg.lerp_(grad, 1-beta1)
+    v[j] = v[j] * A.b2 + omb2 * gr * gr;                // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+    vm[j] = fmaxf(vm[j], v[j]);                         // amsgrad running max
+    const float denom = sqrtf(vm[j]) / bc2s + A.eps;
+    p[j] = p[j] - step_size * (m[j] / denom);
+  }
+  __builtin_nontemporal_store(p, reinterpret_cast<f32x4_t*>(A.p) + i);
+  __builtin_nontemporal_store(m, reinterpret_cast<f32x4_t*>(A.m) + i);
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4_t*>(A.v) + i);
+  __builtin_nontemporal_store(vm, reinterpret_cast<f32x4_t*>(A.vm) + i);
+  if (A.p16) {
+    uint2 u;
+    u.x = (uint32_t)f2bf(p[0]) | ((uint32_t)f2bf(p[1]) << 16);
+    u.y = (uint32_t)f2bf(p[2]) | ((uint32_t)f2bf(p[3]) << 16);
+    reinterpret_cast<uint2*>(A.p16)[i] = u;            // the next forward reads it: keep it cacheable
   }
 }
 
@@ -139,6 +142,6 @@ extern "C" int vqa_adamw_amsgrad(const vqa_adamw_desc* d, hipStream_t s) {
   }
   A.b1 = d->beta1; A.b2 = d->beta2; A.eps = d->eps; A.wd = d->weight_decay; A.gscale = d->grad_scale;
   A.st = d->state;
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(A.n4)), dim3(256), 0, s, A);
+  hipLaunchKernelGGL(adamw_kernel, dim3(vqa::cdiv(A.n4, 256)), dim3(256), 0, s, A);
   return vqa::check_launch("vqa_adamw_amsgrad");
 }
