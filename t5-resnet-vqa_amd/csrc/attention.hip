@@ -202,10 +202,15 @@ int fill(AttnP& P, const vqa_attn_desc* d) {
 
 }  // namespace
 
+bool vqa_attn_mfma_ok(const vqa_attn_desc* d);           // attention_mfma.hip
+int vqa_attn_fwd_mfma(const vqa_attn_desc* d, hipStream_t s);
+int vqa_attn_bwd_mfma(const vqa_attn_desc* d, hipStream_t s);
+
 extern "C" int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t s) {
   AttnP P;
   if (int rc = fill(P, d)) return rc;
   VQA_REQUIRE(d->o, "vqa_attn_fwd: null output");
+  if (vqa_attn_mfma_ok(d)) return vqa_attn_fwd_mfma(d, s);        // the step's shapes
   const size_t sm = fwd_smem(d->lq, d->lk, d->dh);
   VQA_REQUIRE(sm <= 65536, "vqa_attn_fwd: shape needs %zu B of LDS (> 64 KiB)", sm);
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(d->batch * d->heads), dim3(256), sm, s, P);
@@ -217,6 +222,7 @@ extern "C" int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t s) {
   if (int rc = fill(P, d)) return rc;
   VQA_REQUIRE(d->p && d->dout && d->dq && d->dk && d->dv, "vqa_attn_bwd: null P / dO / dQ / dK / dV");
   VQA_REQUIRE(d->lddo % 8 == 0, "vqa_attn_bwd: dO stride must be a multiple of 8");
+  if (vqa_attn_mfma_ok(d)) return vqa_attn_bwd_mfma(d, s);
   const size_t sm = bwd_smem(d->lq, d->lk, d->dh);
   VQA_REQUIRE(sm <= 65536, "vqa_attn_bwd: shape needs %zu B of LDS (> 64 KiB)", sm);
   hipLaunchKernelGGL(attn_bwd_kernel, dim3(d->batch * d->heads), dim3(256), sm, s, P);

@@ -1,0 +1,386 @@
+// MFMA attention core for the step's two attention shapes, one wave per (batch, head):
+//   SGA  MHAtt.att   softmax(QK^T/sqrt(96)) V, 8 heads x 96   multi_head_vision_text_attn.py:73-86
+//   T5   attention   softmax(QK^T + relbias + mask) V, 12 x 64 TF/models/t5/modeling_t5.py:144-173
+// Lq <= 32 queries (one 32-wide MFMA tile), Lk <= 64 keys (two), dh in {64, 96}.
+//
+// Layouts (v_mfma_f32_32x32x16_bf16: D[i][j] += a[i][k] b[k][j]; lane l holds
+// a[l&31][8(l>>5)+0..7], b[8(l>>5)+0..7][l&31]; D lane l = column j = l&31,
+// register r = row i = (r&3) + 8(r>>2) + 4(l>>5)):
+//   * "X" = S^T tile: lane = query, registers = 16 keys of a 32-key tile.  Row
+//     softmax / row sums are in-lane + one lane^32 exchange.  The registers of a
+//     16-key step, in order, are keys 16s + 4h + {0..3, 8..11} (h = l>>5) -- an
+//     MFMA k-order that the other operand reproduces with ds_read_b64_tr_b16
+//     rows 16s+4h and 16s+8+4h, so P / dS feed the next MFMA straight from
+//     registers (no shuffles).
+//   * "Y" = S tile: lane = key, registers = queries (backward only, for dV / dK).
+//   * Q, K, V, dO fragments with k = head dim are 16-B row loads from global;
+//     fragments with k = key / query come from small LDS images via
+//     ds_read_b64_tr_b16 (the transposing read).
+//   * outputs (O, dQ, dK, dV) are produced transposed (lane = token, registers =
+//     4 consecutive head-dim columns) so every store is 8 contiguous bytes.
+// Forward stores the pre-dropout P (fp32) for backward (and the T5 rel-bias
+// gradient needs per-sample dS anyway); backward recomputes nothing else.
+#include "common.h"
+
+namespace {
+
+constexpr float MASK_MIN = -3.4028234663852886e38f;     // torch.finfo(float32).min
+typedef __attribute__((address_space(3))) char lds_char;
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+
+struct AttnM {
+  const bf16_t *q, *k, *v; long ldq, ldk, ldv;
+  bf16_t* o; long ldo;
+  float* p;
+  const float* bias;
+  const long long* mask;
+  int pairs, heads, lq, lk;
+  float scale;
+  const bf16_t* dout; long lddo;
+  bf16_t *dq, *dk, *dv; long lddq, lddk, lddv;
+  float* dbias;
+  vqa_dropout drop;
+};
+
+__device__ __forceinline__ bf16x8_t ld_frag(const bf16_t* row, bool ok) {
+  uint4 u = make_uint4(0, 0, 0, 0);
+  if (ok) u = *reinterpret_cast<const uint4*>(row);
+  return __builtin_bit_cast(bf16x8_t, u);
+}
+
+__device__ __forceinline__ f32x16_t mfma(bf16x8_t a, bf16x8_t b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// tr-read fragment of an LDS image [rows][ROWB bytes] (bf16, row-major): lane gets
+// column c0 + (l & 31) at rows kb0 + 0..3 (j = 0..3) and kb1 + 0..3 (j = 4..7),
+// kb0 = 16s + 4h, kb1 = kb0 + 8 (the X-layout k order).
+template <int ROWB>
+__device__ __forceinline__ bf16x8_t tr_frag(const lds_char* img, int s, int c0) {
+  const int l = threadIdx.x & 63, h = l >> 5, g1 = (l >> 4) & 1, i16 = l & 15, q = i16 >> 2, p = i16 & 3;
+  const int col = c0 + 16 * g1 + 4 * p;
+  const int r0 = 16 * s + 4 * h + q;
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + r0 * ROWB + col * 2));
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + (r0 + 8) * ROWB + col * 2));
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// stage rows [n][DH] bf16 (global row stride ld) into an LDS image [ROWS][ROWB]; rows >= n are zero
+template <int DH, int ROWS, int ROWB>
+__device__ __forceinline__ void stage_img(lds_char* img, const bf16_t* src, long ld, int n) {
+  const int l = threadIdx.x & 63;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int CPR = DH / 8;                           // 16-B chunks per row
+  constexpr int PER = ROWS * CPR / 64;                  // chunks per lane (exact for DH 64 / 96)
+  static_assert(ROWS * CPR % 64 == 0, "image chunks must split evenly over the wave");
+  u32x4 u[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {                       // all loads first, then all LDS writes
+    const int idx = l + 64 * j, r = idx / CPR, c = idx - r * CPR;
+    u[j] = u32x4{0u, 0u, 0u, 0u};
+    if (r < n) u[j] = *reinterpret_cast<const u32x4*>(src + (long)r * ld + c * 8);
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int idx = l + 64 * j, r = idx / CPR, c = idx - r * CPR;
+    *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(img + r * ROWB + c * 16) = u[j];
+  }
+}
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+// X-layout accumulator registers [8s'..8s'+7] (s' = s & 1) as a bf16 MFMA k-fragment
+__device__ __forceinline__ bf16x8_t regs_frag(const f32x16_t& a, int s) {
+  const int o = 8 * (s & 1);
+  uint4 u;
+  u.x = pack2(a[o], a[o + 1]); u.y = pack2(a[o + 2], a[o + 3]);
+  u.z = pack2(a[o + 4], a[o + 5]); u.w = pack2(a[o + 6], a[o + 7]);
+  return __builtin_bit_cast(bf16x8_t, u);
+}
+
+// store a transposed output tile: lane = token row (l&31), registers = columns
+// c0 + (r&3) + 8(r>>2) + 4h -> 4 bf16 (8 B) per register group
+__device__ __forceinline__ void store_tr(bf16_t* base, long ld, int row, bool ok, int c0, const f32x16_t& a,
+                                         float mul) {
+  if (!ok) return;
+  const int h = (threadIdx.x & 63) >> 5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint2 u;
+    u.x = pack2(a[4 * g] * mul, a[4 * g + 1] * mul);
+    u.y = pack2(a[4 * g + 2] * mul, a[4 * g + 3] * mul);
+    *reinterpret_cast<uint2*>(base + (long)row * ld + c0 + 8 * g + 4 * h) = u;
+  }
+}
+
+constexpr int WPB = 2;                                  // waves (= (b, h) pairs) per block
+
+template <int DH>
+struct Geo {
+  static constexpr int KS = DH / 16;                    // k-steps over the head dim
+  static constexpr int ET = DH / 32;                    // 32-wide head-dim tiles
+  static constexpr int ROWB = DH * 2 + 16;              // LDS image row (16-B aligned, banks spread)
+};
+
+// ------------------------------------------------------------------ forward
+template <int DH>
+__global__ __launch_bounds__(64 * WPB) void attn_fwd_mfma(AttnM P) {
+  using G = Geo<DH>;
+  __shared__ __attribute__((aligned(16))) char smem[WPB * 64 * G::ROWB];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h5 = l >> 5, l31 = l & 31;
+  const int pair = blockIdx.x * WPB + w;
+  const bool live = pair < P.pairs;
+  const int b = live ? pair / P.heads : 0, hh = live ? pair - b * P.heads : 0;
+  const int lq = P.lq, lk = P.lk, nt = (lk + 31) / 32;
+  lds_char* vimg = (lds_char*)smem + w * 64 * G::ROWB;
+  const bf16_t* Q = P.q + (long)b * lq * P.ldq + hh * DH;
+  const bf16_t* K = P.k + (long)b * lk * P.ldk + hh * DH;
+  const bf16_t* V = P.v + (long)b * lk * P.ldv + hh * DH;
+
+  // fragments with k = head dim straight from global (16 B per lane per k-step)
+  bf16x8_t qf[G::KS], kf[2][G::KS];
+#pragma unroll
+  for (int s = 0; s < G::KS; ++s) {
+    qf[s] = ld_frag(Q + (long)l31 * P.ldq + 16 * s + 8 * h5, live && l31 < lq);
+    kf[0][s] = ld_frag(K + (long)l31 * P.ldk + 16 * s + 8 * h5, live && l31 < lk);
+    kf[1][s] = ld_frag(K + (long)(32 + l31) * P.ldk + 16 * s + 8 * h5, live && 32 + l31 < lk);
+  }
+  stage_img<DH, 64, G::ROWB>(vimg, V, P.ldv, live ? lk : 0);
+
+  // S^T tiles (X layout: lane = query, registers = keys)
+  f32x16_t sa[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sa[t][e] = 0.f;
+    if (t < nt) {
+#pragma unroll
+      for (int s = 0; s < G::KS; ++s) sa[t] = mfma(kf[t][s], qf[s], sa[t]);
+    }
+  }
+  // softmax over keys for query i = l31
+  const int i = l31;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5;
+      float v = -INFINITY;
+      if (key < lk) {
+        v = sa[t][r] * P.scale;
+        if (P.bias) v += P.bias[((long)hh * lq + min(i, lq - 1)) * lk + key];
+        if (P.mask && P.mask[(long)b * lk + key] == 0) v += MASK_MIN;
+      }
+      sa[t][r] = v;
+      mx = fmaxf(mx, v);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float z = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = sa[t][r] == -INFINITY ? 0.f : __expf(sa[t][r] - mx);
+      sa[t][r] = e;
+      z += e;
+    }
+  z += __shfl_xor(z, 32, 64);
+  const float iz = 1.f / z;
+  const DropK dk = drop_init(P.drop);
+  const long prow = (((long)b * P.heads + hh) * lq + i) * lk;   // element index of P[b, h, i, 0]
+  const bool qok = live && i < lq;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int key0 = 32 * t + 8 * g + 4 * h5;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = 4 * g + u, key = key0 + u;
+        const float pr = sa[t][r] * iz;
+        if (qok && key < lk && P.p) P.p[prow + key] = pr;          // saved pre-dropout P
+        sa[t][r] = dk.on ? pr * drop_mul(dk, (uint32_t)(prow + key)) : pr;
+      }
+    }
+  __syncthreads();                                                  // V image complete
+  // O^T = V^T P^T: a = V^T (tr reads, k = key in X order), b = P from registers
+#pragma unroll
+  for (int et = 0; et < G::ET; ++et) {
+    f32x16_t oa;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) oa[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s < 2 * nt) oa = mfma(tr_frag<G::ROWB>(vimg, s, et * 32), regs_frag(sa[s >> 1], s), oa);
+    }
+    store_tr(P.o + (long)b * lq * P.ldo + hh * DH, P.ldo, i, qok, et * 32, oa, 1.f);
+  }
+}
+
+// ------------------------------------------------------------------ backward
+template <int DH>
+__global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
+  using G = Geo<DH>;
+  constexpr int IMG = (64 + 32 + 32) * G::ROWB;         // K [64], dO [32], Q [32] images
+  __shared__ __attribute__((aligned(16))) char smem[WPB * (IMG + 32 * 4)];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h5 = l >> 5, l31 = l & 31;
+  const int pair = blockIdx.x * WPB + w;
+  const bool live = pair < P.pairs;
+  const int b = live ? pair / P.heads : 0, hh = live ? pair - b * P.heads : 0;
+  const int lq = P.lq, lk = P.lk, nt = (lk + 31) / 32;
+  lds_char* kimg = (lds_char*)smem + w * (IMG + 128);
+  lds_char* oimg = kimg + 64 * G::ROWB;
+  lds_char* qimg = oimg + 32 * G::ROWB;
+  float* dis = (float*)(qimg + 32 * G::ROWB);           // D_i per query
+  const bf16_t* Q = P.q + (long)b * lq * P.ldq + hh * DH;
+  const bf16_t* K = P.k + (long)b * lk * P.ldk + hh * DH;
+  const bf16_t* V = P.v + (long)b * lk * P.ldv + hh * DH;
+  const bf16_t* dO = P.dout + (long)b * lq * P.lddo + hh * DH;
+  const float* Pg = P.p + ((long)b * P.heads + hh) * lq * lk;
+
+  bf16x8_t of[G::KS], vf[2][G::KS];
+#pragma unroll
+  for (int s = 0; s < G::KS; ++s) {
+    of[s] = ld_frag(dO + (long)l31 * P.lddo + 16 * s + 8 * h5, live && l31 < lq);
+    vf[0][s] = ld_frag(V + (long)l31 * P.ldv + 16 * s + 8 * h5, live && l31 < lk);
+    vf[1][s] = ld_frag(V + (long)(32 + l31) * P.ldv + 16 * s + 8 * h5, live && 32 + l31 < lk);
+  }
+  stage_img<DH, 64, G::ROWB>(kimg, K, P.ldk, live ? lk : 0);
+  stage_img<DH, 32, G::ROWB>(oimg, dO, P.lddo, live ? lq : 0);
+  stage_img<DH, 32, G::ROWB>(qimg, Q, P.ldq, live ? lq : 0);
+  const DropK dk = drop_init(P.drop);
+  const long pbase = ((long)b * P.heads + hh) * lq * lk;  // dropout / dbias element base of (b, h)
+
+  // ---- X layout (lane = query): dP^T, D_i, dS^T -> dQ^T
+  const int i = l31;
+  const bool qok = live && i < lq;
+  f32x16_t xa[2];
+  float di = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) xa[t][e] = 0.f;
+    if (t < nt) {
+#pragma unroll
+      for (int s = 0; s < G::KS; ++s) xa[t] = mfma(vf[t][s], of[s], xa[t]);   // dP^T[key][query]
+    }
+  }
+  float px[2][16];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5;
+      const bool ok = qok && key < lk;
+      const float pr = ok ? Pg[(long)i * lk + key] : 0.f;
+      const float dp = ok ? xa[t][r] * drop_mul(dk, (uint32_t)(pbase + (long)i * lk + key)) : 0.f;
+      px[t][r] = pr;
+      xa[t][r] = dp;                                    // dP (gradient w.r.t. the pre-dropout P)
+      di += pr * dp;
+    }
+  di += __shfl_xor(di, 32, 64);
+  if (h5 == 0) dis[i] = di;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float ds = px[t][r] * (xa[t][r] - di);
+      xa[t][r] = ds;
+      const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5;
+      if (P.dbias && qok && key < lk) P.dbias[pbase + (long)i * lk + key] = ds;   // per-sample dS
+    }
+  __syncthreads();                                      // images + D_i complete
+  // dQ^T = scale K^T dS^T: a = K^T (tr reads of the K image, k = key), b = dS^T registers
+#pragma unroll
+  for (int et = 0; et < G::ET; ++et) {
+    f32x16_t acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (s < 2 * nt) acc = mfma(tr_frag<G::ROWB>(kimg, s, et * 32), regs_frag(xa[s >> 1], s), acc);
+    store_tr(P.dq + (long)b * lq * P.lddq + hh * DH, P.lddq, i, qok, et * 32, acc, P.scale);
+  }
+
+  // ---- Y layout (lane = key, registers = queries): dP, dS, dropout(P) -> dV^T, dK^T
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (t >= nt) continue;
+    const int key = 32 * t + l31;
+    const bool kok = live && key < lk;
+    f32x16_t ya;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) ya[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < G::KS; ++s) ya = mfma(of[s], vf[t][s], ya);        // dP[query][key]
+    f32x16_t pd, dsy;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = (r & 3) + 8 * (r >> 2) + 4 * h5;
+      const bool ok = kok && qi < lq;
+      const long e = pbase + (long)qi * lk + key;
+      const float pr = ok ? Pg[(long)qi * lk + key] : 0.f;
+      const float m = ok ? drop_mul(dk, (uint32_t)e) : 0.f;
+      pd[r] = pr * m;                                   // dropout(P)
+      dsy[r] = ok ? pr * (ya[r] * m - dis[qi]) : 0.f;   // dS
+    }
+#pragma unroll
+    for (int et = 0; et < G::ET; ++et) {
+      f32x16_t va, ka;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { va[e] = 0.f; ka[e] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        va = mfma(tr_frag<G::ROWB>(oimg, s, et * 32), regs_frag(pd, s), va);     // dV^T = dO^T dropout(P)
+        ka = mfma(tr_frag<G::ROWB>(qimg, s, et * 32), regs_frag(dsy, s), ka);    // dK^T = Q^T dS
+      }
+      store_tr(P.dv + (long)b * lk * P.lddv + hh * DH, P.lddv, key, kok, et * 32, va, 1.f);
+      store_tr(P.dk + (long)b * lk * P.lddk + hh * DH, P.lddk, key, kok, et * 32, ka, P.scale);
+    }
+  }
+}
+
+}  // namespace
+
+// host side: called by vqa_attn_fwd / vqa_attn_bwd (attention.hip) when the shape fits
+bool vqa_attn_mfma_ok(const vqa_attn_desc* d) {
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  return d->lq >= 1 && d->lq <= 32 && d->lk >= 1 && d->lk <= 64 && (d->dh == 64 || d->dh == 96) &&
+         d->ldq % 8 == 0 && d->ldk % 8 == 0 && d->ldv % 8 == 0 && al16(d->q) && al16(d->k) && al16(d->v) &&
+         (!d->o || (d->ldo % 4 == 0 && ((uintptr_t)d->o & 7) == 0)) &&
+         (!d->dout || (d->lddo % 8 == 0 && al16(d->dout))) &&
+         (!d->dq || (d->lddq % 4 == 0 && ((uintptr_t)d->dq & 7) == 0)) &&
+         (!d->dk || (d->lddk % 4 == 0 && ((uintptr_t)d->dk & 7) == 0)) &&
+         (!d->dv || (d->lddv % 4 == 0 && ((uintptr_t)d->dv & 7) == 0));
+}
+
+static void fillm(AttnM& M, const vqa_attn_desc* d) {
+  M.q = (const bf16_t*)d->q; M.k = (const bf16_t*)d->k; M.v = (const bf16_t*)d->v;
+  M.ldq = d->ldq; M.ldk = d->ldk; M.ldv = d->ldv;
+  M.o = (bf16_t*)d->o; M.ldo = d->ldo; M.p = d->p; M.bias = d->bias; M.mask = d->key_mask;
+  M.pairs = d->batch * d->heads; M.heads = d->heads; M.lq = d->lq; M.lk = d->lk; M.scale = d->scale;
+  M.dout = (const bf16_t*)d->dout; M.lddo = d->lddo;
+  M.dq = (bf16_t*)d->dq; M.dk = (bf16_t*)d->dk; M.dv = (bf16_t*)d->dv;
+  M.lddq = d->lddq; M.lddk = d->lddk; M.lddv = d->lddv;
+  M.dbias = d->dbias; M.drop = d->drop;
+}
+
+int vqa_attn_fwd_mfma(const vqa_attn_desc* d, hipStream_t s) {
+  AttnM M;
+  fillm(M, d);
+  const dim3 grid(vqa::cdiv(M.pairs, WPB));
+  if (d->dh == 64) hipLaunchKernelGGL(attn_fwd_mfma<64>, grid, dim3(64 * WPB), 0, s, M);
+  else hipLaunchKernelGGL(attn_fwd_mfma<96>, grid, dim3(64 * WPB), 0, s, M);
+  return vqa::check_launch("vqa_attn_fwd (mfma)");
+}
+
+int vqa_attn_bwd_mfma(const vqa_attn_desc* d, hipStream_t s) {
+  AttnM M;
+  fillm(M, d);
+  const dim3 grid(vqa::cdiv(M.pairs, WPB));
+  if (d->dh == 64) hipLaunchKernelGGL(attn_bwd_mfma<64>, grid, dim3(64 * WPB), 0, s, M);
+  else hipLaunchKernelGGL(attn_bwd_mfma<96>, grid, dim3(64 * WPB), 0, s, M);
+  return vqa::check_launch("vqa_attn_bwd (mfma)");
+}

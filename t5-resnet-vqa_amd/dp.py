@@ -110,7 +110,10 @@ class DataParallelStep:
             with torch.cuda.graph(g, stream=s):
                 self._run(calls)
             gs.setdefault(name, []).append(g)
-        cap("fwd", e.fwd_calls)
+        g = torch.cuda.CUDAGraph()                          # forward: ResNet || T5 encoder on two streams
+        with torch.cuda.graph(g, stream=s):
+            e.run_forward_streams()
+        gs["fwd"] = [g]
         for seg in self.segments:
             cap("seg", seg)
         cap("tail", self.tail + [self.emb_call])

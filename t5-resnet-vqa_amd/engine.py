@@ -638,11 +638,16 @@ class VQAEngine:
         SGA block 0), and the scaler weight gradient overlaps the T5 backward.
         Buffers of the two branches are disjoint, so the result is the same as
         the sequential order (and bit-identical: no cross-branch reductions)."""
+        self.run_forward_streams()
+        self.run_backward_streams()
+        if optimizer:
+            self._run(self.opt_calls)
+
+    def run_forward_streams(self):
         main = torch.cuda.current_stream(self.dev)
         side = self._side
-        f, b = self.fwd_calls, self.bwd_calls
+        f = self.fwd_calls
         p0, p1, p2 = self._fsplit
-        q0, q1 = self._bsplit
         self._run(f[:p0])                                  # rng advance
         fork = torch.cuda.Event()
         fork.record(main)
@@ -654,8 +659,13 @@ class VQAEngine:
         join.record(side)
         main.wait_event(join)
         self._run(f[p2:])                                  # SGA + head
-        wside = self._wside
-        self._run_tagged(b[:q0], main, wside)              # head + SGA backward (dW beside the chain)
+
+    def run_backward_streams(self):
+        main = torch.cuda.current_stream(self.dev)
+        side, wside = self._side, self._wside
+        b = self.bwd_calls
+        q0, q1 = self._bsplit
+        self._run_tagged(b[:q0], main, wside)              # head + SGA backward
         fork2 = torch.cuda.Event()
         fork2.record(main)
         side.wait_event(fork2)
@@ -666,8 +676,6 @@ class VQAEngine:
             join2 = torch.cuda.Event()
             join2.record(st)
             main.wait_event(join2)
-        if optimizer:
-            self._run(self.opt_calls)
 
     def _run_tagged(self, calls, main, wside):
         """Run `calls` in order on `main`, except runs of side-tagged calls (weight

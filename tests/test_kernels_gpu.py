@@ -83,7 +83,9 @@ def attn_ref(q, kk, v, scale, bias, mask, mult=None):
 @pytest.mark.parametrize("B,H,Lq,Lk,dh,t5,pd", [(4, 8, 32, 49, 96, False, 0.0), (4, 8, 32, 32, 96, False, 0.0),
                                                  (3, 12, 32, 32, 64, True, 0.0), (2, 8, 16, 64, 96, False, 0.0),
                                                  (2, 12, 16, 16, 64, True, 0.0), (4, 8, 32, 49, 96, False, 0.1),
-                                                 (3, 12, 32, 32, 64, True, 0.1)])
+                                                 (3, 12, 32, 32, 64, True, 0.1),
+                                                 (2, 8, 48, 40, 96, False, 0.0),      # lq > 32: VALU kernel
+                                                 (2, 12, 40, 40, 64, True, 0.1)])
 def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5, pd):
     D = H * dh
     q16 = rnd((B * Lq, 3 * D), 10, dtype=torch.bfloat16)                   # fused qkv-like layout
