@@ -63,6 +63,14 @@ __device__ __forceinline__ int mn_off(int kr, int ch) {
   return kr * (ROWLEN * 2) + ((ch ^ mn_swz<ROWLEN>(kr)) << 4);
 }
 
+// a / d for 0 <= a < 2^22 via a float reciprocal + one-step correction (no integer division)
+__device__ __forceinline__ int fdiv(int a, int d, float inv) {
+  int q = (int)((float)a * inv);
+  q -= (q * d > a) ? 1 : 0;
+  q += ((q + 1) * d <= a) ? 1 : 0;
+  return q;
+}
+
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
@@ -113,7 +121,8 @@ struct Loader {
         if constexpr (GATHER) {                  // feature (kh, kw, c) of this column
           const int tap = col / g.c;
           g1[j] = col - tap * g.c;
-          g2[j] = tap;
+          g0[j] = tap / g.kw;
+          g2[j] = tap - g0[j] * g.kw;
         }
       }
     }
@@ -122,6 +131,25 @@ struct Loader {
   __device__ __forceinline__ void issue(const bf16_t* __restrict__ base, long ld, char* stage, int k0, int K,
                                         const vqa_conv_geom& g) {
     const int w = threadIdx.x >> 6;
+    // implicit-im2col A: when C is a multiple of the K-tile (every conv but the stem), the
+    // whole tile shares one (kh, kw) tap -- one uniform division per tile instead of
+    // three per 16-B chunk
+    bool cfast = false;
+    int tkh = 0, tkw = 0, tc0 = 0;
+    float ihw = 0.f, iow = 0.f;
+    if constexpr (!KC && GATHER) {
+      ihw = 1.f / (float)(g.oh * g.ow);
+      iow = 1.f / (float)g.ow;
+    }
+    if constexpr (KC && GATHER) {
+      cfast = (g.c & (BK - 1)) == 0;
+      if (cfast) {
+        const int tap = k0 / g.c;
+        tc0 = k0 - tap * g.c;
+        tkh = tap / g.kw;
+        tkw = tap - tkh * g.kw;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const void* src = vqa_zero_page;
@@ -130,8 +158,14 @@ struct Loader {
         if constexpr (KC && !GATHER) {
           src = base + off[j] + k0;
         } else if constexpr (KC && GATHER) {
-          const int tap = kk / g.c, c = kk - tap * g.c;
-          const int kh = tap / g.kw, kw = tap - kh * g.kw;
+          int kh, kw, c;
+          if (cfast) {                                  // the K-tile lies inside one tap
+            kh = tkh; kw = tkw; c = tc0 + kof[j];
+          } else {
+            const int tap = kk / g.c;
+            c = kk - tap * g.c;
+            kh = tap / g.kw; kw = tap - kh * g.kw;
+          }
           const int ih = g1[j] + kh, iw = g2[j] + kw;
           if (ih >= 0 && ih < g.h && iw >= 0 && iw < g.w)
             src = base + (((long)g0[j] * g.h + ih) * g.w + iw) * g.c + c;
@@ -139,9 +173,9 @@ struct Loader {
           src = base + (long)kk * ld + off[j];
         } else {
           const int hw = g.oh * g.ow;
-          const int im = kk / hw, rem = kk - im * hw;
-          const int oh = rem / g.ow, ow = rem - oh * g.ow;
-          const int kh = g2[j] / g.kw, kw = g2[j] - kh * g.kw;
+          const int im = fdiv(kk, hw, ihw), rem = kk - im * hw;
+          const int oh = fdiv(rem, g.ow, iow), ow = rem - oh * g.ow;
+          const int kh = g0[j], kw = g2[j];
           const int ih = oh * g.stride - g.pad + kh, iw = ow * g.stride - g.pad + kw;
           if (ih >= 0 && ih < g.h && iw >= 0 && iw < g.w)
             src = base + (((long)im * g.h + ih) * g.w + iw) * g.c + g1[j];

@@ -220,6 +220,8 @@ class VQAEngine:
         cout, kh, kw, _ = w16.shape
         oh = (h + 2 * pad - kh) // stride + 1
         g = ops.conv_geom(n, h, w, c, oh, oh, kh, kw, stride, pad)
+        if kh == 1 and kw == 1 and stride == 1 and pad == 0:
+            g = None                                   # a 1x1/1 conv is a plain GEMM over the NHWC rows
         self._gemm(self.res_calls, x, w16, n * oh * oh, cout, kh * kw * c, lda=kh * kw * c, ldb=kh * kw * c, ga=g,
                    c16=out, ldc16=cout, bias=b32, relu=relu, res16=res16, ldres=cout)
 
