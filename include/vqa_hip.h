@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 2
+#define VQA_ABI_VERSION 3
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -43,9 +43,11 @@ const char* vqa_last_error(void);
  *   key = mix32(k1 ^ (site*0xC2B2AE35 + 0x27D4EB2F)),
  *   k1  = mix32(k0 ^ (rng[1]*0x85EBCA6B + 0x632BE5AB)), k0 = mix32(rng[0] + 0x9E3779B9),
  * mix32 = the lowbias32 finaliser; kept values are scaled by 1/(1-p).
- * rng is a device uint32[2] {seed, counter}; vqa_rng_advance() increments the
- * counter (once per step, first call of the forward), so a replayed hipGraph
- * draws fresh masks.  p == 0 or rng == NULL means identity (eval mode). */
+ * rng is a device uint32[3] {seed, counter, training}; vqa_rng_advance()
+ * increments the counter (once per step, first call of the forward), so a
+ * replayed hipGraph draws fresh masks; training == 0 (model.eval()) turns every
+ * dropout into the identity without re-planning or re-capturing.  p == 0 or
+ * rng == NULL also means identity. */
 typedef struct vqa_dropout {
   float p;
   unsigned site;

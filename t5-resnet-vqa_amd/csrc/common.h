@@ -62,7 +62,7 @@ struct DropK {
 };
 __device__ __forceinline__ DropK drop_init(const vqa_dropout& d) {
   DropK k;
-  k.on = d.p > 0.f && d.rng != nullptr;
+  k.on = d.p > 0.f && d.rng != nullptr && d.rng[2] != 0u;      // rng[2]: training flag (eval() clears it)
   k.key = 0; k.thresh = 0; k.scale = 1.f;
   if (k.on) {
     const uint32_t k0 = vqa_mix32(d.rng[0] + 0x9E3779B9u);

@@ -84,6 +84,7 @@ class VQAEngine:
         self.warmup, self.total, self.max_norm = warmup, total, max_norm
         self.betas, self.eps, self.wd = betas, eps, weight_decay
         self.grad_scale = grad_scale
+        self.group_lr = {}                # per-group LR overrides (trainer optimizer_kwargs)
         self.T = batch * seq_len
         self.lay = ParamLayout(vision, answer_spaces, num_blocks)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
@@ -127,8 +128,8 @@ class VQAEngine:
             self.p16[s.name] = self.P16[sl].view(s.shape)
             self.g32[s.name] = self.G32[sl].view(s.shape)
         self.opt_state = self._t(8, zero=True)
-        # dropout RNG state {seed, counter}; the forward's first call advances the counter
-        self.RNG = torch.from_numpy(np.array([self.seed & 0xFFFFFFFF, 0], np.uint32).view(np.int32)).to(self.dev)
+        # dropout RNG state {seed, counter, training}; the forward's first call advances the counter
+        self.RNG = torch.from_numpy(np.array([self.seed & 0xFFFFFFFF, 0, 1, 0], np.uint32).view(np.int32)).to(self.dev)
         self.bucket = torch.from_numpy(t5_bucket_map(self.L, self.L)).reshape(-1).to(self.dev)
 
     def _plan_resnet(self, sd):
@@ -590,6 +591,7 @@ class VQAEngine:
         d.param16 = self.P16.data_ptr()
         d.n = n
         ends, lrs = self.lay.group_of_element()
+        lrs = [self.group_lr.get(g, lr) for g, lr in zip(self.lay.groups, lrs)]
         d.ngroups = len(ends)
         for i, (e, lr) in enumerate(zip(ends, lrs)):
             d.group_end[i], d.group_lr[i] = e, lr
@@ -599,6 +601,32 @@ class VQAEngine:
         self._adam_desc = d
         o.append(ops.Call("vqa_adamw_amsgrad", ctypes.byref(d), desc=d,
                           keep=(self.P32, self.G32, self.M, self.V, self.VMAX, self.P16, self.opt_state)))
+
+    def set_training(self, mode=True):
+        """model.train() / model.eval(): the dropout kernels read this device flag at run
+        time, so captured graphs stay valid."""
+        self.RNG[2].fill_(1 if mode else 0)
+
+    def configure_optimizer(self, group_lr=None, warmup=None, total=None, max_norm=None, weight_decay=None,
+                            betas=None, eps=None):
+        """Re-plan the clip + AdamW + schedule tail (faster_rcnn_vqa_trainer.py:231-287 knobs)."""
+        if group_lr:
+            self.group_lr.update(group_lr)
+        if warmup is not None:
+            self.warmup = int(warmup)
+        if total is not None:
+            self.total = int(total)
+        if max_norm is not None:
+            self.max_norm = float(max_norm)
+        if weight_decay is not None:
+            self.wd = float(weight_decay)
+        if betas is not None:
+            self.betas = tuple(betas)
+        if eps is not None:
+            self.eps = float(eps)
+        self.opt_calls = []
+        self._plan_optimizer()
+        self.graph = None
 
     def set_grad_scale(self, s):
         """DP: grads are summed over ranks; the average enters as a scale."""

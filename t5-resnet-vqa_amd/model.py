@@ -1,0 +1,130 @@
+"""`ResnetVQAModel` — the reference's model API (model/resnet_vqa_model.py:28-165)
+over the MI355X engine.
+
+Same constructor arguments, same `forward(**batch)` keyword set and return
+value `(log_probs [B, answer_spaces], loss or None)`, the same state-dict keys
+ and the attribute names the reference trainer reads
+(`vision_model_name`, `device`).  What differs, by design:
+
+* shapes are planned once: `batch_size`, `seq_len` and `image_size` are fixed
+  at construction (the hipGraph step has static buffers); a batch of another
+  shape raises ValueError (use drop_last=True loaders, as the step is
+  per-batch anyway);
+* weights come from a reference `state_dict` (e.g. `torch.load(best-model.pt,
+  weights_only=True)`) or, offline, from the deterministic synthetic init —
+  `from_pretrained` downloads are not available here;
+* backward / the optimizer live in `trainer.VQATrainer.train_one_step`, which
+  runs zero_grad → forward → backward → clip → AdamW → scheduler as one graph.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import synthetic as S
+from .engine import VQAEngine
+
+SUPPORTED_VISION = ("resnet50", "resnet34")
+
+
+class ResnetVQAModel:
+    def __init__(self, vision_model_name, language_model_name, answer_spaces, fine_tune_lm_encoder=True,
+                 fine_tune_lm_decoder=True, fine_tune_vision=True, num_attention_blocks=3, device="cuda",
+                 *, batch_size=64, seq_len=32, image_size=224, state_dict=None, seed=0, dropout=0.1,
+                 dropout_seed=0):
+        # resnet_vqa_model.py:51-58 builds only resnet18/34/50 and fails later for other names;
+        # fail here, with the reason.
+        if vision_model_name not in SUPPORTED_VISION:
+            raise ValueError(f"vision_model_name {vision_model_name!r}: this path supports {SUPPORTED_VISION}")
+        if language_model_name not in ("t5-base",):
+            raise ValueError("language_model_name must be 't5-base' (d_model 768 is hard-coded in the SGA blocks, "
+                             "multi_head_vision_text_attn.py:9,19)")
+        if num_attention_blocks < 1:
+            raise ValueError("num_attention_blocks must be >= 1")
+        self.vision_model_name = vision_model_name
+        self.language_model_name = language_model_name
+        self.answer_spaces = int(answer_spaces)
+        self.num_attention_blocks = int(num_attention_blocks)
+        self.device = torch.device(device)
+        self.batch_size, self.seq_len, self.image_size = int(batch_size), int(seq_len), int(image_size)
+        self._cfg = dict(dropout=float(dropout), seed=int(dropout_seed))
+        if state_dict is None:
+            state_dict = S.make_state_dict(vision_model_name, seed=seed, answer_spaces=self.answer_spaces,
+                                           num_attention_blocks=self.num_attention_blocks)
+        self._build(state_dict)
+        self.training = True
+
+    # ------------------------------------------------------------------ engine
+    def _build(self, state_dict, **kw):
+        sd = {k: (v.detach().cpu().float().numpy() if isinstance(v, torch.Tensor) else np.asarray(v))
+              for k, v in state_dict.items()}
+        missing = [k for k in S.model_specs(self.vision_model_name, self.answer_spaces, self.num_attention_blocks)
+                   if k not in sd]
+        if missing:
+            raise KeyError(f"state_dict lacks {len(missing)} reference keys, e.g. {missing[:3]}")
+        opt = dict(getattr(self, "_opt", {}))
+        opt.update(kw)
+        self.engine = VQAEngine(sd, vision=self.vision_model_name, batch=self.batch_size, seq_len=self.seq_len,
+                                image_size=self.image_size, device=self.device, answer_spaces=self.answer_spaces,
+                                num_blocks=self.num_attention_blocks, **self._cfg, **opt)
+        self._opt = opt
+
+    def train(self, mode=True):
+        """nn.Module.train: dropout on (the reference trains with p = 0.1 at every site)."""
+        self.training = bool(mode)
+        self.engine.set_training(self.training)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    # ------------------------------------------------------------------ forward
+    def _check_batch(self, question_input_ids, image_tensors):
+        want_q = (self.batch_size, self.seq_len)
+        want_i = (self.batch_size, 3, self.image_size, self.image_size)
+        if tuple(question_input_ids.shape) != want_q:
+            raise ValueError(f"question_input_ids shape {tuple(question_input_ids.shape)} != planned {want_q}")
+        if tuple(image_tensors.shape) != want_i:
+            raise ValueError(f"image_tensors shape {tuple(image_tensors.shape)} != planned {want_i}")
+
+    def load_batch(self, question_input_ids, question_attention_masks, image_tensors, annotation_ids=None):
+        self._check_batch(question_input_ids, image_tensors)
+        self.engine.load_batch({"question_input_ids": question_input_ids,
+                                "question_attention_masks": question_attention_masks,
+                                "image_tensors": image_tensors, "annotation_ids": annotation_ids})
+
+    def forward(self, question_input_ids, decoder_question_input_ids=None, question_attention_masks=None,
+                decoder_question_attention_masks=None, annotation_ids=None, image_tensors=None,
+                answer_input_ids=None, pixel_values=None, answer_attention_masks=None, question_type_ids=None):
+        """resnet_vqa_model.py:101-165: returns (log_probs, loss); loss is None without
+        annotation_ids.  decoder_*, answer_*, pixel_values and question_type_ids are
+        accepted and ignored, as in the reference."""
+        if question_attention_masks is None or image_tensors is None:
+            raise TypeError("forward() needs question_attention_masks and image_tensors")
+        self.load_batch(question_input_ids, question_attention_masks, image_tensors, annotation_ids)
+        self.engine.forward()
+        log_probs = self.engine.LOGP.clone()
+        loss = self.engine.LOSS[0].clone() if annotation_ids is not None else None
+        return log_probs, loss
+
+    __call__ = forward
+
+    # ------------------------------------------------------------------ weights
+    def state_dict(self):
+        """Reference keys -> fp32 CPU tensors (loadable by the reference ResnetVQAModel)."""
+        return {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in self.engine.state_dict().items()}
+
+    def load_state_dict(self, state_dict, strict=True):
+        """Load reference weights (optimizer state restarts, as in the reference's init_model,
+        train_faster_rcnn_vqa.py:40-45)."""
+        sd = dict(state_dict)
+        if not strict:
+            cur = self.state_dict()
+            cur.update({k: v for k, v in sd.items() if k in cur})
+            sd = cur
+        training = self.training
+        self._build(sd)
+        self.train(training)
+
+    def parameters_count(self):
+        return self.engine.lay.num_params

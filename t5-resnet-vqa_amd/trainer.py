@@ -1,0 +1,107 @@
+"""`VQATrainer` — the hot loop of the reference trainer
+(trainer/faster_rcnn_vqa_trainer.py:231-406, ≡ cross_attention_vqa_trainer.py)
+over the MI355X engine.
+
+Mirrors:
+  _init_optimizer   AdamW(amsgrad) param groups: lang_model `lm_encoder_lr`,
+                    scaler / SGA / pooler 5e-4 (hard-coded :244-261),
+                    classifier `classifier_lr`; `kwargs` (weight_decay,
+                    amsgrad=True, betas, eps)                     :231-267
+  _init_lr_scheduler linear warm-up/decay, warmup = min(T//10 if -1,
+                    max_warmup_steps)                            :279-287
+  train_one_step    zero_grad -> forward -> backward -> clip_grad_norm_
+                    (gradient_clipping) -> step -> sched; returns
+                    (loss.item(), log-probs)                      :391-406
+  train_one_epoch   the batch loop with the "secs/batch" timing log, averaged
+                    every 10% of the epoch                        :314-360
+  valid_one_step    eval-mode forward (dropout off), no update    :408-430
+The whole train step is one replayed hipGraph; the only host sync per step is
+the `loss.item()` the reference API returns (pass sync=False to skip it).
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from .model import ResnetVQAModel
+
+HARD_CODED_LR = 5e-4          # faster_rcnn_vqa_trainer.py:244-261
+
+
+class VQATrainer:
+    def __init__(self, model: ResnetVQAModel, optimizer_kwargs: dict, lr_scheduler_kwargs: dict,
+                 num_training_steps: int, gradient_clipping=1.0, use_graph=True, logger=print):
+        if optimizer_kwargs.get("type", "AdamW") != "AdamW":
+            raise ValueError("only AdamW is on this path (vit_daquar_config.json:41)")
+        kw = dict(optimizer_kwargs.get("kwargs", {}))
+        if not kw.get("amsgrad", True):
+            raise ValueError("the reference trains with amsgrad=True; plain AdamW is not planned here")
+        self.model = model
+        self.logger = logger
+        self.num_training_steps = int(num_training_steps)
+        warm = lr_scheduler_kwargs.get("num_warmup_steps", -1)
+        warm = self.num_training_steps // 10 if warm == -1 else int(warm)
+        warm = min(warm, int(lr_scheduler_kwargs.get("max_warmup_steps", warm)))
+        self.num_warmup_steps = warm
+        group_lr = {"lang_model": float(optimizer_kwargs.get("lm_encoder_lr", 5e-3)),
+                    "scaler": HARD_CODED_LR, "sga_modules": HARD_CODED_LR, "attention_pooler": HARD_CODED_LR,
+                    "classification_layer": float(optimizer_kwargs.get("classifier_lr", 1e-5))}
+        model.engine.configure_optimizer(group_lr=group_lr, warmup=warm, total=self.num_training_steps,
+                                         max_norm=float(gradient_clipping or 0.0),
+                                         weight_decay=float(kw.get("weight_decay", 1e-2)),
+                                         betas=tuple(kw.get("betas", (0.9, 0.999))), eps=float(kw.get("eps", 1e-8)))
+        self.use_graph = use_graph
+        self.total_training_time = 0.0
+
+    # ------------------------------------------------------------------ steps
+    def train_one_step(self, data_items, sync=True):
+        """Returns (loss.item(), log_probs) like the reference (:391-406)."""
+        m = self.model
+        if not m.training:
+            m.train()
+        m.load_batch(data_items["question_input_ids"], data_items["question_attention_masks"],
+                     data_items["image_tensors"], data_items["annotation_ids"])
+        e = m.engine
+        if self.use_graph and e.graph is None:
+            e.capture()
+        e.train_step()
+        loss = float(e.LOSS.item()) if sync else e.LOSS[0]
+        return loss, e.LOGP
+
+    @torch.no_grad()
+    def valid_one_step(self, data_items):
+        """Eval-mode forward (dropout off); returns (loss.item() or None, log_probs)."""
+        m = self.model
+        was = m.training
+        m.eval()
+        lp, loss = m(**{k: data_items.get(k) for k in ("question_input_ids", "question_attention_masks",
+                                                      "image_tensors", "annotation_ids")})
+        m.train(was)
+        return (float(loss) if loss is not None else None), lp
+
+    def train_one_epoch(self, batches, epoch=0):
+        """The reference's epoch loop without the WUPS/wandb tail: returns
+        {avg_loss, secs_per_batch, steps}."""
+        total, n, t_epoch = 0.0, 0, 0.0
+        window = max(1, len(batches) // 10) if hasattr(batches, "__len__") else 10
+        win_loss, win_time = 0.0, 0.0
+        for i, data_items in enumerate(batches):
+            t0 = time.time()
+            loss, _ = self.train_one_step(data_items)
+            dt = time.time() - t0
+            total += loss
+            n += 1
+            t_epoch += dt
+            win_loss += loss
+            win_time += dt
+            if (i + 1) % window == 0 and self.logger:
+                self.logger(f"Epoch {epoch} - iter {i}/{n} - total loss {win_loss / window:.4f}"
+                            f" - secs/batch {win_time / window:.4f}")
+                win_loss, win_time = 0.0, 0.0
+        self.total_training_time += t_epoch
+        return {"avg_loss": total / max(1, n), "secs_per_batch": t_epoch / max(1, n), "steps": n}
+
+    def grad_norm(self):
+        """clip_grad_norm_'s returned total norm of the last step."""
+        return self.model.engine.last_grad_norm()

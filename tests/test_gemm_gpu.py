@@ -109,7 +109,7 @@ def test_dropout_epilogue(ops, pkg, vec, relu):
     a, b = bf((Bt, M, K), seed=21), bf((Bt, N, K), seed=22)
     bias = torch.randn(N, device="cuda")
     res = None if relu else torch.randn(Bt, M, N, device="cuda")
-    rng = torch.tensor([5, 9], dtype=torch.int32, device="cuda")
+    rng = torch.tensor([5, 9, 1], dtype=torch.int32, device="cuda")
     c = torch.empty(Bt, M, N, device="cuda")
     d = ops.gemm_desc(a, b, M, N, K, lda=K, ldb=K, c32=c, ldc32=N, bias=bias, res32=res, ldres=N, relu=relu,
                       alpha=0.75, batch=Bt, stride_a=M * K, stride_b=N * K, stride_c32=M * N, stride_res=M * N)
@@ -172,7 +172,7 @@ def test_all_tile_configs_bitwise_identical(ops, pkg, layout):
     element in the same K order, so outputs are bit-identical (engines autotune
     per call and DP ranks may pick differently without diverging)."""
     n_cfg = max(pkg.lib.GEMM_TILES)
-    rng = torch.tensor([1, 2], dtype=torch.int32, device="cuda")
+    rng = torch.tensor([1, 2, 1], dtype=torch.int32, device="cuda")
     if layout in ("conv", "convw"):
         nb, h, c, co = 2, 14, 64, 96
         x = bf((nb, h, h, c), seed=31)

@@ -109,7 +109,7 @@ def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5, pd):
     mult = None
     if pd > 0:
         from oracle import vqa_oracle as orc
-        rng = torch.tensor([11, 4], dtype=torch.int32, device="cuda")
+        rng = torch.tensor([11, 4, 1], dtype=torch.int32, device="cuda")
         d.drop = L.Dropout(pd, 77, rng.data_ptr())
         mult = torch.from_numpy(orc.dropout_multiplier(pd, 11, 4, 77, B * H * Lq * Lk)).cuda().view(B, H, Lq, Lk)
     L.check(L.load().vqa_attn_fwd(ctypes.byref(d), L.stream_handle()), "fwd")
@@ -277,7 +277,7 @@ def test_dropout_mask_matches_oracle_hash(k):
     L = k.lib
     for seed, ctr, site, p, n in [(0, 1, 1, 0.1, 100003), (123456789, 77, 150, 0.1, 4096),
                                   (0xFFFFFFFF, 2**31 + 5, 16, 0.5, 5000), (3, 3, 3, 0.0, 64)]:
-        rng = torch.from_numpy(np.array([seed, ctr], np.uint32).view(np.int32)).cuda()
+        rng = torch.from_numpy(np.array([seed, ctr, 1], np.uint32).view(np.int32)).cuda()
         d = L.Dropout(p, site, rng.data_ptr())
         out = torch.empty(n, device="cuda")
         L.check(L.load().vqa_dropout_mask(ctypes.byref(d), ctypes.c_void_p(out.data_ptr()), n, L.stream_handle()),
@@ -286,7 +286,7 @@ def test_dropout_mask_matches_oracle_hash(k):
         ref = orc.dropout_multiplier(p, seed, ctr, site, n) if p > 0 else np.ones(n, np.float32)
         np.testing.assert_array_equal(out.cpu().numpy(), ref)
     # law: keep rate 1-p, scale 1/(1-p); advancing the counter changes the mask
-    rng = torch.tensor([0, 0], dtype=torch.int32, device="cuda")
+    rng = torch.tensor([0, 0, 1], dtype=torch.int32, device="cuda")
     d = L.Dropout(0.1, 5, rng.data_ptr())
     m0, m1 = torch.empty(1 << 20, device="cuda"), torch.empty(1 << 20, device="cuda")
     L.load().vqa_dropout_mask(ctypes.byref(d), ctypes.c_void_p(m0.data_ptr()), 1 << 20, L.stream_handle())
@@ -305,7 +305,7 @@ def test_norm_and_embedding_dropout_hooks(k):
     from oracle import vqa_oracle as orc
     L = k.lib
     rows, D = 256, 768
-    rng = torch.tensor([9, 2], dtype=torch.int32, device="cuda")
+    rng = torch.tensor([9, 2, 1], dtype=torch.int32, device="cuda")
     mk = lambda site: L.Dropout(0.1, site, rng.data_ptr())
     mult = lambda site: torch.from_numpy(orc.dropout_multiplier(0.1, 9, 2, site, rows * D)).cuda().view(rows, D)
     dA, dB, dC = mk(40), mk(41), mk(42)
