@@ -107,6 +107,8 @@ struct Loader {
             const int im = grow / hw, rem = grow - im * hw;
             const int oh = rem / g.ow, ow = rem - oh * g.ow;
             g0[j] = im; g1[j] = oh * g.stride - g.pad; g2[j] = ow * g.stride - g.pad;
+            // element offset of this chunk at tap (0, 0); a tap adds (kh*W + kw)*C
+            off[j] = (((long)im * g.h + g1[j]) * g.w + g2[j]) * g.c + kof[j];
           } else {
             g0[j] = 0; g1[j] = -(1 << 28); g2[j] = -(1 << 28);
           }
@@ -136,6 +138,7 @@ struct Loader {
     // three per 16-B chunk
     bool cfast = false;
     int tkh = 0, tkw = 0, tc0 = 0;
+    long toff = 0;
     float ihw = 0.f, iow = 0.f;
     if constexpr (!KC && GATHER) {
       ihw = 1.f / (float)(g.oh * g.ow);
@@ -148,6 +151,7 @@ struct Loader {
         tc0 = k0 - tap * g.c;
         tkh = tap / g.kw;
         tkw = tap - tkh * g.kw;
+        toff = (long)(tkh * g.w + tkw) * g.c + tc0;
       }
     }
 #pragma unroll
@@ -158,17 +162,17 @@ struct Loader {
         if constexpr (KC && !GATHER) {
           src = base + off[j] + k0;
         } else if constexpr (KC && GATHER) {
-          int kh, kw, c;
           if (cfast) {                                  // the K-tile lies inside one tap
-            kh = tkh; kw = tkw; c = tc0 + kof[j];
+            const int ih = g1[j] + tkh, iw = g2[j] + tkw;
+            if (ih >= 0 && ih < g.h && iw >= 0 && iw < g.w) src = base + off[j] + toff;
           } else {
             const int tap = kk / g.c;
-            c = kk - tap * g.c;
-            kh = tap / g.kw; kw = tap - kh * g.kw;
+            const int c = kk - tap * g.c;
+            const int kh = tap / g.kw, kw = tap - kh * g.kw;
+            const int ih = g1[j] + kh, iw = g2[j] + kw;
+            if (ih >= 0 && ih < g.h && iw >= 0 && iw < g.w)
+              src = base + (((long)g0[j] * g.h + ih) * g.w + iw) * g.c + c;
           }
-          const int ih = g1[j] + kh, iw = g2[j] + kw;
-          if (ih >= 0 && ih < g.h && iw >= 0 && iw < g.w)
-            src = base + (((long)g0[j] * g.h + ih) * g.w + iw) * g.c + c;
         } else if constexpr (!KC && !GATHER) {
           src = base + (long)kk * ld + off[j];
         } else {

@@ -316,7 +316,7 @@ __global__ __launch_bounds__(1024) void colsum3_partials_kernel(const float* __r
   }
 }
 
-constexpr int NORM_BWD_ROWS = 16;      // rows per block in the backward kernels
+constexpr int NORM_BWD_ROWS = 8;       // rows per block in the backward kernels (256 blocks at 2048 rows)
 
 vqa_dropout dr(const vqa_dropout* d) {
   vqa_dropout o{0.f, 0u, nullptr};

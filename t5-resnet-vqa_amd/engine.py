@@ -277,7 +277,7 @@ class VQAEngine:
         self.dH32 = t((T, D))
         self.dHM32 = t((T, D))
         self.dPB = t((S.T5_HEADS, Lq, Lq), zero=True)
-        self.dSB = t((B, S.T5_HEADS, Lq, Lq))             # per-sample attention dS (rel-bias grad)
+        self.dSB = t((S.T5_LAYERS, B, S.T5_HEADS, Lq, Lq))   # per-layer, per-sample attention dS (rel-bias grad)
         self.WS_EMB = t(3 * T, torch.int32)
         lib = L.load()
         self.WS_NORM = t(lib.vqa_norm_bwd_workspace_floats(T, D))
@@ -555,11 +555,8 @@ class VQAEngine:
             self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B, heads=S.T5_HEADS, lq=Lq,
                        lk=Lq, dh=S.T5_DKV, scale=1.0, dout=self.dO16, lddo=D, dq=dq, lddq=3 * D,
-                       dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dSB,
+                       dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dSB[i],
                        drop=t5_site(i, 0))
-            # relative-position bias is shared by all 12 layers: dPB = sum_layers sum_b dS
-            self._call(b, "vqa_batch_sum", self.dSB, B, S.T5_HEADS * Lq * Lq, self.dPB,
-                       0.0 if i == S.T5_LAYERS - 1 else 1.0)
             self._dw(b, dq, self.N0[i], f"t5.{i}.qkv_w", T)
             self._dx(b, dq, f"t5.{i}.qkv_w", T, out32=self.dC32)
             # layer 0: dH32 becomes the embedding gradient (masked by the embedding dropout :725);
@@ -571,6 +568,9 @@ class VQAEngine:
                        self.dH32, dH16[i - 1] if i > 0 else None, self.g32[f"t5.{i}.ln0"], 0.0, self.WS_NORM, T, D,
                        None, d32, d16, extra=kp + [self.RNG])
             mark(f"t5.{i}.ln1")
+        # the relative-position bias is shared by all 12 layers: dPB = sum over (layer, sample) of dS,
+        # one fixed-order reduction after the last layer instead of one per layer
+        self._call(b, "vqa_batch_sum", self.dSB, S.T5_LAYERS * B, S.T5_HEADS * Lq * Lq, self.dPB, 0.0)
         self._call(b, "vqa_t5_relbias_bwd", self.dPB, self.bucket, self.g32["t5.relbias"], S.T5_HEADS, Lq, Lq,
                    S.T5_BUCKETS)
         mark("t5.relbias")
