@@ -103,6 +103,11 @@ typedef struct vqa_gemm_desc {
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
 /* tile configuration (1..VQA_GEMM_CONFIGS) that vqa_gemm would run for this descriptor */
 int vqa_gemm_select(const vqa_gemm_desc* d);
+/* Two independent GEMMs in one launch: a layer's input gradient dX (a_trans=0,
+ * b_trans=1) and weight gradient dW (a_trans=1, b_trans=1), both batch 1, no
+ * conv.  Each keeps its own epilogue and tile config (configs 3, 4, 6, 7; others
+ * map to 4).  Any other pair of descriptors runs as two vqa_gemm calls. */
+int vqa_gemm_pair(const vqa_gemm_desc* dx, const vqa_gemm_desc* dw, hipStream_t stream);
 
 /* ------------------------------------------------------------- attention ---
  * Multi-head attention core for Lq, Lk <= 64 (one workgroup per (b, head)):

@@ -278,18 +278,24 @@ __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
 }
 
+template <int BM, int BN, int STAGES>
+struct TileCfg {
+  static constexpr int LDS = STAGES * (BM + BN) * BK * 2;       // LDS ring bytes
+};
+
+// One output tile.  `bid` is the tile's linear id within its problem (the
+// paired launcher offsets it), `smem` the block's LDS ring (a __shared__ array
+// of the calling kernel; inlined, so the LDS address space is preserved).
 template <int BM, int BN, int STAGES, bool AKC, bool BKC, bool GA, bool GB>
-__global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
+__device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, char* smem) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, ST_BYTES = A_BYTES + B_BYTES;
   using LA = Loader<BM, AKC, GA>;
   using LB = Loader<BN, BKC, GB>;
   constexpr int NL = LA::NI + LB::NI;                 // glds instructions per thread per K-tile
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * ST_BYTES];
 
   // XCD-aware bijective remap of the linear block id
   const int nwg = P.tiles_m * P.tiles_n;
-  const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int tm = wg / P.tiles_n, tn = wg - tm * P.tiles_n;
@@ -508,6 +514,29 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
 }
 
 template <int BM, int BN, int STAGES, bool AKC, bool BKC, bool GA, bool GB>
+__global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
+  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<BM, BN, STAGES>::LDS];
+  gemm_body<BM, BN, STAGES, AKC, BKC, GA, GB>(P, blockIdx.x, smem);
+}
+
+// Two independent problems in one launch (the backward's dX and dW of one
+// layer share dY): blocks [0, t1) run problem 1, the padding up to a multiple
+// of 8 exits (keeps problem 2's XCD remap aligned), the rest run problem 2.
+// Fills the chip where either GEMM alone leaves CUs idle and saves a launch.
+template <int BM1, int BN1, int S1, int BM2, int BN2, int S2>
+__global__ __launch_bounds__(NT) void gemm_pair_kernel(GemmParams P1, GemmParams P2, int t1pad) {
+  constexpr int L1 = TileCfg<BM1, BN1, S1>::LDS, L2 = TileCfg<BM2, BN2, S2>::LDS;
+  __shared__ __attribute__((aligned(1024))) char smem[L1 > L2 ? L1 : L2];
+  const int t1 = P1.tiles_m * P1.tiles_n;
+  const int bid = blockIdx.x;
+  if (bid < t1) {
+    gemm_body<BM1, BN1, S1, true, false, false, false>(P1, bid, smem);       // dX: A k-contig, B n-contig
+  } else if (bid >= t1pad) {
+    gemm_body<BM2, BN2, S2, false, false, false, false>(P2, bid - t1pad, smem);   // dW: both m/n-contig
+  }
+}
+
+template <int BM, int BN, int STAGES, bool AKC, bool BKC, bool GA, bool GB>
 int launch(GemmParams& P, int batch, hipStream_t s) {
   P.tiles_m = vqa::cdiv(P.m, BM);
   P.tiles_n = vqa::cdiv(P.n, BN);
@@ -556,7 +585,7 @@ extern "C" int vqa_gemm_select(const vqa_gemm_desc* d) {
   return d->config ? d->config : auto_config(d->m, d->n, d->k, d->batch);
 }
 
-extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
+static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
   VQA_REQUIRE(d != nullptr, "vqa_gemm: null descriptor");
   VQA_REQUIRE(d->m > 0 && d->n > 0 && d->k > 0, "vqa_gemm: empty problem m=%d n=%d k=%d", d->m, d->n, d->k);
   VQA_REQUIRE(d->a && d->b, "vqa_gemm: null operand");
@@ -575,7 +604,6 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   VQA_REQUIRE(d->drop.p >= 0.f && d->drop.p < 1.f, "vqa_gemm: dropout p must be in [0, 1)");
   VQA_REQUIRE(!(d->drop.p > 0.f && d->drop.rng && d->relu && (d->res32 || d->res16)),
               "vqa_gemm: relu + residual + dropout is not a supported epilogue");
-  GemmParams P;
   P.a = (const bf16_t*)d->a; P.lda = d->lda;
   P.b = (const bf16_t*)d->b; P.ldb = d->ldb;
   P.m = d->m; P.n = d->n; P.k = d->k;
@@ -587,13 +615,19 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   P.ga = d->ga; P.gb = d->gb;
   P.sa = d->stride_a; P.sb = d->stride_b; P.sc32 = d->stride_c32; P.sc16 = d->stride_c16; P.sres = d->stride_res;
   P.drop = d->drop;
-  const int batch = d->batch, cfg = d->config;
   auto al = [](const void* p, int bytes) { return p == nullptr || ((uintptr_t)p % bytes) == 0; };
   P.vec = d->n % 8 == 0 && (!d->c32 || (d->ldc32 % 8 == 0 && al(d->c32, 16) && d->stride_c32 % 8 == 0)) &&
           (!d->c16 || (d->ldc16 % 8 == 0 && al(d->c16, 16) && d->stride_c16 % 8 == 0)) &&
           (!d->res32 || (d->ldres % 8 == 0 && al(d->res32, 16))) && (!d->res16 || (d->ldres % 8 == 0 && al(d->res16, 16))) &&
           (!d->mask16 || (d->ldmask % 8 == 0 && al(d->mask16, 16))) &&
           (!(d->res32 || d->res16 || d->mask16) || d->stride_res % 8 == 0) && al(d->bias, 16);
+  return VQA_OK;
+}
+
+extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
+  GemmParams P;
+  if (int rc = prepare(d, P)) return rc;
+  const int batch = d->batch, cfg = d->config;
   const bool akc = !d->a_trans, bkc = !d->b_trans;
   if (akc && bkc && !d->a_conv) return dispatch_tile<true, true, false, false>(P, batch, cfg, stream);
   if (akc && bkc && d->a_conv) return dispatch_tile<true, true, true, false>(P, batch, cfg, stream);
@@ -602,4 +636,57 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   if (!akc && !bkc && d->b_conv) return dispatch_tile<false, false, false, true>(P, batch, cfg, stream);
   if (!akc && bkc) return dispatch_tile<false, true, false, false>(P, batch, cfg, stream);
   return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: unsupported layout combination");
+}
+
+namespace {
+// tile configs available to the paired launch (a subset of dispatch_tile's)
+template <int C> struct CfgOf;
+template <> struct CfgOf<3> { static constexpr int BM = 64, BN = 64, S = 4; };
+template <> struct CfgOf<4> { static constexpr int BM = 64, BN = 64, S = 2; };
+template <> struct CfgOf<6> { static constexpr int BM = 128, BN = 64, S = 2; };
+template <> struct CfgOf<7> { static constexpr int BM = 64, BN = 128, S = 2; };
+
+template <int C1, int C2>
+int launch_pair(GemmParams& P1, GemmParams& P2, hipStream_t s) {
+  using X = CfgOf<C1>;
+  using Y = CfgOf<C2>;
+  P1.tiles_m = vqa::cdiv(P1.m, X::BM); P1.tiles_n = vqa::cdiv(P1.n, X::BN);
+  P2.tiles_m = vqa::cdiv(P2.m, Y::BM); P2.tiles_n = vqa::cdiv(P2.n, Y::BN);
+  const int t1 = P1.tiles_m * P1.tiles_n, t1pad = (t1 + 7) / 8 * 8;
+  const int grid = t1pad + P2.tiles_m * P2.tiles_n;
+  hipLaunchKernelGGL((gemm_pair_kernel<X::BM, X::BN, X::S, Y::BM, Y::BN, Y::S>), dim3(grid), dim3(NT), 0, s, P1, P2,
+                     t1pad);
+  return vqa::check_launch("vqa_gemm_pair");
+}
+
+template <int C1>
+int pair_second(int c2, GemmParams& P1, GemmParams& P2, hipStream_t s) {
+  switch (c2) {
+    case 3: return launch_pair<C1, 3>(P1, P2, s);
+    case 6: return launch_pair<C1, 6>(P1, P2, s);
+    case 7: return launch_pair<C1, 7>(P1, P2, s);
+    default: return launch_pair<C1, 4>(P1, P2, s);
+  }
+}
+
+int pair_cfg(int c) { return (c == 3 || c == 6 || c == 7) ? c : 4; }
+}  // namespace
+
+extern "C" int vqa_gemm_pair(const vqa_gemm_desc* dx, const vqa_gemm_desc* dw, hipStream_t stream) {
+  GemmParams P1, P2;
+  if (int rc = prepare(dx, P1)) return rc;
+  if (int rc = prepare(dw, P2)) return rc;
+  const bool shape_ok = !dx->a_trans && dx->b_trans && !dx->a_conv && !dx->b_conv && dx->batch == 1 &&
+                        dw->a_trans && dw->b_trans && !dw->a_conv && !dw->b_conv && dw->batch == 1;
+  if (!shape_ok) {                                       // not a (dX, dW) pair: run them one after the other
+    if (int rc = vqa_gemm(dx, stream)) return rc;
+    return vqa_gemm(dw, stream);
+  }
+  const int c1 = pair_cfg(vqa_gemm_select(dx)), c2 = pair_cfg(vqa_gemm_select(dw));
+  switch (c1) {
+    case 3: return pair_second<3>(c2, P1, P2, stream);
+    case 6: return pair_second<6>(c2, P1, P2, stream);
+    case 7: return pair_second<7>(c2, P1, P2, stream);
+    default: return pair_second<4>(c2, P1, P2, stream);
+  }
 }

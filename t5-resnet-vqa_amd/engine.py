@@ -85,6 +85,7 @@ class VQAEngine:
         self.betas, self.eps, self.wd = betas, eps, weight_decay
         self.grad_scale = grad_scale
         self.group_lr = {}                # per-group LR overrides (trainer optimizer_kwargs)
+        self.pair_bwd = True              # dX + dW of a layer as one paired GEMM launch
         self.T = batch * seq_len
         self.lay = ParamLayout(vision, answer_spaces, num_blocks)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
@@ -348,6 +349,20 @@ class VQAEngine:
         self._gemm(lst, dy16, w, m, k, n, lda=n, ldb=k, b_trans=True, c32=out32, ldc32=k, c16=out16, ldc16=k,
                    res32=res32, ldres=k, mask16=mask16, ldmask=k, beta=beta, alpha=alpha)
 
+    def _dxdw(self, lst, dy16, x16, wname, rows, bias_from=None, **dxkw):
+        """A layer's input gradient and weight gradient (they share dY) as ONE paired
+        launch (vqa_gemm_pair), then the bias column sum."""
+        tmp = []
+        self._dx(tmp, dy16, wname, rows, **dxkw)
+        self._dw(tmp, dy16, x16, wname, rows, bias_from=bias_from)
+        if not self.pair_bwd:
+            lst.extend(tmp)
+            return
+        gx, gw = tmp[0], tmp[1]
+        lst.append(ops.Call("vqa_gemm_pair", ctypes.byref(gx.desc), ctypes.byref(gw.desc), keep=gx.keep + gw.keep,
+                            desc=(gx.desc, gw.desc)))
+        lst.extend(tmp[2:])
+
     def _gbuf(self, name, shape):
         """A bf16 backward buffer private to one use (see _plan_backward)."""
         if name not in self._gbufs:
@@ -478,45 +493,39 @@ class VQAEngine:
             self._call(b, "vqa_layernorm_bwd", dy, s["S3"], s["MU3"], s["RS3"], self.p32[p + "ln3_g"], None,
                        self.dA32, dA3, self.g32[p + "ln3_g"], self.g32[p + "ln3_b"], self.WS_NORM, T, D,
                        self._dptr(sga_site(n, 5), kp), self.g32[p + "fc2_b"], extra=kp + [self.RNG])
-            self._dw(b, dA3, s["FFh"], p + "fc2_w", T)
-            self._dx(b, dA3, p + "fc2_w", T, out16=dB, mask16=s["FFh"], alpha=ks)
-            self._dw(b, dB, s["X2h"], p + "fc1_w", T, bias_from=dB)
-            self._dx(b, dB, p + "fc1_w", T, out32=self.dC32, res32=self.dA32)
+            self._dxdw(b, dA3, s["FFh"], p + "fc2_w", T, out16=dB, mask16=s["FFh"], alpha=ks)
+            self._dxdw(b, dB, s["X2h"], p + "fc1_w", T, bias_from=dB, out32=self.dC32, res32=self.dA32)
             # norm2 + cross attention (q from x, k/v from y)
             kp = []
             self._call(b, "vqa_layernorm_bwd", self.dC32, s["S2"], s["MU2"], s["RS2"], self.p32[p + "ln2_g"], None,
                        self.dA32, dA2, self.g32[p + "ln2_g"], self.g32[p + "ln2_b"], self.WS_NORM, T, D,
                        self._dptr(sga_site(n, 3), kp), self.g32[p + "m2_b"], extra=kp + [self.RNG])
-            self._dw(b, dA2, s["O2"], p + "m2_w", T)
-            self._dx(b, dA2, p + "m2_w", T, out16=self.dO16)
+            self._dxdw(b, dA2, s["O2"], p + "m2_w", T, out16=self.dO16)
             kv = s["KV2"]
             self._attn(b, "vqa_attn_bwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
                        p=s["P2"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=s["lk"], dh=S.SGA_DHEAD, scale=sc,
                        dout=self.dO16, lddo=D, dq=dQ, lddq=D, dk=dKV, lddk=2 * D,
                        dv=ops.addr(dKV, D), lddv=2 * D, drop=sga_site(n, 2))
-            self._dw(b, dQ, s["X1h"], p + "q2_w", T, bias_from=dQ)
-            self._dx(b, dQ, p + "q2_w", T, out32=self.dC32, res32=self.dA32)
-            self._dw(b, dKV, y16, p + "kv2_w", s["ly"], bias_from=dKV)
+            self._dxdw(b, dQ, s["X1h"], p + "q2_w", T, bias_from=dQ, out32=self.dC32, res32=self.dA32)
             if n == 0:
-                self._dx(b, dKV, p + "kv2_w", s["ly"], out32=self.dVIS32, out16=self.dVIS16)
+                self._dxdw(b, dKV, y16, p + "kv2_w", s["ly"], bias_from=dKV, out32=self.dVIS32, out16=self.dVIS16)
             else:
-                self._dx(b, dKV, p + "kv2_w", s["ly"], out32=self.dY[(n - 1) & 1])
+                self._dxdw(b, dKV, y16, p + "kv2_w", s["ly"], bias_from=dKV, out32=self.dY[(n - 1) & 1])
             # norm1 + self attention
             kp = []
             self._call(b, "vqa_layernorm_bwd", self.dC32, s["S1"], s["MU1"], s["RS1"], self.p32[p + "ln1_g"], None,
                        self.dA32, dA1, self.g32[p + "ln1_g"], self.g32[p + "ln1_b"], self.WS_NORM, T, D,
                        self._dptr(sga_site(n, 1), kp), self.g32[p + "m1_b"], extra=kp + [self.RNG])
-            self._dw(b, dA1, s["O1"], p + "m1_w", T)
-            self._dx(b, dA1, p + "m1_w", T, out16=self.dO16)
+            self._dxdw(b, dA1, s["O1"], p + "m1_w", T, out16=self.dO16)
             q = s["QKV1"]
             dq = dQKV
             self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, p=s["P1"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=Lq, dh=S.SGA_DHEAD, scale=sc,
                        dout=self.dO16, lddo=D, dq=dq, lddq=3 * D, dk=ops.addr(dq, D), lddk=3 * D,
                        dv=ops.addr(dq, 2 * D), lddv=3 * D, drop=sga_site(n, 0))
-            self._dw(b, dq, self.TXT16, p + "qkv1_w", T, bias_from=dq)
             # text gradient accumulates over the three blocks (x is the T5 output for every block)
-            self._dx(b, dq, p + "qkv1_w", T, out32=self.dTXT, res32=self.dA32, beta=0.0 if n == NB - 1 else 1.0)
+            self._dxdw(b, dq, self.TXT16, p + "qkv1_w", T, bias_from=dq, out32=self.dTXT, res32=self.dA32,
+                       beta=0.0 if n == NB - 1 else 1.0)
             mark(f"sga{n}.ln3_b")
         # ConvTranspose2d scaler weight/bias gradient: implicit im2col of layer4 as the B operand
         # (vision branch: independent of the T5 backward below; its own colsum workspace)
@@ -540,16 +549,13 @@ class VQAEngine:
         mark("t5.final_ln")
         for i in reversed(range(S.T5_LAYERS)):
             dF, dHM, dQKV = g(f"t5.{i}.dF", (T, S.T5_DFF)), g(f"t5.{i}.dHM", (T, D)), g(f"t5.{i}.dQKV", (T, 3 * D))
-            self._dw(b, dH16[i], self.FF[i], f"t5.{i}.wo", T)
-            self._dx(b, dH16[i], f"t5.{i}.wo", T, out16=dF, mask16=self.FF[i], alpha=ks)
-            self._dw(b, dF, self.N1[i], f"t5.{i}.wi", T)
-            self._dx(b, dF, f"t5.{i}.wi", T, out32=self.dC32)
+            self._dxdw(b, dH16[i], self.FF[i], f"t5.{i}.wo", T, out16=dF, mask16=self.FF[i], alpha=ks)
+            self._dxdw(b, dF, self.N1[i], f"t5.{i}.wi", T, out32=self.dC32)
             kp = []
             self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HM[i], self.R1[i], self.p32[f"t5.{i}.ln1"], self.dH32,
                        self.dHM32, dHM, self.g32[f"t5.{i}.ln1"], 0.0, self.WS_NORM, T, D,
                        None, None, self._dptr(t5_site(i, 1), kp), extra=kp + [self.RNG])
-            self._dw(b, dHM, self.O[i], f"t5.{i}.o_w", T)
-            self._dx(b, dHM, f"t5.{i}.o_w", T, out16=self.dO16)
+            self._dxdw(b, dHM, self.O[i], f"t5.{i}.o_w", T, out16=self.dO16)
             q = self.QKV[i]
             dq = dQKV
             self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
@@ -557,8 +563,7 @@ class VQAEngine:
                        lk=Lq, dh=S.T5_DKV, scale=1.0, dout=self.dO16, lddo=D, dq=dq, lddq=3 * D,
                        dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dSB[i],
                        drop=t5_site(i, 0))
-            self._dw(b, dq, self.N0[i], f"t5.{i}.qkv_w", T)
-            self._dx(b, dq, f"t5.{i}.qkv_w", T, out32=self.dC32)
+            self._dxdw(b, dq, self.N0[i], f"t5.{i}.qkv_w", T, out32=self.dC32)
             # layer 0: dH32 becomes the embedding gradient (masked by the embedding dropout :725);
             # otherwise dH16 is the FF branch gradient of layer i-1
             kp = []
@@ -795,6 +800,27 @@ class VQAEngine:
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         chosen = {}
         for c in self.fwd_calls + self.bwd_calls:
+            if c.name == "vqa_gemm_pair":
+                d1, d2 = c.desc
+                key = repr(("pair", _gemm_key(d1), _gemm_key(d2)))
+                if key not in _TUNE_CACHE:
+                    best = None
+                    for c1 in (3, 4, 6, 7):
+                        for c2 in (3, 4, 6, 7):
+                            d1.config, d2.config = c1, c2
+                            c(s)
+                            st.record()
+                            for _ in range(reps):
+                                c(s)
+                            en.record()
+                            en.synchronize()
+                            t = st.elapsed_time(en)
+                            if best is None or t < best[0]:
+                                best = (t, c1 * 10 + c2)
+                    _TUNE_CACHE[key] = best[1]
+                d1.config, d2.config = _TUNE_CACHE[key] // 10, _TUNE_CACHE[key] % 10
+                chosen[key] = _TUNE_CACHE[key]
+                continue
             if c.name != "vqa_gemm":
                 continue
             d = c.desc

@@ -107,6 +107,7 @@ def load():
         raise RuntimeError(f"libvqa_hip.so ABI {lib.vqa_abi_version()} != header ABI {abi_version()}: rebuild it")
     lib.vqa_gemm.argtypes = [ctypes.POINTER(GemmDesc), c_void_p]
     lib.vqa_gemm_select.argtypes = [ctypes.POINTER(GemmDesc)]
+    lib.vqa_gemm_pair.argtypes = [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc), c_void_p]
     lib.vqa_attn_fwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_attn_bwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_adamw_amsgrad.argtypes = [ctypes.POINTER(AdamWDesc), c_void_p]

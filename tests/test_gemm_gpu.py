@@ -209,3 +209,36 @@ def test_all_tile_configs_bitwise_identical(ops, pkg, layout):
     torch.cuda.synchronize()
     for cfg, o in enumerate(outs[1:], start=2):
         assert torch.equal(o, outs[0]), f"config {cfg} differs from config 1"
+
+
+def test_pair_launch_equals_two_launches(ops, pkg):
+    """vqa_gemm_pair (a layer's dX and dW in one launch) gives exactly the results of the two
+    separate launches, for every config combination it supports (and falls back to two
+    launches for other layouts)."""
+    import ctypes
+    L = pkg.lib
+    T, N, K = 520, 264, 392                        # dX[T, K] = dY[T, N] W[N, K] ; dW[N, K] = dY^T X
+    dy, w, x = bf((T, N), seed=41), bf((N, K), seed=42), bf((T, K), seed=43)
+    mask = bf((T, K), seed=44)
+
+    def descs(out_x, out_w):
+        dxd = ops.gemm_desc(dy, w, T, K, N, lda=N, ldb=K, b_trans=True, c16=out_x, ldc16=K, mask16=mask, ldmask=K,
+                            alpha=1.25)
+        dwd = ops.gemm_desc(dy, x, N, K, T, lda=N, ldb=K, a_trans=True, b_trans=True, c32=out_w, ldc32=K)
+        return dxd, dwd
+    rx, rw = torch.empty(T, K, device="cuda", dtype=torch.bfloat16), torch.empty(N, K, device="cuda")
+    d1, d2 = descs(rx, rw)
+    ops.run(d1)
+    ops.run(d2)
+    torch.cuda.synchronize()
+    ref = torch.where(mask.float() > 0, 1.25 * (dy.float() @ w.float()), torch.zeros(T, K, device="cuda"))
+    close(rx, ref, 1.25 * (dy.float().abs() @ w.float().abs()).max().item(), rtol=1e-2)
+    for c1 in (3, 4, 6, 7):
+        for c2 in (3, 4, 6, 7):
+            ox, ow = torch.empty_like(rx), torch.empty_like(rw)
+            a, b = descs(ox, ow)
+            a.config, b.config = c1, c2
+            rc = L.load().vqa_gemm_pair(ctypes.byref(a), ctypes.byref(b), L.stream_handle())
+            L.check(rc, "pair")
+            torch.cuda.synchronize()
+            assert torch.equal(ox, rx) and torch.equal(ow, rw), (c1, c2)
