@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 3
+#define VQA_ABI_VERSION 4
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -97,12 +97,26 @@ typedef struct vqa_gemm_desc {
   int batch; long long stride_a, stride_b, stride_c32, stride_c16, stride_res;
   int config;              /* 0 auto, else a tile config 1..VQA_GEMM_CONFIGS (speed only: results are identical) */
   vqa_dropout drop;        /* dropout of the (alpha*acc + bias) branch, before the residual */
+  /* split-K: splitk > 1 cuts K into splitk slices of whole 64-deep k-tiles computed by
+   * separate workgroups; the last slice of a tile to finish sums all slices' fp32
+   * partials in slice order (deterministic: same bits for every tile config at a
+   * given splitk, different rounding from splitk = 1) and runs the epilogue.
+   * workspace: >= vqa_gemm_workspace_bytes(d) bytes, zero-filled before its first
+   * use (its counters are left zero after every launch); one in-flight launch per
+   * workspace.  splitk <= 1 ignores it. */
+  int splitk;
+  void* workspace;
+  long long workspace_bytes;
 } vqa_gemm_desc;
 
-#define VQA_GEMM_CONFIGS 8
+/* tile configs: 1 128x128/3 stages, 2 128x64/4, 3 64x64/4, 4 64x64/2, 5 64x64/3, 6 128x64/2,
+ * 7 64x128/2, 8 128x128/2 (4 waves); 9 256x128/2, 10 128x256/2, 11 256x256/2, 12 256x128/3 (8 waves) */
+#define VQA_GEMM_CONFIGS 12
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
 /* tile configuration (1..VQA_GEMM_CONFIGS) that vqa_gemm would run for this descriptor */
 int vqa_gemm_select(const vqa_gemm_desc* d);
+/* workspace bytes vqa_gemm needs for d (its config and splitk; 0 when splitk <= 1) */
+long long vqa_gemm_workspace_bytes(const vqa_gemm_desc* d);
 /* Two independent GEMMs in one launch: a layer's input gradient dX (a_trans=0,
  * b_trans=1) and weight gradient dW (a_trans=1, b_trans=1), both batch 1, no
  * conv.  Each keeps its own epilogue and tile config (configs 3, 4, 6, 7; others

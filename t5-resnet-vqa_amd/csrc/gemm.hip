@@ -29,7 +29,6 @@ __device__ __attribute__((aligned(64))) uint4 vqa_zero_page[4];   // zero-initia
 namespace {
 
 constexpr int BK = 64;
-constexpr int NT = 256;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 struct GemmParams {
@@ -47,6 +46,9 @@ struct GemmParams {
   int tiles_m, tiles_n;
   int vec;                 // LDS-staged 8-wide epilogue legal (N, ld*, pointers 16-B aligned)
   vqa_dropout drop;        // dropout of the (alpha*acc + bias) branch
+  int splitk, kper;        // K slices and 64-deep k-tiles per slice (splitk <= 1: no split)
+  float* slab;             // [batch][tile][slice][BM*BN] fp32 partials, fragment order
+  unsigned* cnt;           // [batch][tile] arrival counters (zero between launches)
 };
 
 // byte offset of 16-B chunk `ch` of row `row` in a k-contig image ([rows][64 bf16])
@@ -55,7 +57,9 @@ __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + ((ch
 // byte offset of chunk `ch` of k-row `kr` in an m/n-contig image ([64][ROWLEN bf16])
 template <int ROWLEN>
 __device__ __forceinline__ int mn_swz(int kr) {
-  if constexpr (ROWLEN == 128) return ((kr & 3) << 2) | ((kr >> 2) & 3);
+  // 256- and 512-B rows: the bank of a chunk depends on its index mod 16 only,
+  // so the same XOR keeps ds_read_b64_tr_b16 conflict-free for both
+  if constexpr (ROWLEN >= 128) return ((kr & 3) << 2) | ((kr >> 2) & 3);
   else return ((((kr >> 1) & 1) << 2) | ((kr >> 2) & 3));
 }
 template <int ROWLEN>
@@ -77,11 +81,13 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
 
 // ---------------------------------------------------------------- LDS-DMA loader
 // One operand tile of ROWS (m or n) x 64 (k): ROWS*128 bytes = ROWS/8 wave
-// instructions of 1 KiB; NI per wave.  KC image: 8 rows per instruction;
-// MN image: 1024 / (2*ROWS) k-rows per instruction.
-template <int ROWS, bool KC, bool GATHER>
+// instructions of 1 KiB; NI per wave (NW waves).  KC image: 8 rows per
+// instruction; MN image: 1024 / (2*ROWS) k-rows per instruction.
+template <int ROWS, bool KC, bool GATHER, int NW>
 struct Loader {
-  static constexpr int NI = ROWS / 32;
+  static_assert(ROWS % (8 * NW) == 0, "operand tile must split evenly over the waves");
+  static_assert(KC || ROWS == 64 || ROWS == 128 || ROWS == 256, "m/n-contig image rows: 64, 128 or 256");
+  static constexpr int NI = ROWS / (8 * NW);
   static constexpr int RPI = KC ? 8 : 1024 / (ROWS * 2);
   static constexpr int CPR = KC ? 8 : ROWS / 8;          // 16-B chunks per image row
   long off[NI];            // KC: element offset of (row, chunk) at k0 = 0; MN: column index
@@ -286,19 +292,26 @@ struct TileCfg {
 // One output tile.  `bid` is the tile's linear id within its problem (the
 // paired launcher offsets it), `smem` the block's LDS ring (a __shared__ array
 // of the calling kernel; inlined, so the LDS address space is preserved).
-template <int BM, int BN, int STAGES, bool AKC, bool BKC, bool GA, bool GB>
+// NWM x NWN waves, each owning a (BM/NWM) x (BN/NWN) sub-tile.
+template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB>
 __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, char* smem) {
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  constexpr int NW = NWM * NWN, NT = 64 * NW;
+  constexpr int WM = BM / NWM, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
+  static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "wave sub-tile must be whole 32x32 blocks");
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, ST_BYTES = A_BYTES + B_BYTES;
-  using LA = Loader<BM, AKC, GA>;
-  using LB = Loader<BN, BKC, GB>;
+  using LA = Loader<BM, AKC, GA, NW>;
+  using LB = Loader<BN, BKC, GB, NW>;
   constexpr int NL = LA::NI + LB::NI;                 // glds instructions per thread per K-tile
 
-  // XCD-aware bijective remap of the linear block id
-  const int nwg = P.tiles_m * P.tiles_n;
+  // XCD-aware bijective remap of the linear block id; with split-K the slices of
+  // one tile are consecutive ids, i.e. (mostly) on one XCD, next to their reducer
+  const int S = P.splitk > 1 ? P.splitk : 1;
+  const int ntile = P.tiles_m * P.tiles_n;
+  const int nwg = ntile * S;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tm = wg / P.tiles_n, tn = wg - tm * P.tiles_n;
+  const int tile = wg / S, slice = wg - tile * S;
+  const int tm = tile / P.tiles_n, tn = tile - tm * P.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int z = blockIdx.z;
@@ -306,7 +319,7 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
   const bf16_t* B = P.b + (long)z * P.sb;
 
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / NWN, wn = w % NWN;
 
   LA la;
   LB lb;
@@ -328,12 +341,14 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  const int nk = (P.k + BK - 1) / BK;
+  const int nk_all = (P.k + BK - 1) / BK;
+  const int kb = S > 1 ? slice * P.kper : 0;                  // this slice's first k-tile
+  const int nk = S > 1 ? min(nk_all - kb, P.kper) : nk_all;   // >= 1 (host checks)
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s) {
     if (s < nk) {
-      la.issue(A, P.lda, smem + s * ST_BYTES, s * BK, P.k, P.ga);
-      lb.issue(B, P.ldb, smem + s * ST_BYTES + A_BYTES, s * BK, P.k, P.gb);
+      la.issue(A, P.lda, smem + s * ST_BYTES, (kb + s) * BK, P.k, P.ga);
+      lb.issue(B, P.ldb, smem + s * ST_BYTES + A_BYTES, (kb + s) * BK, P.k, P.gb);
     }
   }
   for (int kt = 0; kt < nk; ++kt) {
@@ -343,8 +358,8 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
     const int nt = kt + STAGES - 1;
     if (nt < nk) {
       char* st = smem + (nt % STAGES) * ST_BYTES;
-      la.issue(A, P.lda, st, nt * BK, P.k, P.ga);
-      lb.issue(B, P.ldb, st + A_BYTES, nt * BK, P.k, P.gb);
+      la.issue(A, P.lda, st, (kb + nt) * BK, P.k, P.ga);
+      lb.issue(B, P.ldb, st + A_BYTES, (kb + nt) * BK, P.k, P.gb);
     }
     const uint32_t cur = lds0 + (kt % STAGES) * ST_BYTES;
     constexpr int R = FA::READS + FB::READS;
@@ -372,6 +387,72 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
     }
   }
 
+  if (S > 1) {
+    // Split-K hand-off (cdna_hip_programming.md Guideline 16, R1 form): every slice
+    // stores its partials WRITE-THROUGH (sc1 buffer stores, 1 KiB contiguous per wave
+    // store, fragment order), every storing wave drains, then one lane counts the
+    // arrival with a relaxed agent-scope atomic.  The slice that arrives last reads
+    // the other slices' partials with sc1 loads (no release/acquire fences needed)
+    // and sums all slices IN SLICE ORDER, its own from registers -- the result does
+    // not depend on arrival order.  No workgroup waits on another (nothing can
+    // hang); the reducer resets the counter for the next launch.
+    typedef __attribute__((address_space(1))) unsigned gu32;
+    constexpr int FR = TM * TN * 1024;                  // floats per wave
+    const long tlin = (long)z * ntile + tile;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(P.slab + tlin * S * (long)(BM * BN), (short)0, S * BM * BN * 4, 0x00020000);
+    const int wof = w * FR + l * 4;                     // this lane's float offset inside a slice
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const i32x4_t v = {__float_as_int(acc[i][j][4 * g]), __float_as_int(acc[i][j][4 * g + 1]),
+                             __float_as_int(acc[i][j][4 * g + 2]), __float_as_int(acc[i][j][4 * g + 3])};
+          __builtin_amdgcn_raw_buffer_store_b128(v, rs, (slice * (BM * BN) + wof + (i * TN + j) * 1024 + g * 256) * 4,
+                                                 0, 16);
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // EVERY storing wave drains its sc1 stores
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);           // the ring is idle (the K loop drained every DMA)
+    if (tid == 0) {
+      gu32* c = (gu32*)(P.cnt + tlin);
+      const unsigned prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == (unsigned)(S - 1);
+      if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x16_t t;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) t[e] = 0.f;
+        for (int s = 0; s < S; ++s) {
+          if (s == slice) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) t[e] += acc[i][j][e];
+          } else {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const i32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(
+                  rs, (s * (BM * BN) + wof + (i * TN + j) * 1024 + g * 256) * 4, 0, 16);
+              t[4 * g] += __int_as_float(v[0]);
+              t[4 * g + 1] += __int_as_float(v[1]);
+              t[4 * g + 2] += __int_as_float(v[2]);
+              t[4 * g + 3] += __int_as_float(v[3]);
+            }
+          }
+        }
+        acc[i][j] = t;
+      }
+  }
+
   // epilogue: acc[i][j][4g+t] -> row m0+wm*WM+i*32+(l&31), col n0+wn*WN+j*32+8g+4(l>>5)+t.
   // Per element: k = [mask > 0] * dropout multiplier (1 if neither), then
   //   v = k*(alpha*acc + bias) + res ; relu ; c32 = v + beta*c32 ; c16 = bf16(v).
@@ -387,28 +468,34 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
   const int rl = l & 31, ch = l >> 5;
   if (P.vec) {
     // Staged through LDS (the ring is idle now): each wave parks alpha*acc of its
-    // fragments as fp32 rows, then all 256 threads walk the tile row-major, 8
+    // fragments as fp32 rows, then all NT threads walk the tile row-major, 8
     // columns (16-32 B) per thread, so every global access -- bias, residual,
     // mask, old C, the stores -- is a full coalesced line instead of 16-B
-    // pieces of 32 rows.  Two passes of BM/2 rows keep the image <= 64 KiB.
+    // pieces of 32 rows.  One pass per wave row (WM rows) bounds the image.
     constexpr int LDR = BN + 4;                         // fp32 row stride (+16 B: spreads the banks)
-    constexpr int HALF = BM / 2;
-    static_assert(HALF * LDR * 4 <= STAGES * ST_BYTES, "epilogue image must fit the ring");
+    constexpr int RING = STAGES * ST_BYTES;
+    // 32-row fragment groups parked per pass: a wave row's whole sub-tile when it fits
+    constexpr int G = (TM * 32 * LDR * 4 <= RING) ? TM : ((TM / 2) * 32 * LDR * 4 <= RING ? TM / 2 : 1);
+    constexpr int HALF = G * 32;                        // rows per pass
+    constexpr int GPW = TM / G;                         // passes per wave row
+    static_assert(TM % G == 0 && HALF * LDR * 4 <= RING, "epilogue image must fit the ring");
     float* img = reinterpret_cast<float*>(smem);
     constexpr int TPR = BN / 8;                         // threads per row
     constexpr int RPP = NT / TPR;                       // rows per sweep
     // __syncthreads (waits for this wave's LDS ops, then barriers); no LDS-DMA is in flight now
     __syncthreads();                                    // every wave is done with the ring
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      if (wm == pass) {
+    for (int pass = 0; pass < NWM * GPW; ++pass) {
+      const int pw = pass / GPW, pg = pass % GPW;
+      if (wm == pw) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int ii = 0; ii < G; ++ii)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              const int r = i * 32 + rl, c = wn * WN + j * 32 + 8 * g + 4 * ch;
+              const int i = pg * G + ii;
+              const int r = ii * 32 + rl, c = wn * WN + j * 32 + 8 * g + 4 * ch;
               *reinterpret_cast<float4*>(img + r * LDR + c) =
                   make_float4(acc[i][j][4 * g] * P.alpha, acc[i][j][4 * g + 1] * P.alpha,
                               acc[i][j][4 * g + 2] * P.alpha, acc[i][j][4 * g + 3] * P.alpha);
@@ -418,7 +505,7 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
       const int c = (tid % TPR) * 8, col = n0 + c;
 #pragma unroll
       for (int r0 = 0; r0 < HALF; r0 += RPP) {
-        const int r = r0 + tid / TPR, row = m0 + pass * HALF + r;
+        const int r = r0 + tid / TPR, row = m0 + pw * WM + pg * HALF + r;
         if (HALF % RPP != 0 && r >= HALF) continue;
         if (row >= P.m || col >= P.n) continue;
         const float4 x0 = *reinterpret_cast<const float4*>(img + r * LDR + c);
@@ -484,7 +571,7 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
           *reinterpret_cast<uint4*>(C16 + (long)row * P.ldc16 + col) = u;
         }
       }
-      if (pass == 0) __syncthreads();                   // image reused by the second half
+      if (pass + 1 < NWM * GPW) __syncthreads();        // image reused by the next pass
     }
   } else {
     // generic scalar path (odd N or leading dimensions)
@@ -513,10 +600,10 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
   }
 }
 
-template <int BM, int BN, int STAGES, bool AKC, bool BKC, bool GA, bool GB>
-__global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
+template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB>
+__global__ __launch_bounds__(64 * NWM * NWN) void gemm_kernel(GemmParams P) {
   __shared__ __attribute__((aligned(1024))) char smem[TileCfg<BM, BN, STAGES>::LDS];
-  gemm_body<BM, BN, STAGES, AKC, BKC, GA, GB>(P, blockIdx.x, smem);
+  gemm_body<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB>(P, blockIdx.x, smem);
 }
 
 // Two independent problems in one launch (the backward's dX and dW of one
@@ -524,29 +611,42 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams P) {
 // of 8 exits (keeps problem 2's XCD remap aligned), the rest run problem 2.
 // Fills the chip where either GEMM alone leaves CUs idle and saves a launch.
 template <int BM1, int BN1, int S1, int BM2, int BN2, int S2>
-__global__ __launch_bounds__(NT) void gemm_pair_kernel(GemmParams P1, GemmParams P2, int t1pad) {
+__global__ __launch_bounds__(256) void gemm_pair_kernel(GemmParams P1, GemmParams P2, int t1pad) {
   constexpr int L1 = TileCfg<BM1, BN1, S1>::LDS, L2 = TileCfg<BM2, BN2, S2>::LDS;
   __shared__ __attribute__((aligned(1024))) char smem[L1 > L2 ? L1 : L2];
   const int t1 = P1.tiles_m * P1.tiles_n;
   const int bid = blockIdx.x;
   if (bid < t1) {
-    gemm_body<BM1, BN1, S1, true, false, false, false>(P1, bid, smem);       // dX: A k-contig, B n-contig
+    gemm_body<BM1, BN1, S1, 2, 2, true, false, false, false>(P1, bid, smem);       // dX: A k-contig, B n-contig
   } else if (bid >= t1pad) {
-    gemm_body<BM2, BN2, S2, false, false, false, false>(P2, bid - t1pad, smem);   // dW: both m/n-contig
+    gemm_body<BM2, BN2, S2, 2, 2, false, false, false, false>(P2, bid - t1pad, smem);   // dW: both m/n-contig
   }
 }
 
-template <int BM, int BN, int STAGES, bool AKC, bool BKC, bool GA, bool GB>
+// split-K workspace: slabs then counters (16-B aligned)
+long long splitk_bytes(int bm, int bn, int m, int n, int batch, int S) {
+  if (S <= 1) return 0;
+  const long long tiles = (long long)vqa::cdiv(m, bm) * vqa::cdiv(n, bn) * batch;
+  return tiles * S * bm * bn * 4 + (tiles * 4 + 15) / 16 * 16;
+}
+
+template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB>
 int launch(GemmParams& P, int batch, hipStream_t s) {
   P.tiles_m = vqa::cdiv(P.m, BM);
   P.tiles_n = vqa::cdiv(P.n, BN);
-  dim3 grid(P.tiles_m * P.tiles_n, 1, batch);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, STAGES, AKC, BKC, GA, GB>), grid, dim3(NT), 0, s, P);
+  if (P.splitk > 1) {
+    const long long tiles = (long long)P.tiles_m * P.tiles_n * batch;
+    P.cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(P.slab) + tiles * P.splitk * BM * BN * 4);
+  }
+  dim3 grid(P.tiles_m * P.tiles_n * (P.splitk > 1 ? P.splitk : 1), 1, batch);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB>), grid, dim3(64 * NWM * NWN), 0, s, P);
   return vqa::check_launch("vqa_gemm");
 }
 
 // config: 0 = auto; 1 = 128x128 (3 stages); 2 = 128x64 (4); 3 = 64x64 (4); 4 = 64x64 (2);
-//         5 = 64x64 (3); 6 = 128x64 (2); 7 = 64x128 (2); 8 = 128x128 (2).
+//         5 = 64x64 (3); 6 = 128x64 (2); 7 = 64x128 (2); 8 = 128x128 (2)  -- 4 waves (2x2);
+//         9 = 256x128 (2, 8 waves 4x2); 10 = 128x256 (2, 8 waves 2x4); 11 = 256x256 (2, 8 waves 2x4);
+//         12 = 256x128 (3, 8 waves 4x2).
 // Every config accumulates each output element in the same K order (BK = 64
 // k-tiles, 16-deep MFMA steps), so the choice changes speed, never the bits.
 // Auto (measured on MI355X, tools/callprof.py): fewer stages = less LDS = more
@@ -565,24 +665,54 @@ template <bool AKC, bool BKC, bool GA, bool GB>
 int dispatch_tile(GemmParams& P, int batch, int config, hipStream_t s) {
   if (config == 0) config = auto_config(P.m, P.n, P.k, batch);
   switch (config) {
-    case 1: return launch<128, 128, 3, AKC, BKC, GA, GB>(P, batch, s);
-    case 2: return launch<128, 64, 4, AKC, BKC, GA, GB>(P, batch, s);
-    case 4: return launch<64, 64, 2, AKC, BKC, GA, GB>(P, batch, s);
-    case 5: return launch<64, 64, 3, AKC, BKC, GA, GB>(P, batch, s);
-    case 6: return launch<128, 64, 2, AKC, BKC, GA, GB>(P, batch, s);
-    case 7: return launch<64, 128, 2, AKC, BKC, GA, GB>(P, batch, s);
-    case 8: return launch<128, 128, 2, AKC, BKC, GA, GB>(P, batch, s);
-    default: return launch<64, 64, 4, AKC, BKC, GA, GB>(P, batch, s);
+    case 1: return launch<128, 128, 3, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 2: return launch<128, 64, 4, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 4: return launch<64, 64, 2, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 5: return launch<64, 64, 3, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 6: return launch<128, 64, 2, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 7: return launch<64, 128, 2, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 8: return launch<128, 128, 2, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 9: return launch<256, 128, 2, 4, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 10: return launch<128, 256, 2, 2, 4, AKC, BKC, GA, GB>(P, batch, s);
+    case 11: return launch<256, 256, 2, 2, 4, AKC, BKC, GA, GB>(P, batch, s);
+    case 12: return launch<256, 128, 3, 4, 2, AKC, BKC, GA, GB>(P, batch, s);
+    default: return launch<64, 64, 4, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
   }
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// (BM, BN) of a tile config (dispatch_tile's table)
+void tile_of(int config, int& bm, int& bn) {
+  static const int T[VQA_GEMM_CONFIGS + 1][2] = {{64, 64},   {128, 128}, {128, 64}, {64, 64},  {64, 64},
+                                                 {64, 64},   {128, 64},  {64, 128}, {128, 128}, {256, 128},
+                                                 {128, 256}, {256, 256}, {256, 128}};
+  bm = T[config][0];
+  bn = T[config][1];
+}
+
+// slices actually launched: whole k-tiles per slice, no empty slice
+int effective_splitk(int k, int splitk, int* kper) {
+  const int nk = vqa::cdiv(k, BK);
+  if (splitk <= 1 || nk <= 1) { *kper = nk; return 1; }
+  const int per = vqa::cdiv(nk, splitk < nk ? splitk : nk);
+  *kper = per;
+  return vqa::cdiv(nk, per);
+}
 
 }  // namespace
 
 extern "C" int vqa_gemm_select(const vqa_gemm_desc* d) {
   if (!d) return 0;
   return d->config ? d->config : auto_config(d->m, d->n, d->k, d->batch);
+}
+
+extern "C" long long vqa_gemm_workspace_bytes(const vqa_gemm_desc* d) {
+  if (!d || d->splitk <= 1) return 0;
+  int bm, bn, kper;
+  tile_of(vqa_gemm_select(d), bm, bn);
+  const int S = effective_splitk(d->k, d->splitk, &kper);
+  return splitk_bytes(bm, bn, d->m, d->n, d->batch < 1 ? 1 : d->batch, S);
 }
 
 static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
@@ -615,6 +745,24 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
   P.ga = d->ga; P.gb = d->gb;
   P.sa = d->stride_a; P.sb = d->stride_b; P.sc32 = d->stride_c32; P.sc16 = d->stride_c16; P.sres = d->stride_res;
   P.drop = d->drop;
+  P.splitk = 1;
+  P.kper = 0;
+  P.slab = nullptr;
+  P.cnt = nullptr;
+  VQA_REQUIRE(d->splitk >= 0 && d->splitk <= 64, "vqa_gemm: splitk must be 0..64");
+  if (d->splitk > 1) {
+    int kper;
+    const int S = effective_splitk(d->k, d->splitk, &kper);
+    if (S > 1) {
+      const long long need = vqa_gemm_workspace_bytes(d);
+      VQA_REQUIRE(d->workspace && aligned16(d->workspace), "vqa_gemm: splitk needs a 16-byte aligned workspace");
+      VQA_REQUIRE(d->workspace_bytes >= need, "vqa_gemm: workspace %lld bytes < %lld needed for splitk=%d",
+                  d->workspace_bytes, need, d->splitk);
+      P.splitk = S;
+      P.kper = kper;
+      P.slab = (float*)d->workspace;
+    }
+  }
   auto al = [](const void* p, int bytes) { return p == nullptr || ((uintptr_t)p % bytes) == 0; };
   P.vec = d->n % 8 == 0 && (!d->c32 || (d->ldc32 % 8 == 0 && al(d->c32, 16) && d->stride_c32 % 8 == 0)) &&
           (!d->c16 || (d->ldc16 % 8 == 0 && al(d->c16, 16) && d->stride_c16 % 8 == 0)) &&
@@ -654,7 +802,7 @@ int launch_pair(GemmParams& P1, GemmParams& P2, hipStream_t s) {
   P2.tiles_m = vqa::cdiv(P2.m, Y::BM); P2.tiles_n = vqa::cdiv(P2.n, Y::BN);
   const int t1 = P1.tiles_m * P1.tiles_n, t1pad = (t1 + 7) / 8 * 8;
   const int grid = t1pad + P2.tiles_m * P2.tiles_n;
-  hipLaunchKernelGGL((gemm_pair_kernel<X::BM, X::BN, X::S, Y::BM, Y::BN, Y::S>), dim3(grid), dim3(NT), 0, s, P1, P2,
+  hipLaunchKernelGGL((gemm_pair_kernel<X::BM, X::BN, X::S, Y::BM, Y::BN, Y::S>), dim3(grid), dim3(256), 0, s, P1, P2,
                      t1pad);
   return vqa::check_launch("vqa_gemm_pair");
 }
@@ -677,7 +825,8 @@ extern "C" int vqa_gemm_pair(const vqa_gemm_desc* dx, const vqa_gemm_desc* dw, h
   if (int rc = prepare(dx, P1)) return rc;
   if (int rc = prepare(dw, P2)) return rc;
   const bool shape_ok = !dx->a_trans && dx->b_trans && !dx->a_conv && !dx->b_conv && dx->batch == 1 &&
-                        dw->a_trans && dw->b_trans && !dw->a_conv && !dw->b_conv && dw->batch == 1;
+                        dw->a_trans && dw->b_trans && !dw->a_conv && !dw->b_conv && dw->batch == 1 &&
+                        P1.splitk == 1 && P2.splitk == 1;
   if (!shape_ok) {                                       // not a (dX, dW) pair: run them one after the other
     if (int rc = vqa_gemm(dx, stream)) return rc;
     return vqa_gemm(dw, stream);

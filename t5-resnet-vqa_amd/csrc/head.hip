@@ -4,7 +4,8 @@
 //   pooler kernels: one workgroup per sample, each thread keeps its D/256
 //     columns of all L rows in registers, so scores, softmax, pooling and the
 //     pooler backward need a single read of the sample;
-//   classifier contractions (logits, dpooled, dWc): an LDS-tiled fp32 GEMM;
+//   classifier: logits fused into the forward kernel; dpooled and dWc by an
+//     LDS-tiled fp32 GEMM;
 //   every reduction runs in a fixed order (bit-reproducible).
 #include <type_traits>
 
@@ -76,14 +77,21 @@ __device__ __forceinline__ void block_row_sums(float (&part)[LMAX], int L, float
   __syncthreads();
 }
 
-// scores = x wp + bp ; a = softmax_t(scores) ; pooled = a^T x     (D <= 768: 3 columns per thread)
+// The whole forward head of one sample in one workgroup (resnet_vqa_model.py:152-160):
+// pooler (scores, softmax over L, weighted sum) -> pooled row in LDS -> 170 logits, one wave per
+// answer at a time, lanes striding the D-long dot so the Wc row read is one
+// coalesced 256-B access per step -> log_softmax over the answers in LDS -> NLL.
+// Replaces a K=768 LDS-tiled sgemm whose 12 workgroups walked K serially (~33 us).
 template <int LMAX>
-__global__ __launch_bounds__(256) void pool_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wp,
-                                                       const float* __restrict__ bp, float* __restrict__ att,
-                                                       float* __restrict__ pooled, int L, int D) {
+__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wp,
+                                                       const float* __restrict__ bp, const float* __restrict__ wc,
+                                                       const float* __restrict__ bc, const long long* __restrict__ tgt,
+                                                       float* __restrict__ att, float* __restrict__ pooled,
+                                                       float* __restrict__ logp, float* __restrict__ nll, int L, int D,
+                                                       int A) {
   constexpr int NC = 3;
-  __shared__ float red[4 * LMAX], sc[LMAX];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ float red[4 * LMAX], sc[LMAX], pr[768], lg[MAXA], r4[4];
+  const int b = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const float* xb = x + (long)b * L * D;
   float xr[LMAX][NC], part[LMAX];
   float w[NC];
@@ -117,31 +125,32 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const float* __restrict__
     for (int t = 0; t < LMAX; ++t)
       if (t < L) p = fmaf(sc[t], xr[t][j], p);
     pooled[(long)b * D + d] = p;
+    pr[d] = p;
   }
-}
-
-// log_softmax over the A logits of one sample, NLL of its target
-__global__ __launch_bounds__(256) void lse_kernel(const float* __restrict__ logits, const long long* __restrict__ tgt,
-                                                  float* __restrict__ logp, float* __restrict__ nll, int A) {
-  __shared__ float red[4];
-  const int b = blockIdx.x, wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const float* lg = logits + (long)b * A;
-  float m = -INFINITY;
-  for (int c = threadIdx.x; c < A; c += 256) m = fmaxf(m, lg[c]);
-  m = wave_max(m);
-  if (l == 0) red[wv] = m;
   __syncthreads();
-  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  const float lt = (threadIdx.x == 0 && tgt) ? lg[tgt[b]] : 0.f;    // read before the in-place write below
+  for (int a = wv; a < A; a += 4) {                   // logits = pooled Wc^T + bc
+    const float* wr = wc + (long)a * D;
+    float s = 0.f;
+    for (int k = l; k < D; k += 64) s = fmaf(pr[k], wr[k], s);
+    s = wave_sum(s);
+    if (l == 0) lg[a] = s + bc[a];
+  }
+  __syncthreads();
+  float m = -INFINITY;
+  for (int c = tid; c < A; c += 256) m = fmaxf(m, lg[c]);
+  m = wave_max(m);
+  if (l == 0) r4[wv] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(r4[0], r4[1]), fmaxf(r4[2], r4[3]));
   __syncthreads();
   float z = 0.f;
-  for (int c = threadIdx.x; c < A; c += 256) z += __expf(lg[c] - m);
+  for (int c = tid; c < A; c += 256) z += __expf(lg[c] - m);
   z = wave_sum(z);
-  if (l == 0) red[wv] = z;
+  if (l == 0) r4[wv] = z;
   __syncthreads();
-  const float lse = m + __logf(red[0] + red[1] + red[2] + red[3]);
-  for (int c = threadIdx.x; c < A; c += 256) logp[(long)b * A + c] = lg[c] - lse;
-  if (threadIdx.x == 0 && tgt) nll[b] = -(lt - lse);
+  const float lse = m + __logf(r4[0] + r4[1] + r4[2] + r4[3]);
+  for (int c = tid; c < A; c += 256) logp[(long)b * A + c] = lg[c] - lse;
+  if (tid == 0 && tgt) nll[b] = -(lg[tgt[b]] - lse);
 }
 
 // fixed-order mean / sum of n values by one workgroup
@@ -251,15 +260,11 @@ extern "C" int vqa_head_fwd(const float* x, const float* wp, const float* bp, co
   VQA_REQUIRE(seq <= 64 && d <= 768 && answers <= MAXA, "vqa_head_fwd: shape out of range (L<=64, D<=768)");
   VQA_REQUIRE(!targets || (nll && loss), "vqa_head_fwd: targets need nll and loss outputs");
   int rc = with_lmax(seq, [&](auto lm) {
-    hipLaunchKernelGGL(pool_fwd_kernel<decltype(lm)::value>, dim3(batch), dim3(256), 0, s, x, wp, bp, att, pooled,
-                       seq, d);
-    return vqa::check_launch("vqa_head_fwd/pool");
+    hipLaunchKernelGGL(head_fwd_kernel<decltype(lm)::value>, dim3(batch), dim3(256), 0, s, x, wp, bp, wc, bc, targets,
+                       att, pooled, logp, nll, seq, d, answers);
+    return vqa::check_launch("vqa_head_fwd");
   });
   if (rc) return rc;
-  // logits are staged in logp, then replaced by log_softmax in place
-  if ((rc = sgemm(s, batch, answers, d, pooled, d, 1, wc, 1, d, logp, answers, bc))) return rc;
-  hipLaunchKernelGGL(lse_kernel, dim3(batch), dim3(256), 0, s, logp, targets, logp, nll, answers);
-  if ((rc = vqa::check_launch("vqa_head_fwd/lse"))) return rc;
   if (targets) {
     hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, s, nll, batch, 1.0f / batch, loss);
     return vqa::check_launch("vqa_head_fwd/mean");

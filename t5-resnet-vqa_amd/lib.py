@@ -46,6 +46,7 @@ class GemmDesc(ctypes.Structure):
         ("batch", c_int), ("stride_a", c_ll), ("stride_b", c_ll), ("stride_c32", c_ll),
         ("stride_c16", c_ll), ("stride_res", c_ll), ("config", c_int),
         ("drop", Dropout),
+        ("splitk", c_int), ("workspace", c_void_p), ("workspace_bytes", c_ll),
     ]
 
 
@@ -61,8 +62,10 @@ class AttnDesc(ctypes.Structure):
 
 
 # vqa_gemm tile configs (gemm.hip dispatch_tile): config -> (BM, BN, LDS stages)
+# config -> (BM, BN, stages); 1-8 run 4 waves (2x2), 9-12 run 8 waves (include/vqa_hip.h)
 GEMM_TILES = {1: (128, 128, 3), 2: (128, 64, 4), 3: (64, 64, 4), 4: (64, 64, 2), 5: (64, 64, 3), 6: (128, 64, 2),
-              7: (64, 128, 2), 8: (128, 128, 2)}
+              7: (64, 128, 2), 8: (128, 128, 2), 9: (256, 128, 2), 10: (128, 256, 2), 11: (256, 256, 2),
+              12: (256, 128, 3)}
 
 MAX_GROUPS = 8
 ST_STEP, ST_GRAD_NORM, ST_CLIP_COEF, ST_LR_SCALE, ST_BC1, ST_BC2_SQRT = range(6)
@@ -107,6 +110,8 @@ def load():
         raise RuntimeError(f"libvqa_hip.so ABI {lib.vqa_abi_version()} != header ABI {abi_version()}: rebuild it")
     lib.vqa_gemm.argtypes = [ctypes.POINTER(GemmDesc), c_void_p]
     lib.vqa_gemm_select.argtypes = [ctypes.POINTER(GemmDesc)]
+    lib.vqa_gemm_workspace_bytes.argtypes = [ctypes.POINTER(GemmDesc)]
+    lib.vqa_gemm_workspace_bytes.restype = c_ll
     lib.vqa_gemm_pair.argtypes = [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc), c_void_p]
     lib.vqa_attn_fwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_attn_bwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]

@@ -29,7 +29,7 @@ def conv_geom(n, h, w, c, oh, ow, kh, kw, stride, pad):
 def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None, ldc32=0, c16=None, ldc16=0,
               bias=None, res32=None, res16=None, ldres=0, mask16=None, ldmask=0, alpha=1.0, beta=0.0,
               relu=False, ga=None, gb=None, batch=1, stride_a=0, stride_b=0, stride_c32=0, stride_c16=0,
-              stride_res=0):
+              stride_res=0, splitk=0, workspace=None):
     for t in (a, b, c16, res16, mask16):
         assert not isinstance(t, torch.Tensor) or t.dtype == torch.bfloat16, "bf16 operand expected"
     for t in (c32, bias, res32):
@@ -55,7 +55,22 @@ def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None
         d.gb = gb
     d.batch, d.stride_a, d.stride_b = batch, stride_a, stride_b
     d.stride_c32, d.stride_c16, d.stride_res = stride_c32, stride_c16, stride_res
+    set_splitk(d, splitk, workspace)
     return d
+
+
+def set_splitk(d, splitk, workspace=None):
+    """Split-K of a descriptor: `workspace` (a zero-filled device tensor, see
+    vqa_gemm_workspace_bytes) holds the fp32 partials and arrival counters."""
+    d.splitk = int(splitk)
+    d.workspace = addr(workspace)
+    d.workspace_bytes = 0 if workspace is None else workspace.numel() * workspace.element_size()
+
+
+def splitk_workspace(d, device="cuda"):
+    """A zero-filled workspace large enough for descriptor `d` as configured now."""
+    n = int(L.load().vqa_gemm_workspace_bytes(ctypes.byref(d)))
+    return torch.zeros(max(n, 16) // 4 + 4, dtype=torch.int32, device=device)
 
 
 class Call:

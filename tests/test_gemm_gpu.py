@@ -28,7 +28,7 @@ def close(got, ref, scale, rtol=2e-5):
     assert err <= rtol * scale + 1e-6, f"max err {err} vs scale {scale}"
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 9, 10, 11, 12])
 @pytest.mark.parametrize("M,N,K", [(2048, 2304, 768), (100, 200, 136), (64, 170, 768), (3136, 768, 1024),
                                    (37, 24, 8)])
 def test_linear_forward_epilogue(ops, M, N, K, cfg):
@@ -48,7 +48,7 @@ def test_linear_forward_epilogue(ops, M, N, K, cfg):
     assert (out16.float() - ref).abs().max().item() <= ref.abs().max().item() * 2 ** -8 + 1e-6
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 9, 10, 11, 12])
 @pytest.mark.parametrize("M,N,K", [(2048, 768, 2304), (96, 136, 200), (2048, 3072, 768)])
 def test_input_grad_layout(ops, M, N, K, cfg):
     # dX[M, N] = dY[M, K] @ W[K, N]  (W stored [K, N] row-major: B n-contig)
@@ -61,7 +61,7 @@ def test_input_grad_layout(ops, M, N, K, cfg):
     close(out, dy.float() @ w.float(), (dy.float().abs() @ w.float().abs()).max().item())
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 9, 10, 11, 12])
 @pytest.mark.parametrize("NO,KI,T", [(768, 768, 2048), (2304, 768, 3136), (136, 64, 200), (8, 16, 40)])
 def test_weight_grad_layout(ops, NO, KI, T, cfg):
     # dW[NO, KI] = dY[T, NO]^T @ X[T, KI]   (A m-contig, B n-contig)
@@ -123,7 +123,7 @@ def test_dropout_epilogue(ops, pkg, vec, relu):
     assert ((c == 0) == (v == 0)).float().mean() > 0.999
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 9, 11])
 @pytest.mark.parametrize("n,h,w,c,co,k,s,p", [
     (2, 56, 56, 64, 64, 1, 1, 0), (2, 56, 56, 64, 128, 3, 1, 1), (2, 56, 56, 128, 128, 3, 2, 1),
     (2, 28, 28, 256, 512, 1, 2, 0), (2, 32, 32, 8, 64, 7, 2, 3), (3, 7, 7, 2048, 768, 3, 1, 1)])
@@ -146,7 +146,7 @@ def test_conv_forward_gather(ops, pkg, n, h, w, c, co, k, s, p, cfg):
     close(out, ref, scale)
 
 
-@pytest.mark.parametrize("cfg", [0, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 2, 3, 10, 11])
 @pytest.mark.parametrize("n,h,c,co", [(2, 7, 64, 96), (4, 7, 2048, 768)])
 def test_conv_weight_grad_gather(ops, n, h, c, co, cfg):
     # ConvTranspose2d(k3,s1,p1) dW as the weight-grad of the equivalent conv: B = implicit im2col
@@ -242,3 +242,63 @@ def test_pair_launch_equals_two_launches(ops, pkg):
             L.check(rc, "pair")
             torch.cuda.synchronize()
             assert torch.equal(ox, rx) and torch.equal(ow, rw), (c1, c2)
+
+
+@pytest.mark.parametrize("layout", ["AB", "ABt", "AtBt", "conv"])
+@pytest.mark.parametrize("splitk", [2, 3, 5])
+def test_splitk_matches_reference_and_is_config_invariant(ops, pkg, layout, splitk):
+    """Split-K: every slice's partials are summed in slice order by the last slice to
+    arrive, so (i) the result matches the fp32 reference, (ii) it is bit-identical
+    for every tile config at the same splitk, (iii) repeated launches (counter reuse)
+    give the same bits."""
+    rng = torch.tensor([3, 4, 1], dtype=torch.int32, device="cuda")
+    if layout == "conv":
+        nb, h, c, co = 2, 7, 256, 200
+        x = bf((nb, h, h, c), seed=51)
+        wt = bf((co, 3, 3, c), 0.05, seed=52)
+        g = ops.conv_geom(nb, h, h, c, h, h, 3, 3, 1, 1)
+        M, N, K = nb * h * h, co, 9 * c
+        bias = torch.randn(N, device="cuda")
+        mk = lambda out: ops.gemm_desc(x, wt, M, N, K, lda=K, ldb=K, c32=out, ldc32=N, bias=bias, ga=g)
+        ref = F.conv2d(x.float().permute(0, 3, 1, 2), wt.float().permute(0, 3, 1, 2), bias, padding=1)
+        ref = ref.permute(0, 2, 3, 1).reshape(M, N)
+        scale = F.conv2d(x.float().abs().permute(0, 3, 1, 2), wt.float().abs().permute(0, 3, 1, 2),
+                         padding=1).max().item()
+    else:
+        M, N, K = 328, 264, 1800
+        at, bt = layout == "AtBt", layout in ("ABt", "AtBt")
+        a = bf((K, M) if at else (M, K), seed=53)
+        b = bf((K, N) if bt else (N, K), seed=54)
+        res = torch.randn(M, N, device="cuda")
+        A = a.float().T if at else a.float()
+        Bm = b.float() if bt else b.float().T
+
+        def mk(out):
+            return ops.gemm_desc(a, b, M, N, K, lda=M if at else K, ldb=N if bt else K, a_trans=at, b_trans=bt,
+                                 c32=out, ldc32=N, res32=res, ldres=N, alpha=0.5)
+        ref = 0.5 * (A @ Bm) + res
+        scale = 0.5 * (A.abs() @ Bm.abs()).max().item()
+    outs = []
+    cfgs = sorted(pkg.lib.GEMM_TILES)
+    nk = -(-K // 64)
+    per = -(-nk // min(splitk, nk))
+    s_eff = -(-nk // per)
+    for cfg in cfgs:
+        out = torch.full((M, N), float("nan"), device="cuda")
+        d = mk(out)
+        d.config = cfg
+        ops.set_splitk(d, splitk)
+        ws = ops.splitk_workspace(d)
+        ops.set_splitk(d, splitk, ws)
+        ops.run(d)
+        ops.run(d)                                       # second launch reuses the counters
+        outs.append(out)
+        bm, bn, _ = pkg.lib.GEMM_TILES[cfg]
+        tiles = -(-M // bm) * -(-N // bn)
+        off = tiles * s_eff * bm * bn
+        torch.cuda.synchronize()
+        assert int(ws[off:off + tiles].abs().sum()) == 0, "arrival counters must be left zero"
+    torch.cuda.synchronize()
+    close(outs[0], ref, scale)
+    for cfg, o in zip(cfgs[1:], outs[1:]):
+        assert torch.equal(o, outs[0]), f"config {cfg} differs at splitk={splitk}"

@@ -5,8 +5,8 @@ sys.path.insert(0, ROOT)
 import torch
 from __graft_entry__ import load_package
 pkg = load_package(); ops = pkg.ops; L = pkg.lib
-shapes = [(2048, 768, 768), (2048, 3072, 768), (2048, 768, 3072), (2048, 2304, 768), (3136, 768, 18432), (8192, 8192, 8192)]
-cfgs = [int(c) for c in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 3]
+shapes = [(2048, 768, 768), (2048, 3072, 768), (2048, 768, 3072), (2048, 2304, 768), (3136, 768, 18432), (4096, 4096, 4096), (8192, 8192, 8192)]
+cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["1", "3"]          # "<config>[s<splitk>]"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 s = L.stream_handle()
 for M, N, K in shapes:
@@ -17,15 +17,21 @@ for M, N, K in shapes:
     fl = 2.0 * M * N * K
     for cfg in cfgs:
         d = ops.gemm_desc(a, b, M, N, K, lda=K, ldb=K, c16=c, ldc16=N)
-        d.config = cfg
-        call = ops.gemm_call(d)
+        cf, _, sk = cfg.partition("s")
+        d.config = int(cf)
+        ws = None
+        if sk:
+            ops.set_splitk(d, int(sk))
+            ws = ops.splitk_workspace(d)
+            ops.set_splitk(d, int(sk), ws)
+        call = ops.gemm_call(d, (a, b, c, ws))
         for _ in range(3): call(s)
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st.record()
         for _ in range(reps): call(s)
         en.record(); en.synchronize()
         t = st.elapsed_time(en) / reps * 1e-3
-        line += f" | c{cfg} {t*1e6:8.1f}us {fl/t/1e12:6.0f}TF"
+        line += f" | c{cfg} {t*1e6:7.1f}us {fl/t/1e12:5.0f}"
     for _ in range(3): torch.matmul(a, b.T, out=c)
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     st.record()
