@@ -211,6 +211,11 @@ int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int 
 /* deterministic: each touched row is written once (sorted, fixed token order); tokens <= 8192; ws = 3*tokens ints */
 int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab, int* ws,
                       hipStream_t stream);
+/* zero the dtable rows named by ids_prev[0, tokens) (the rows the previous vqa_embedding_bwd
+ * wrote), then ids_prev = ids_cur when ids_cur != NULL: keeps the dense gradient zero outside
+ * the touched rows without clearing all vocab*d floats every step */
+int vqa_embedding_zero_rows(long long* ids_prev, const long long* ids_cur, int tokens, float* dtable, int d,
+                            int vocab, hipStream_t stream);
 int vqa_t5_relbias_fwd(const float* table, const int* bucket, float* out, int heads, int lq, int lk,
                        hipStream_t stream);
 /* dtable[b, h] = sum_{(i,j): bucket = b} dbias[h, i, j] (overwrites, fixed order) */

@@ -42,9 +42,17 @@ struct AttnM {
   vqa_dropout drop;
 };
 
+// Every global load below is issued UNconditionally at a clamped (valid) address
+// and zeroed afterwards by an AND mask / multiply: "if (ok) load" or "ok ? load : 0"
+// makes hipcc branch around each load and wait for it (one L2 round trip per
+// load, cdna_hip_programming.md §5 'Three .s-level traps' (c)).
+__device__ __forceinline__ uint32_t okmask(bool ok) { return ok ? 0xffffffffu : 0u; }
+
+// `row` must point at a valid row (callers clamp the index); ok = 0 zeroes the fragment
 __device__ __forceinline__ bf16x8_t ld_frag(const bf16_t* row, bool ok) {
-  uint4 u = make_uint4(0, 0, 0, 0);
-  if (ok) u = *reinterpret_cast<const uint4*>(row);
+  uint4 u = *reinterpret_cast<const uint4*>(row);
+  const uint32_t m = okmask(ok);
+  u.x &= m; u.y &= m; u.z &= m; u.w &= m;
   return __builtin_bit_cast(bf16x8_t, u);
 }
 
@@ -78,8 +86,8 @@ __device__ __forceinline__ void stage_img(lds_char* img, const bf16_t* src, long
 #pragma unroll
   for (int j = 0; j < PER; ++j) {                       // all loads first, then all LDS writes
     const int idx = l + 64 * j, r = idx / CPR, c = idx - r * CPR;
-    u[j] = u32x4{0u, 0u, 0u, 0u};
-    if (r < n) u[j] = *reinterpret_cast<const u32x4*>(src + (long)r * ld + c * 8);
+    u[j] = *reinterpret_cast<const u32x4*>(src + (long)max(min(r, n - 1), 0) * ld + c * 8);
+    u[j] &= u32x4{okmask(r < n), okmask(r < n), okmask(r < n), okmask(r < n)};
   }
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -140,13 +148,37 @@ __global__ __launch_bounds__(64 * WPB) void attn_fwd_mfma(AttnM P) {
 
   // fragments with k = head dim straight from global (16 B per lane per k-step)
   bf16x8_t qf[G::KS], kf[2][G::KS];
+  const int qr = min(l31, lq - 1), kr0 = min(l31, lk - 1), kr1 = min(32 + l31, lk - 1);   // clamped rows
 #pragma unroll
   for (int s = 0; s < G::KS; ++s) {
-    qf[s] = ld_frag(Q + (long)l31 * P.ldq + 16 * s + 8 * h5, live && l31 < lq);
-    kf[0][s] = ld_frag(K + (long)l31 * P.ldk + 16 * s + 8 * h5, live && l31 < lk);
-    kf[1][s] = ld_frag(K + (long)(32 + l31) * P.ldk + 16 * s + 8 * h5, live && 32 + l31 < lk);
+    qf[s] = ld_frag(Q + (long)qr * P.ldq + 16 * s + 8 * h5, live && l31 < lq);
+    kf[0][s] = ld_frag(K + (long)kr0 * P.ldk + 16 * s + 8 * h5, live && l31 < lk);
+    kf[1][s] = ld_frag(K + (long)kr1 * P.ldk + 16 * s + 8 * h5, live && 32 + l31 < lk);
   }
   stage_img<DH, 64, G::ROWB>(vimg, V, P.ldv, live ? lk : 0);
+  // additive score terms (rel-bias row, key-padding mask) for this lane's 32 keys,
+  // loaded up front at clamped indices (uniform pointer tests only)
+  const int i = l31;
+  float add[2][16];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) add[t][r] = 0.f;
+  if (P.bias) {
+    const float* brow = P.bias + ((long)hh * lq + min(i, lq - 1)) * lk;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) add[t][r] = brow[min(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5, lk - 1)];
+  }
+  if (P.mask) {
+    const long long* mrow = P.mask + (long)b * lk;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        add[t][r] += mrow[min(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5, lk - 1)] == 0 ? MASK_MIN : 0.f;
+  }
 
   // S^T tiles (X layout: lane = query, registers = keys)
   f32x16_t sa[2];
@@ -160,19 +192,13 @@ __global__ __launch_bounds__(64 * WPB) void attn_fwd_mfma(AttnM P) {
     }
   }
   // softmax over keys for query i = l31
-  const int i = l31;
   float mx = -INFINITY;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5;
-      float v = -INFINITY;
-      if (key < lk) {
-        v = sa[t][r] * P.scale;
-        if (P.bias) v += P.bias[((long)hh * lq + min(i, lq - 1)) * lk + key];
-        if (P.mask && P.mask[(long)b * lk + key] == 0) v += MASK_MIN;
-      }
+      const float v = key < lk ? sa[t][r] * P.scale + add[t][r] : -INFINITY;
       sa[t][r] = v;
       mx = fmaxf(mx, v);
     }
@@ -241,11 +267,12 @@ __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
   const float* Pg = P.p + ((long)b * P.heads + hh) * lq * lk;
 
   bf16x8_t of[G::KS], vf[2][G::KS];
+  const int qr = min(l31, lq - 1), kr0 = min(l31, lk - 1), kr1 = min(32 + l31, lk - 1);   // clamped rows
 #pragma unroll
   for (int s = 0; s < G::KS; ++s) {
-    of[s] = ld_frag(dO + (long)l31 * P.lddo + 16 * s + 8 * h5, live && l31 < lq);
-    vf[0][s] = ld_frag(V + (long)l31 * P.ldv + 16 * s + 8 * h5, live && l31 < lk);
-    vf[1][s] = ld_frag(V + (long)(32 + l31) * P.ldv + 16 * s + 8 * h5, live && 32 + l31 < lk);
+    of[s] = ld_frag(dO + (long)qr * P.lddo + 16 * s + 8 * h5, live && l31 < lq);
+    vf[0][s] = ld_frag(V + (long)kr0 * P.ldv + 16 * s + 8 * h5, live && l31 < lk);
+    vf[1][s] = ld_frag(V + (long)kr1 * P.ldv + 16 * s + 8 * h5, live && 32 + l31 < lk);
   }
   stage_img<DH, 64, G::ROWB>(kimg, K, P.ldk, live ? lk : 0);
   stage_img<DH, 32, G::ROWB>(oimg, dO, P.lddo, live ? lq : 0);
@@ -268,13 +295,21 @@ __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
     }
   }
   float px[2][16];
+  const float* prow = Pg + (long)min(i, lq - 1) * lk;   // saved P of this lane's query (clamped row)
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5;
+      px[t][r] = prow[min(key, lk - 1)];                // unconditional loads, masked below
+    }
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5;
       const bool ok = qok && key < lk;
-      const float pr = ok ? Pg[(long)i * lk + key] : 0.f;
+      const float pr = px[t][r] * (ok ? 1.f : 0.f);
       const float dp = ok ? xa[t][r] * drop_mul(dk, (uint32_t)(pbase + (long)i * lk + key)) : 0.f;
       px[t][r] = pr;
       xa[t][r] = dp;                                    // dP (gradient w.r.t. the pre-dropout P)
@@ -316,12 +351,16 @@ __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
 #pragma unroll
     for (int s = 0; s < G::KS; ++s) ya = mfma(of[s], vf[t][s], ya);        // dP[query][key]
     f32x16_t pd, dsy;
+    float pv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)                          // unconditional loads at clamped (query, key)
+      pv[r] = Pg[(long)min((r & 3) + 8 * (r >> 2) + 4 * h5, lq - 1) * lk + min(key, lk - 1)];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qi = (r & 3) + 8 * (r >> 2) + 4 * h5;
       const bool ok = kok && qi < lq;
       const long e = pbase + (long)qi * lk + key;
-      const float pr = ok ? Pg[(long)qi * lk + key] : 0.f;
+      const float pr = pv[r] * (ok ? 1.f : 0.f);
       const float m = ok ? drop_mul(dk, (uint32_t)e) : 0.f;
       pd[r] = pr * m;                                   // dropout(P)
       dsy[r] = ok ? pr * (ya[r] * m - dis[qi]) : 0.f;   // dS

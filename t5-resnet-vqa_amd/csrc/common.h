@@ -33,6 +33,31 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// N independent 64-lane sums at once (N a power of two <= 64) by a butterfly
+// reduce-scatter: each exchange step halves the values a lane keeps, so the N sums
+// cost N-1 + log2(64/N) shuffles instead of 6N.  Returns the sum of value index
+// (lane >> (6 - log2 N)) -- every lane of that index's group holds it.
+template <int N>
+__device__ __forceinline__ float wave_sum_scatter(float (&v)[N]) {
+  static_assert(N >= 1 && N <= 64 && (N & (N - 1)) == 0, "N must be a power of two <= 64");
+  const int l = threadIdx.x & 63;
+  int m = 32;
+#pragma unroll
+  for (int c = N; c > 1; c >>= 1, m >>= 1) {
+    const bool up = (l & m) != 0;
+#pragma unroll
+    for (int i = 0; i < c / 2; ++i) {
+      const float keep = up ? v[c / 2 + i] : v[i];
+      const float send = up ? v[i] : v[c / 2 + i];
+      v[i] = keep + __shfl_xor(send, m, 64);
+    }
+  }
+  float r = v[0];
+#pragma unroll
+  for (; m > 0; m >>= 1) r += __shfl_xor(r, m, 64);
+  return r;
+}
+
 // block-wide sum for blockDim.x == NT (multiple of 64); `red` must hold NT/64 floats
 template <int NT>
 __device__ __forceinline__ float block_sum(float v, float* red) {

@@ -115,6 +115,21 @@ __global__ __launch_bounds__(256) void dropout_mask_kernel(vqa_dropout d, float*
   out[i] = drop_mul(dk, (uint32_t)i);
 }
 
+// Re-zero only the table rows the previous step's gradient wrote (its ids),
+// instead of the whole dense [vocab, d] gradient; then remember this step's ids.
+// One workgroup per token: reads its previous id before replacing it.
+__global__ __launch_bounds__(256) void embedding_zero_rows_kernel(long long* __restrict__ prev,
+                                                                  const long long* __restrict__ cur,
+                                                                  float* __restrict__ dtable, int d, int vocab) {
+  const int t = blockIdx.x;
+  long long id = prev[t];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  float4* row = reinterpret_cast<float4*>(dtable + id * (long long)d);
+  for (int c = threadIdx.x; c < d / 4; c += 256) row[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  if (cur && threadIdx.x == 0) prev[t] = cur[t];
+}
+
 // Deterministic dense embedding gradient (nn.Embedding sparse=False), no atomics:
 //   1. one workgroup bitonic-sorts the keys (id << 16 | position) in LDS, which
 //      groups equal ids with their positions in token order, and finds each
@@ -338,6 +353,13 @@ extern "C" int vqa_dropout_mask(const vqa_dropout* d, float* out, long long n, h
   VQA_REQUIRE(d->p >= 0.f && d->p < 1.f, "vqa_dropout_mask: p must be in [0, 1)");
   hipLaunchKernelGGL(dropout_mask_kernel, dim3(vqa::cdiv(n, 256)), dim3(256), 0, s, *d, out, (long)n);
   return vqa::check_launch("vqa_dropout_mask");
+}
+
+extern "C" int vqa_embedding_zero_rows(long long* ids_prev, const long long* ids_cur, int tokens, float* dtable,
+                                       int d, int vocab, hipStream_t s) {
+  VQA_REQUIRE(ids_prev && dtable && tokens > 0 && d % 4 == 0 && vocab > 0, "vqa_embedding_zero_rows: bad arguments");
+  hipLaunchKernelGGL(embedding_zero_rows_kernel, dim3(tokens), dim3(256), 0, s, ids_prev, ids_cur, dtable, d, vocab);
+  return vqa::check_launch("vqa_embedding_zero_rows");
 }
 
 extern "C" int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab,

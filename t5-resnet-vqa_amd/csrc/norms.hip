@@ -125,9 +125,10 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* __restric
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   for (int row = r0 + wv; row < r1; row += ROWS_PER_BLOCK) {
-    float d[NV][4], v[NV][4];
+    float d[NV][4], v[NV][4], o[NV][4];
     load_row<NV>(dy + (long)row * D, d);
     load_row<NV>(x + (long)row * D, v);
+    if (dres) load_row<NV>(dres + (long)row * D, o);   // issued with dy and x: one round trip per row
     drop_row<NV>(kdy, row, d);
     const float r = rstd[row];
     float s = 0.f;
@@ -140,8 +141,6 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* __restric
       }
     s = wave_sum(s);
     const float c = r * r * r * s / D;
-    float o[NV][4];
-    if (dres) load_row<NV>(dres + (long)row * D, o);
 #pragma unroll
     for (int i = 0; i < NV; ++i)
 #pragma unroll
@@ -217,9 +216,10 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   for (int row = r0 + wv; row < r1; row += ROWS_PER_BLOCK) {
-    float d[NV][4], v[NV][4];
+    float d[NV][4], v[NV][4], o[NV][4];
     load_row<NV>(dy + (long)row * D, d);
     load_row<NV>(x + (long)row * D, v);
+    if (dres) load_row<NV>(dres + (long)row * D, o);   // issued with dy and x: one round trip per row
     const float mu = mean[row], r = rstd[row];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -235,8 +235,6 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
       }
     s1 = wave_sum(s1) / D;
     s2 = wave_sum(s2) / D;
-    float o[NV][4];
-    if (dres) load_row<NV>(dres + (long)row * D, o);
 #pragma unroll
     for (int i = 0; i < NV; ++i)
 #pragma unroll

@@ -70,14 +70,20 @@ class DataParallelStep:
         self.buckets = plan_buckets(e.ready_marks, emb.offset, bucket_mb << 20)
         calls = e.bwd_calls[:-1]                            # all but the local embedding scatter
         assert e.bwd_calls[-1] is e.emb_call
+        T, D = e.T, S.D_MODEL
+        dev = e.dev
+        self.GIDS = torch.zeros(self.world * T, dtype=torch.int64, device=dev)
+        # the rows to re-zero are the previous step's GATHERED ids (every rank's rows were written);
+        # GIDS still holds them when the backward starts (the gather runs after the first segment)
+        assert calls[0] is e.zero_calls[0]
+        g = e.g32["t5.embed"]
+        calls = [ops.Call("vqa_embedding_zero_rows", self.GIDS.data_ptr(), None, self.world * T, g.data_ptr(), D,
+                          S.T5_VOCAB, keep=(self.GIDS, g))] + calls[1:]
         self.segments, prev = [], 0
         for ci, _, _ in self.buckets:
             self.segments.append(calls[prev:ci])
             prev = ci
         self.tail = calls[prev:]                            # nothing should remain after the last mark
-        T, D = e.T, S.D_MODEL
-        dev = e.dev
-        self.GIDS = torch.zeros(self.world * T, dtype=torch.int64, device=dev)
         self.GDH = torch.zeros(self.world * T, D, dtype=torch.float32, device=dev)
         self.WS = torch.empty(3 * self.world * T, dtype=torch.int32, device=dev)
         self.emb_call = ops.Call("vqa_embedding_bwd", self.GIDS.data_ptr(), self.GDH.data_ptr(),

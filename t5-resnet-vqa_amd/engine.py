@@ -232,6 +232,7 @@ class VQAEngine:
         t = self._t
         # inputs
         self.IDS = t((B, Lq), I64, zero=True)
+        self.IDS_PREV = t((B, Lq), I64, zero=True)     # ids whose embedding-gradient rows are nonzero
         self.MASK = t((B, Lq), I64, zero=True)
         self.TGT = t((B,), I64, zero=True)
         # vision tokens
@@ -457,9 +458,11 @@ class VQAEngine:
     def _plan_backward(self):
         b = self.bwd_calls
         B, Lq, T, NB = self.B, self.L, self.T, self.NB
-        # the dense embedding gradient only gets the touched rows written
+        # the dense embedding gradient only ever gets the touched rows written: re-zero the rows
+        # the previous step wrote (IDS_PREV) instead of all 32128 x 768 floats (DP: dp.py swaps in
+        # the gathered ids of every rank)
         z = self.g32["t5.embed"]
-        self._call(self.zero_calls, "vqa_zero", z, z.numel() * 4)
+        self._call(self.zero_calls, "vqa_embedding_zero_rows", self.IDS_PREV, self.IDS, T, z, D, S.T5_VOCAB)
         b += self.zero_calls
         # head: log_softmax + NLL + classifier + attention pooler
         last = self.sga[-1]["OUT"]

@@ -85,9 +85,9 @@ _lib = None
 
 
 def header_symbols():
-    """Every `int vqa_*(` / `const char* vqa_*(` export declared in include/vqa_hip.h."""
+    """Every `int vqa_*(` / `long long vqa_*(` / `const char* vqa_*(` export declared in include/vqa_hip.h."""
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(vqa_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|long long|const char\*)\s+(vqa_\w+)\s*\(", txt, re.M)))
 
 
 def abi_version():
@@ -147,6 +147,7 @@ register("vqa_maxpool3x3s2_nhwc", P, P, c_int, c_int, c_int, c_int, c_int, c_int
 register("vqa_colsum", P, c_int, c_int, c_int, c_ll, P, c_float, P)
 register("vqa_embedding_fwd", P, P, P, c_int, c_int, c_int, P)
 register("vqa_embedding_bwd", P, P, P, c_int, c_int, c_int, P)
+register("vqa_embedding_zero_rows", P, P, c_int, P, c_int, c_int)
 register("vqa_t5_relbias_fwd", P, P, P, c_int, c_int, c_int)
 register("vqa_t5_relbias_bwd", P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_batch_sum", P, c_int, c_ll, P, c_float)
