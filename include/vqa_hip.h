@@ -101,9 +101,11 @@ typedef struct vqa_gemm_desc {
    * separate workgroups; the last slice of a tile to finish sums all slices' fp32
    * partials in slice order (deterministic: same bits for every tile config at a
    * given splitk, different rounding from splitk = 1) and runs the epilogue.
-   * workspace: >= vqa_gemm_workspace_bytes(d) bytes, zero-filled before its first
-   * use (its counters are left zero after every launch); one in-flight launch per
-   * workspace.  splitk <= 1 ignores it. */
+   * workspace: >= vqa_gemm_workspace_bytes(d) bytes = a 64 KiB block of arrival
+   * counters (<= 16384 tiles x batch) then the fp32 partial slabs; zero-filled
+   * before its first use (the counters are left zero after every launch, so calls
+   * on one stream may share a workspace); one in-flight launch per workspace.
+   * splitk <= 1 ignores it. */
   int splitk;
   void* workspace;
   long long workspace_bytes;

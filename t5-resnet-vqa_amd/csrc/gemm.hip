@@ -623,20 +623,25 @@ __global__ __launch_bounds__(256) void gemm_pair_kernel(GemmParams P1, GemmParam
   }
 }
 
-// split-K workspace: slabs then counters (16-B aligned)
+// split-K workspace: a fixed 64 KiB counter block first (so any sequence of calls
+// sharing a workspace only ever finds zeros there), then the slabs
+constexpr long long SPLITK_CNT_BYTES = 65536;
+constexpr long long SPLITK_MAX_TILES = SPLITK_CNT_BYTES / 4;
 long long splitk_bytes(int bm, int bn, int m, int n, int batch, int S) {
   if (S <= 1) return 0;
   const long long tiles = (long long)vqa::cdiv(m, bm) * vqa::cdiv(n, bn) * batch;
-  return tiles * S * bm * bn * 4 + (tiles * 4 + 15) / 16 * 16;
+  return SPLITK_CNT_BYTES + tiles * S * bm * bn * 4;
 }
 
 template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB>
 int launch(GemmParams& P, int batch, hipStream_t s) {
   P.tiles_m = vqa::cdiv(P.m, BM);
   P.tiles_n = vqa::cdiv(P.n, BN);
-  if (P.splitk > 1) {
+  if (P.splitk > 1) {                                   // workspace = [counters | slabs]
     const long long tiles = (long long)P.tiles_m * P.tiles_n * batch;
-    P.cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(P.slab) + tiles * P.splitk * BM * BN * 4);
+    if (tiles > SPLITK_MAX_TILES) return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: split-K needs <= %lld tiles", SPLITK_MAX_TILES);
+    P.cnt = reinterpret_cast<unsigned*>(P.slab);
+    P.slab = reinterpret_cast<float*>(reinterpret_cast<char*>(P.slab) + SPLITK_CNT_BYTES);
   }
   dim3 grid(P.tiles_m * P.tiles_n * (P.splitk > 1 ? P.splitk : 1), 1, batch);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB>), grid, dim3(64 * NWM * NWN), 0, s, P);

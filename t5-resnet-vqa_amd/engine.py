@@ -57,6 +57,7 @@ def sga_site(block, kind):
 
 
 _TUNE_CACHE = {}
+SPLITS = (1, 2, 3, 4, 6, 8)        # split-K counts the tuner tries for small grids
 
 
 def lib_gemm_configs():
@@ -103,6 +104,7 @@ class VQAEngine:
         self._side = torch.cuda.Stream(self.dev)
         self._wside = torch.cuda.Stream(self.dev)
         self.dw_stream = False
+        self._scratch = None             # split-K workspace used while autotuning
 
     @classmethod
     def from_state_dict(cls, sd, **kw):
@@ -799,13 +801,37 @@ class VQAEngine:
         self.graph = parts
 
     # ------------------------------------------------------------------ GEMM autotuning
+    def _tune_scratch(self, d):
+        """Zero-filled split-K workspace shared by every candidate timed during tuning
+        (one stream, one launch at a time; each launch leaves its counters zero)."""
+        need = int(L.load().vqa_gemm_workspace_bytes(ctypes.byref(d)))
+        if self._scratch is None or self._scratch.numel() * 4 < need:
+            self._scratch = torch.zeros(need // 4 + 4, dtype=torch.int32, device=self.dev)
+        return self._scratch
+
+    def _apply_choice(self, c, choice):
+        """Tuning-table value = tile config + 100 * splitk (splitk 0/1 = no split).  A split
+        call gets its own zero-filled workspace, kept alive by the call."""
+        d = c.desc
+        d.config, sk = choice % 100, choice // 100
+        if sk > 1:
+            ops.set_splitk(d, sk)
+            ws = ops.splitk_workspace(d, self.dev)
+            ops.set_splitk(d, sk, ws)
+            c.keep = tuple(c.keep or ()) + (ws,)
+        else:
+            ops.set_splitk(d, 0)
+
     def autotune(self, reps=5, table=None, save=None):
-        """Pick the fastest tile config for every prepared GEMM by timing them in
-        place (HIP events).  Configs differ only in speed: each output element is
-        accumulated in the same K order whatever the tile, so results (and DP
-        rank agreement) do not depend on the choice.  Run after a batch is
-        loaded and one forward/backward has filled the activations; it
-        scribbles only on buffers the next step recomputes."""
+        """Pick the fastest (tile config, split-K) for every prepared GEMM by timing
+        them in place (HIP events).  Tile configs differ only in speed: each output
+        element is accumulated in the same K order whatever the tile.  Split-K
+        (tried only for grids < 512 tiles) re-associates the K sum in a fixed slice
+        order, so a given choice is deterministic; DP ranks stay in lockstep either
+        way because they apply the same all-reduced gradient.  The committed table
+        (`table`) pins the choices of known shapes.  Run after a batch is loaded and
+        one forward/backward has filled the activations; it scribbles only on
+        buffers the next step recomputes."""
         import json
         import os
         if table and os.path.exists(table):                # measured table (tools: bench --tune-save)
@@ -843,21 +869,32 @@ class VQAEngine:
             key = repr(_gemm_key(d))
             if key not in _TUNE_CACHE:
                 best = None
+                nk = -(-d.k // 64)
                 for cfg in range(1, lib_gemm_configs() + 1):
-                    d.config = cfg
-                    c(s)
-                    st.record()
-                    for _ in range(reps):
+                    bm, bn, _ = L.GEMM_TILES[cfg]
+                    tiles = -(-d.m // bm) * -(-d.n // bn) * max(1, d.batch)
+                    for sk in SPLITS:
+                        # split only grids that leave CUs idle, with >= 2 k-tiles per slice
+                        if sk > 1 and (tiles >= 512 or nk < 2 * sk or tiles > 16384):
+                            continue
+                        d.config = cfg
+                        ops.set_splitk(d, sk)
+                        ops.set_splitk(d, sk, self._tune_scratch(d) if sk > 1 else None)
                         c(s)
-                    en.record()
-                    en.synchronize()
-                    t = st.elapsed_time(en)
-                    if best is None or t < best[0]:
-                        best = (t, cfg)
+                        st.record()
+                        for _ in range(reps):
+                            c(s)
+                        en.record()
+                        en.synchronize()
+                        t = st.elapsed_time(en)
+                        if best is None or t < best[0]:
+                            best = (t, cfg + 100 * sk)
+                ops.set_splitk(d, 0)
                 _TUNE_CACHE[key] = best[1]
-            d.config = _TUNE_CACHE[key]
-            chosen[key] = d.config
+            self._apply_choice(c, _TUNE_CACHE[key])
+            chosen[key] = _TUNE_CACHE[key]
         torch.cuda.synchronize(self.dev)
+        self._scratch = None
         self.graph = None
         if save:
             json.dump(dict(sorted(chosen.items())), open(save, "w"), indent=0)

@@ -280,9 +280,6 @@ def test_splitk_matches_reference_and_is_config_invariant(ops, pkg, layout, spli
         scale = 0.5 * (A.abs() @ Bm.abs()).max().item()
     outs = []
     cfgs = sorted(pkg.lib.GEMM_TILES)
-    nk = -(-K // 64)
-    per = -(-nk // min(splitk, nk))
-    s_eff = -(-nk // per)
     for cfg in cfgs:
         out = torch.full((M, N), float("nan"), device="cuda")
         d = mk(out)
@@ -293,11 +290,8 @@ def test_splitk_matches_reference_and_is_config_invariant(ops, pkg, layout, spli
         ops.run(d)
         ops.run(d)                                       # second launch reuses the counters
         outs.append(out)
-        bm, bn, _ = pkg.lib.GEMM_TILES[cfg]
-        tiles = -(-M // bm) * -(-N // bn)
-        off = tiles * s_eff * bm * bn
         torch.cuda.synchronize()
-        assert int(ws[off:off + tiles].abs().sum()) == 0, "arrival counters must be left zero"
+        assert int(ws[:16384].abs().sum()) == 0, "arrival counters (first 64 KiB) must be left zero"
     torch.cuda.synchronize()
     close(outs[0], ref, scale)
     for cfg, o in zip(cfgs[1:], outs[1:]):
