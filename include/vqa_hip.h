@@ -190,6 +190,20 @@ int vqa_norm_bwd_workspace_floats(int rows, int d);
 /* out[c] = beta*out[c] + sum_p ws[p*stride + c] (fixed order) */
 int vqa_colsum_partials(const float* ws, int parts, long long stride, int cols, float* out, float beta,
                         hipStream_t stream);
+/* Deferred reductions: vqa_rmsnorm_bwd with dw == NULL, vqa_layernorm_bwd with
+ * dgamma == dbeta == NULL and vqa_colsum with out == NULL only write their per-block
+ * partial rows into ws (rmsnorm: [vqa_norm_bwd_parts(rows)][d]; layernorm:
+ * [parts][3][d] = dgamma, dbeta, dsum; colsum: [vqa_colsum_parts(rows)][cols]);
+ * vqa_colsum_batched then finishes any number of such reductions in ONE launch.
+ * jobs: DEVICE array; job j covers blocks [first_block, first_block + ceil(cols/64))
+ * (first_block cumulative, nblocks = total), each computing
+ * out[c] = beta*out[c] + sum_{p < parts} ws[p*stride + c] in fixed order. */
+typedef struct vqa_colsum_job {
+  const float* ws; float* out; long long stride; int parts; int cols; float beta; int first_block;
+} vqa_colsum_job;
+int vqa_norm_bwd_parts(int rows);
+int vqa_colsum_parts(int rows);
+int vqa_colsum_batched(const vqa_colsum_job* jobs, int njobs, int nblocks, hipStream_t stream);
 
 /* ---------------------------------------------------------- elementwise ---
  * vqa_image_to_nhwc8: NCHW fp32 [N,3,H,W] (collate ToTensor,

@@ -317,10 +317,11 @@ extern "C" int vqa_maxpool3x3s2_nhwc(const void* x, void* y, int n, int h, int w
 }
 
 extern "C" int vqa_colsum_workspace_floats(int rows, int cols) { return vqa::cdiv(rows, COLSUM_ROWS) * cols; }
+extern "C" int vqa_colsum_parts(int rows) { return vqa::cdiv(rows, COLSUM_ROWS); }
 
 extern "C" int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long long ld, float* out, float beta,
                           float* ws, hipStream_t s) {
-  VQA_REQUIRE(x && out && ws && cols % 4 == 0 && ld % 4 == 0, "vqa_colsum: bad arguments");
+  VQA_REQUIRE(x && ws && cols % 4 == 0 && ld % 4 == 0, "vqa_colsum: bad arguments");
   const int parts = vqa::cdiv(rows, COLSUM_ROWS);
   dim3 grid(vqa::cdiv(cols, 256), parts);
   if (x_bf16)
@@ -328,6 +329,7 @@ extern "C" int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long lo
   else
     hipLaunchKernelGGL(colsum_part_kernel<false>, grid, dim3(256), 0, s, x, rows, cols, (long)ld, ws);
   if (int rc = vqa::check_launch("vqa_colsum")) return rc;
+  if (!out) return VQA_OK;                                   // deferred: vqa_colsum_batched reduces ws
   return vqa_colsum_partials(ws, parts, cols, cols, out, beta, s);
 }
 

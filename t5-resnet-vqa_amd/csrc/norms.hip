@@ -314,6 +314,30 @@ __global__ __launch_bounds__(1024) void colsum3_partials_kernel(const float* __r
   }
 }
 
+// Any number of deferred partial-row reductions in one launch: block b serves job
+// j (scalar scan, first_block ascending), 64 columns x 16 part-groups as above.
+__global__ __launch_bounds__(1024) void colsum_batched_kernel(const vqa_colsum_job* __restrict__ jobs, int njobs) {
+  int j = 0;
+  while (j + 1 < njobs && jobs[j + 1].first_block <= (int)blockIdx.x) ++j;
+  const vqa_colsum_job J = jobs[j];
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = ((int)blockIdx.x - J.first_block) * 64 + tx;
+  float s = 0.f;
+  if (c < J.cols) {
+#pragma unroll 4
+    for (int p = ty; p < J.parts; p += 16) s += J.ws[(long)p * J.stride + c];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < J.cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][tx];
+    J.out[c] = J.beta != 0.f ? J.beta * J.out[c] + t : t;
+  }
+}
+
 constexpr int NORM_BWD_ROWS = 8;       // rows per block in the backward kernels (256 blocks at 2048 rows)
 
 vqa_dropout dr(const vqa_dropout* d) {
@@ -343,20 +367,21 @@ extern "C" int vqa_rmsnorm_fwd(const float* x, const float* w, float* y32, void*
   return vqa::check_launch("vqa_rmsnorm_fwd");
 }
 
-int vqa_norm_bwd_parts(int rows) { return vqa::cdiv(rows, NORM_BWD_ROWS); }
+extern "C" int vqa_norm_bwd_parts(int rows) { return vqa::cdiv(rows, NORM_BWD_ROWS); }
 extern "C" int vqa_norm_bwd_workspace_floats(int rows, int d) { return 3 * vqa_norm_bwd_parts(rows) * d; }
 
 extern "C" int vqa_rmsnorm_bwd(const float* dy, const float* x, const float* rstd, const float* w, const float* dres,
                                float* dx32, void* dx16, float* dw, float dw_beta, float* ws, int rows, int d,
                                const vqa_dropout* drop_dy, const vqa_dropout* drop_dx32, const vqa_dropout* drop_dx16,
                                hipStream_t s) {
-  VQA_REQUIRE(dy && x && rstd && w && dw && ws && (dx32 || dx16) && d % 256 == 0, "vqa_rmsnorm_bwd: bad arguments");
+  VQA_REQUIRE(dy && x && rstd && w && ws && (dx32 || dx16) && d % 256 == 0, "vqa_rmsnorm_bwd: bad arguments");
   VQA_REQUIRE(dr_ok(drop_dy) && dr_ok(drop_dx32) && dr_ok(drop_dx16), "vqa_rmsnorm_bwd: dropout p must be in [0, 1)");
   const int parts = vqa_norm_bwd_parts(rows);
   DISPATCH_NV(d, hipLaunchKernelGGL(rmsnorm_bwd_kernel<NV>, dim3(parts), dim3(256), 0, s, dy, x, rstd, w, dres, dx32,
                                     (bf16_t*)dx16, ws, rows, NORM_BWD_ROWS, dr(drop_dy), dr(drop_dx32),
                                     dr(drop_dx16)));
   if (int rc = vqa::check_launch("vqa_rmsnorm_bwd")) return rc;
+  if (!dw) return VQA_OK;                                    // deferred: vqa_colsum_batched reduces ws
   hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(d, 64)), dim3(1024), 0, s, ws, parts, (long)d, d, dw,
                      dw_beta);
   return vqa::check_launch("vqa_rmsnorm_bwd/colsum");
@@ -375,7 +400,7 @@ extern "C" int vqa_layernorm_bwd(const float* dy, const float* x, const float* m
                                  const float* gamma, const float* dres, float* dx32, void* dx16, float* dgamma,
                                  float* dbeta, float* ws, int rows, int d, const vqa_dropout* drop_dx16,
                                  float* dsum, hipStream_t s) {
-  VQA_REQUIRE(dy && x && mean && rstd && gamma && dgamma && dbeta && ws && (dx32 || dx16) && d % 256 == 0,
+  VQA_REQUIRE(dy && x && mean && rstd && gamma && ws && (dx32 || dx16) && d % 256 == 0 && !dgamma == !dbeta,
               "vqa_layernorm_bwd: bad arguments");
   VQA_REQUIRE(dr_ok(drop_dx16), "vqa_layernorm_bwd: dropout p must be in [0, 1)");
   const int parts = vqa_norm_bwd_parts(rows);
@@ -383,6 +408,7 @@ extern "C" int vqa_layernorm_bwd(const float* dy, const float* x, const float* m
                                     dres, dx32, (bf16_t*)dx16, ws, rows, NORM_BWD_ROWS, dr(drop_dx16),
                                     dsum != nullptr ? 1 : 0));
   if (int rc = vqa::check_launch("vqa_layernorm_bwd")) return rc;
+  if (!dgamma) return VQA_OK;                                // deferred: vqa_colsum_batched reduces ws
   hipLaunchKernelGGL(colsum3_partials_kernel, dim3(vqa::cdiv(d, 64), dsum ? 3 : 2), dim3(1024), 0, s, ws, parts,
                      (long)3 * d, d, dgamma, dbeta, dsum);
   return vqa::check_launch("vqa_layernorm_bwd/colsum");
@@ -394,4 +420,10 @@ extern "C" int vqa_colsum_partials(const float* ws, int parts, long long stride,
   hipLaunchKernelGGL(colsum_partials_kernel, dim3(vqa::cdiv(cols, 64)), dim3(1024), 0, s, ws, parts, (long)stride, cols,
                      out, beta);
   return vqa::check_launch("vqa_colsum_partials");
+}
+
+extern "C" int vqa_colsum_batched(const vqa_colsum_job* jobs, int njobs, int nblocks, hipStream_t s) {
+  VQA_REQUIRE(jobs && njobs > 0 && nblocks > 0, "vqa_colsum_batched: bad arguments");
+  hipLaunchKernelGGL(colsum_batched_kernel, dim3(nblocks), dim3(1024), 0, s, jobs, njobs);
+  return vqa::check_launch("vqa_colsum_batched");
 }

@@ -284,8 +284,6 @@ class VQAEngine:
         self.dSB = t((S.T5_LAYERS, B, S.T5_HEADS, Lq, Lq))   # per-layer, per-sample attention dS (rel-bias grad)
         self.WS_EMB = t(3 * T, torch.int32)
         lib = L.load()
-        self.WS_NORM = t(lib.vqa_norm_bwd_workspace_floats(T, D))
-        self.WS_COL = t(lib.vqa_colsum_workspace_floats(mx, 3 * D))
         self.WS_COL2 = t(lib.vqa_colsum_workspace_floats(V, D))
         self.WS_HEAD = t(lib.vqa_head_workspace_floats(B, Lq, D, self.A))
         self.SQ_PARTS = 1024
@@ -366,6 +364,30 @@ class VQAEngine:
                             desc=(gx.desc, gw.desc)))
         lst.extend(tmp[2:])
 
+    def _defer(self, ws, parts, stride, cols, out, beta=0.0, offset=0):
+        """Queue the final reduction out = beta*out + sum_p ws[offset + p*stride + c] (a norm
+        weight/bias or Linear bias gradient whose per-block partial rows a backward kernel
+        wrote); _flush() finishes every queued one in a single vqa_colsum_batched launch."""
+        self._jobs.append((ops.addr(ws) + 4 * offset, ops.addr(out), stride, parts, cols, beta, (ws, out)))
+
+    def _flush(self, lst):
+        if not self._jobs:
+            return
+        arr = (L.ColsumJob * len(self._jobs))()
+        blk = 0
+        keep = []
+        for j, (ws, out, stride, parts, cols, beta, k) in enumerate(self._jobs):
+            arr[j] = L.ColsumJob(ws, out, stride, parts, cols, beta, blk)
+            blk += -(-cols // 64)
+            keep += list(k)
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.dev)
+        lst.append(ops.Call("vqa_colsum_batched", raw.data_ptr(), len(self._jobs), blk, keep=tuple(keep) + (raw,)))
+        self._jobs = []
+
+    def _norm_ws(self):
+        """A private partial-row workspace for one deferred norm backward."""
+        return self._t(L.load().vqa_norm_bwd_workspace_floats(self.T, D))
+
     def _gbuf(self, name, shape):
         """A bf16 backward buffer private to one use (see _plan_backward)."""
         if name not in self._gbufs:
@@ -380,10 +402,11 @@ class VQAEngine:
         n, k = g.shape
         self._gemm(lst, dy16, x16, n, k, rows, lda=n, ldb=k, a_trans=True, b_trans=True, c32=g, ldc32=k)
         lst[-1].side = True
-        if bias_from is not None:
-            self._call(lst, "vqa_colsum", bias_from, int(bias_bf16), rows, n, n, self.g32[wname[:-1] + "b"], 0.0,
-                       self.WS_COL)
-            lst[-1].side = True
+        if bias_from is not None:                   # partial column sums now, final sum deferred (_flush)
+            lib = L.load()
+            ws = self._t(lib.vqa_colsum_workspace_floats(rows, n))
+            self._call(lst, "vqa_colsum", bias_from, int(bias_bf16), rows, n, n, None, 0.0, ws)
+            self._defer(ws, lib.vqa_colsum_parts(rows), n, n, self.g32[wname[:-1] + "b"])
 
     # ------------------------------------------------------------------ forward plan
     def _plan_forward(self):
@@ -460,6 +483,7 @@ class VQAEngine:
     def _plan_backward(self):
         b = self.bwd_calls
         B, Lq, T, NB = self.B, self.L, self.T, self.NB
+        nparts = L.load().vqa_norm_bwd_parts(T)
         # the dense embedding gradient only ever gets the touched rows written: re-zero the rows
         # the previous step wrote (IDS_PREV) instead of all 32128 x 768 floats (DP: dp.py swaps in
         # the gathered ids of every rank)
@@ -476,7 +500,10 @@ class VQAEngine:
         # a prefix of G32: DP all-reduces bucket [prev_end, end) as soon as it is final.
         self.ready_marks = []
 
+        self._jobs = []
+
         def mark(seg):
+            self._flush(b)                          # finish this segment's deferred reductions first
             sg = self.lay[seg]
             self.ready_marks.append((len(b), sg.offset + (sg.numel + 63) // 64 * 64))
         mark("pool_b")
@@ -495,16 +522,22 @@ class VQAEngine:
             # norm3 + FFN: dA32 = grad of x + dropout3(ffn(x)) (the residual), dA16 = its dropout3 branch;
             # the fc2 bias gradient (column sums of the branch) is fused into the LayerNorm backward
             kp = []
+            ws = self._norm_ws()
             self._call(b, "vqa_layernorm_bwd", dy, s["S3"], s["MU3"], s["RS3"], self.p32[p + "ln3_g"], None,
-                       self.dA32, dA3, self.g32[p + "ln3_g"], self.g32[p + "ln3_b"], self.WS_NORM, T, D,
+                       self.dA32, dA3, None, None, ws, T, D,
                        self._dptr(sga_site(n, 5), kp), self.g32[p + "fc2_b"], extra=kp + [self.RNG])
+            for j, nm in enumerate(("ln3_g", "ln3_b", "fc2_b")):      # ws = [parts][dgamma | dbeta | dsum]
+                self._defer(ws, nparts, 3 * D, D, self.g32[p + nm], offset=j * D)
             self._dxdw(b, dA3, s["FFh"], p + "fc2_w", T, out16=dB, mask16=s["FFh"], alpha=ks)
             self._dxdw(b, dB, s["X2h"], p + "fc1_w", T, bias_from=dB, out32=self.dC32, res32=self.dA32)
             # norm2 + cross attention (q from x, k/v from y)
             kp = []
+            ws = self._norm_ws()
             self._call(b, "vqa_layernorm_bwd", self.dC32, s["S2"], s["MU2"], s["RS2"], self.p32[p + "ln2_g"], None,
-                       self.dA32, dA2, self.g32[p + "ln2_g"], self.g32[p + "ln2_b"], self.WS_NORM, T, D,
+                       self.dA32, dA2, None, None, ws, T, D,
                        self._dptr(sga_site(n, 3), kp), self.g32[p + "m2_b"], extra=kp + [self.RNG])
+            for j, nm in enumerate(("ln2_g", "ln2_b", "m2_b")):      # ws = [parts][dgamma | dbeta | dsum]
+                self._defer(ws, nparts, 3 * D, D, self.g32[p + nm], offset=j * D)
             self._dxdw(b, dA2, s["O2"], p + "m2_w", T, out16=self.dO16)
             kv = s["KV2"]
             self._attn(b, "vqa_attn_bwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
@@ -518,9 +551,12 @@ class VQAEngine:
                 self._dxdw(b, dKV, y16, p + "kv2_w", s["ly"], bias_from=dKV, out32=self.dY[(n - 1) & 1])
             # norm1 + self attention
             kp = []
+            ws = self._norm_ws()
             self._call(b, "vqa_layernorm_bwd", self.dC32, s["S1"], s["MU1"], s["RS1"], self.p32[p + "ln1_g"], None,
-                       self.dA32, dA1, self.g32[p + "ln1_g"], self.g32[p + "ln1_b"], self.WS_NORM, T, D,
+                       self.dA32, dA1, None, None, ws, T, D,
                        self._dptr(sga_site(n, 1), kp), self.g32[p + "m1_b"], extra=kp + [self.RNG])
+            for j, nm in enumerate(("ln1_g", "ln1_b", "m1_b")):      # ws = [parts][dgamma | dbeta | dsum]
+                self._defer(ws, nparts, 3 * D, D, self.g32[p + nm], offset=j * D)
             self._dxdw(b, dA1, s["O1"], p + "m1_w", T, out16=self.dO16)
             q = s["QKV1"]
             dq = dQKV
@@ -547,19 +583,23 @@ class VQAEngine:
         g = lambda nm, shape: self._gbuf(nm, shape)
         dH16 = [g(f"t5.{i}.dH", (T, D)) for i in range(S.T5_LAYERS)]     # FF-branch grad of layer i
         kp = []
+        ws = self._norm_ws()
         self._call(b, "vqa_rmsnorm_bwd", self.dTXT, self.HS[-1], self.RF, self.p32["t5.final_ln"], None, self.dH32,
-                   dH16[-1], self.g32["t5.final_ln"], 0.0, self.WS_NORM, T, D,
+                   dH16[-1], None, 0.0, ws, T, D,
                    self._dptr(SITE_FINAL, kp), None, self._dptr(t5_site(S.T5_LAYERS - 1, 3), kp),
                    extra=kp + [self.RNG])
+        self._defer(ws, nparts, D, D, self.g32["t5.final_ln"])
         mark("t5.final_ln")
         for i in reversed(range(S.T5_LAYERS)):
             dF, dHM, dQKV = g(f"t5.{i}.dF", (T, S.T5_DFF)), g(f"t5.{i}.dHM", (T, D)), g(f"t5.{i}.dQKV", (T, 3 * D))
             self._dxdw(b, dH16[i], self.FF[i], f"t5.{i}.wo", T, out16=dF, mask16=self.FF[i], alpha=ks)
             self._dxdw(b, dF, self.N1[i], f"t5.{i}.wi", T, out32=self.dC32)
             kp = []
+            ws = self._norm_ws()
             self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HM[i], self.R1[i], self.p32[f"t5.{i}.ln1"], self.dH32,
-                       self.dHM32, dHM, self.g32[f"t5.{i}.ln1"], 0.0, self.WS_NORM, T, D,
+                       self.dHM32, dHM, None, 0.0, ws, T, D,
                        None, None, self._dptr(t5_site(i, 1), kp), extra=kp + [self.RNG])
+            self._defer(ws, nparts, D, D, self.g32[f"t5.{i}.ln1"])
             self._dxdw(b, dHM, self.O[i], f"t5.{i}.o_w", T, out16=self.dO16)
             q = self.QKV[i]
             dq = dQKV
@@ -574,9 +614,11 @@ class VQAEngine:
             kp = []
             d32 = self._dptr(SITE_EMBED, kp) if i == 0 else None
             d16 = self._dptr(t5_site(i - 1, 3), kp) if i > 0 else None
+            ws = self._norm_ws()
             self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HS[i], self.R0[i], self.p32[f"t5.{i}.ln0"], self.dHM32,
-                       self.dH32, dH16[i - 1] if i > 0 else None, self.g32[f"t5.{i}.ln0"], 0.0, self.WS_NORM, T, D,
+                       self.dH32, dH16[i - 1] if i > 0 else None, None, 0.0, ws, T, D,
                        None, d32, d16, extra=kp + [self.RNG])
+            self._defer(ws, nparts, D, D, self.g32[f"t5.{i}.ln0"])
             mark(f"t5.{i}.ln1")
         # the relative-position bias is shared by all 12 layers: dPB = sum over (layer, sample) of dS,
         # one fixed-order reduction after the last layer instead of one per layer
@@ -584,6 +626,7 @@ class VQAEngine:
         self._call(b, "vqa_t5_relbias_bwd", self.dPB, self.bucket, self.g32["t5.relbias"], S.T5_HEADS, Lq, Lq,
                    S.T5_BUCKETS)
         mark("t5.relbias")
+        self._flush(b)
         # embedding rows last (DP replaces this call by an all-gather of (id, dH row) pairs)
         self._call(b, "vqa_embedding_bwd", self.IDS, self.dH32, self.g32["t5.embed"], T, D, S.T5_VOCAB, self.WS_EMB)
         self.emb_call = b[-1]

@@ -50,6 +50,11 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class ColsumJob(ctypes.Structure):
+    _fields_ = [("ws", c_void_p), ("out", c_void_p), ("stride", c_ll), ("parts", c_int), ("cols", c_int),
+                ("beta", c_float), ("first_block", c_int)]
+
+
 class AttnDesc(ctypes.Structure):
     _fields_ = [
         ("q", c_void_p), ("ldq", c_ll), ("k", c_void_p), ("ldk", c_ll), ("v", c_void_p), ("ldv", c_ll),
@@ -119,6 +124,8 @@ def load():
     for name in ("vqa_norm_bwd_workspace_floats", "vqa_colsum_workspace_floats"):
         getattr(lib, name).argtypes = [c_int, c_int]
     lib.vqa_head_workspace_floats.argtypes = [c_int] * 4
+    lib.vqa_norm_bwd_parts.argtypes = [c_int]
+    lib.vqa_colsum_parts.argtypes = [c_int]
     for name, argtypes in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
@@ -148,6 +155,7 @@ register("vqa_colsum", P, c_int, c_int, c_int, c_ll, P, c_float, P)
 register("vqa_embedding_fwd", P, P, P, c_int, c_int, c_int, P)
 register("vqa_embedding_bwd", P, P, P, c_int, c_int, c_int, P)
 register("vqa_embedding_zero_rows", P, P, c_int, P, c_int, c_int)
+register("vqa_colsum_batched", P, c_int, c_int)
 register("vqa_t5_relbias_fwd", P, P, P, c_int, c_int, c_int)
 register("vqa_t5_relbias_bwd", P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_batch_sum", P, c_int, c_ll, P, c_float)
