@@ -66,17 +66,26 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const void* __restrict
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 256 + tx * 4;
   const int r0 = blockIdx.y * COLSUM_ROWS;
+  // the thread's 16 rows are loaded unconditionally (clamped row / column, masked
+  // by a multiply) before the first add: one round trip instead of 16
   float s[4] = {0.f, 0.f, 0.f, 0.f};
-  if (c < cols) {
-    for (int r = r0 + ty; r < min(rows, r0 + COLSUM_ROWS); r += 4) {
-      if constexpr (BF16) {
-        uint2 u = *reinterpret_cast<const uint2*>((const bf16_t*)xv + (long)r * ld + c);
-        s[0] += bf2f(u.x & 0xffff); s[1] += bf2f(u.x >> 16); s[2] += bf2f(u.y & 0xffff); s[3] += bf2f(u.y >> 16);
-      } else {
-        float4 v = *reinterpret_cast<const float4*>((const float*)xv + (long)r * ld + c);
-        s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
-      }
+  constexpr int RPT = COLSUM_ROWS / 4;
+  const int cl = min(c, cols - 4);
+  float4 v[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int r = min(r0 + ty + 4 * q, rows - 1);
+    if constexpr (BF16) {
+      const uint2 u = *reinterpret_cast<const uint2*>((const bf16_t*)xv + (long)r * ld + cl);
+      v[q] = make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
+    } else {
+      v[q] = *reinterpret_cast<const float4*>((const float*)xv + (long)r * ld + cl);
     }
+  }
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const float m = (c < cols && r0 + ty + 4 * q < rows) ? 1.f : 0.f;
+    s[0] += v[q].x * m; s[1] += v[q].y * m; s[2] += v[q].z * m; s[3] += v[q].w * m;
   }
   __shared__ float red[4][256];
 #pragma unroll

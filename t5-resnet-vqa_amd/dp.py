@@ -120,14 +120,41 @@ class DataParallelStep:
         with torch.cuda.graph(g, stream=s):
             e.run_forward_streams()
         gs["fwd"] = [g]
+        if e.pipeline:                                      # the next batch's ResNet, replayed beside the step
+            cap("res", e.res_calls)
         for seg in self.segments:
             cap("seg", seg)
         cap("tail", self.tail + [self.emb_call])
         cap("opt", e.opt_calls)
         self.graphs = gs
 
+    def _res_begin(self):
+        """Pipelined engines: F4 <- F4N, then the next batch's frozen ResNet on its own
+        stream (graph or eager), overlapping this whole step; _res_end joins it."""
+        e = self.eng
+        if not e.pipeline:
+            return
+        main = torch.cuda.current_stream(e.dev)
+        e.F4.copy_(e.F4N)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        e._rstream.wait_event(ev)
+        with torch.cuda.stream(e._rstream):
+            if self.graphs is not None:
+                self.graphs["res"][0].replay()
+            else:
+                self._run(e.res_calls)
+
+    def _res_end(self):
+        e = self.eng
+        if e.pipeline:
+            ev = torch.cuda.Event()
+            ev.record(e._rstream)
+            torch.cuda.current_stream(e.dev).wait_event(ev)
+
     def step(self):
         e = self.eng
+        self._res_begin()
         if self.graphs is None:
             e.forward()
             works = []
@@ -141,6 +168,7 @@ class DataParallelStep:
             for w in works[:-2]:
                 w.wait()
             self._run(e.opt_calls)
+            self._res_end()
             return
         g = self.graphs
         g["fwd"][0].replay()
@@ -155,3 +183,4 @@ class DataParallelStep:
         for w in works[:-2]:
             w.wait()
         g["opt"][0].replay()
+        self._res_end()

@@ -76,8 +76,11 @@ def _gemm_key(d):
 class VQAEngine:
     def __init__(self, state_dict, vision="resnet50", batch=64, seq_len=32, image_size=224, device="cuda:0",
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
-                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0):
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0, pipeline=False):
         L.load()
+        # pipeline: the frozen ResNet (no trainable input) of the NEXT batch runs on its own
+        # stream beside this step's T5 / SGA / backward / optimizer (see train_step)
+        self.pipeline = bool(pipeline)
         self.p_drop, self.seed = float(dropout), int(seed)
         self.dev = torch.device(device)
         self.vision, self.B, self.L, self.H = vision, batch, seq_len, image_size
@@ -103,6 +106,7 @@ class VQAEngine:
         self.allreduce = None            # set by the DP trainer: fn(G32 tensor) on the current stream
         self._side = torch.cuda.Stream(self.dev)
         self._wside = torch.cuda.Stream(self.dev)
+        self._rstream = torch.cuda.Stream(self.dev)
         self.dw_stream = False
         self._scratch = None             # split-K workspace used while autotuning
 
@@ -178,6 +182,9 @@ class VQAEngine:
         bufs = [self._t(maxel, BF16) for _ in range(5)]
         self.res_bufs = bufs
         self.F4 = self._t((B, hh, hh, cin), BF16)
+        # pipelined: the ResNet writes the next batch's layer4 map here; each step first
+        # moves it into F4 (read by the ConvTranspose2d forward and weight gradient)
+        self.F4N = self._t((B, hh, hh, cin), BF16) if self.pipeline else self.F4
 
         # stem: conv7x7/2 + BN + ReLU, then maxpool 3x3/2
         w16, b32 = conv_w("conv1", "bn1", cin_pad=8)
@@ -194,7 +201,7 @@ class VQAEngine:
             p = f"layer{li + 1}.{bi}."
             t1, t2, ds, y = free[0], free[1], free[2], free[3]
             if idx == nblocks_total - 1:
-                y = self.F4
+                y = self.F4N
             if bottleneck:
                 w, b = conv_w(p + "conv1", p + "bn1")
                 self._conv(x, (B, hi, hi, ci), w, b, 1, 0, t1, relu=True)
@@ -215,7 +222,7 @@ class VQAEngine:
             k3 = 1 if bottleneck else 3
             self._conv(last_in, (B, last_h, last_h, last_c), w3, b3, 1, 1 if k3 == 3 else 0, y, relu=True,
                        res16=res)
-            if y is not self.F4:
+            if y is not self.F4N:
                 free = [x, t1, t2, ds]
                 x = y
 
@@ -415,7 +422,8 @@ class VQAEngine:
         if self.p_drop > 0.0:                                # fresh dropout masks every step
             self._call(f, "vqa_rng_advance", self.RNG)
         self._fsplit = [len(f)]                              # [pre | vision | text | fusion]
-        f += self.res_calls
+        if not self.pipeline:                                # pipelined: res_calls run beside the step
+            f += self.res_calls
         # ConvTranspose2d scaler as implicit GEMM over the layer4 map (+bias) -> vision tokens
         cin, fh = self.fc, self.fh
         g = ops.conv_geom(B, fh, fh, cin, fh, fh, 3, 3, 1, 1)
@@ -694,17 +702,27 @@ class VQAEngine:
         for c in calls:
             c(s)
 
-    def load_batch(self, batch):
-        """Copy a batch dict (numpy or torch, host or device) into the static input buffers."""
+    def load_batch(self, batch, next_images=None):
+        """Copy a batch dict (numpy or torch, host or device) into the static input buffers.
+        Pipelined engines take the batch's text and targets, and `next_images` = the image
+        tensors of the batch that the FOLLOWING step trains on (this batch's images went
+        in one step earlier, or through prime())."""
         def cp(dst, src):
             if src is None:
                 return
             src = torch.as_tensor(src)
             dst.copy_(src.to(dst.dtype).reshape(dst.shape), non_blocking=True)
-        cp(self.IMG, batch["image_tensors"])
+        cp(self.IMG, next_images if self.pipeline else batch["image_tensors"])
         cp(self.IDS, batch["question_input_ids"])
         cp(self.MASK, batch["question_attention_masks"])
         cp(self.TGT, batch.get("annotation_ids"))
+
+    def prime(self, images):
+        """Pipelined engines: compute the layer4 features of the first batch's images, so
+        that the first train_step has them (later steps produce their successor's)."""
+        assert self.pipeline, "prime() is for pipelined engines"
+        self.IMG.copy_(torch.as_tensor(images).to(self.IMG.dtype).reshape(self.IMG.shape), non_blocking=True)
+        self._run(self.res_calls)
 
     def forward(self):
         self._run(self.fwd_calls)
@@ -797,6 +815,25 @@ class VQAEngine:
                 self._run(calls[i:j])
             i = j
 
+    def _step_pipelined(self):
+        """One pipelined step: F4 <- F4N (features of this batch, made last step), then the
+        ResNet of the next batch (IMG -> F4N) on its own stream, concurrently with this
+        step's whole chain on the current stream; joined at the end.  The two sides share
+        no buffer, so every result equals the unpipelined step's bit for bit."""
+        main = torch.cuda.current_stream(self.dev)
+        self.F4.copy_(self.F4N)
+        fork = torch.cuda.Event()
+        fork.record(main)
+        self._rstream.wait_event(fork)
+        with torch.cuda.stream(self._rstream):
+            self._run(self.res_calls)
+        self.run_forward_streams()                         # ConvTranspose2d || T5 encoder, then SGA
+        self.run_backward_streams()
+        self._run(self.opt_calls)
+        join = torch.cuda.Event()
+        join.record(self._rstream)
+        main.wait_event(join)
+
     def train_step(self):
         """zero_grad -> forward -> backward -> (all-reduce) -> clip -> AdamW -> sched, all on-device."""
         if self.graph is not None:
@@ -805,6 +842,10 @@ class VQAEngine:
                     g()
                 else:
                     g.replay()
+            return
+        if self.pipeline:
+            assert self.allreduce is None, "pipelined DP steps go through dp.DataParallelStep"
+            self._step_pipelined()
             return
         self.forward()
         self.backward()
@@ -828,7 +869,10 @@ class VQAEngine:
         if self.allreduce is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
-                self._run_step_streams()
+                if self.pipeline:
+                    self._step_pipelined()
+                else:
+                    self._run_step_streams()
             parts = [g]
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -884,7 +928,8 @@ class VQAEngine:
         lib = L.load()
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         chosen = {}
-        for c in self.fwd_calls + self.bwd_calls:
+        extra = self.res_calls if self.pipeline else []
+        for c in extra + self.fwd_calls + self.bwd_calls:
             if c.name == "vqa_gemm_pair":
                 d1, d2 = c.desc
                 key = repr(("pair", _gemm_key(d1), _gemm_key(d2)))

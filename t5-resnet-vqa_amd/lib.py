@@ -71,6 +71,7 @@ class AttnDesc(ctypes.Structure):
 GEMM_TILES = {1: (128, 128, 3), 2: (128, 64, 4), 3: (64, 64, 4), 4: (64, 64, 2), 5: (64, 64, 3), 6: (128, 64, 2),
               7: (64, 128, 2), 8: (128, 128, 2), 9: (256, 128, 2), 10: (128, 256, 2), 11: (256, 256, 2),
               12: (256, 128, 3)}
+GEMM_WAVES = {c: ((4, 2) if c in (9, 12) else (2, 4) if c in (10, 11) else (2, 2)) for c in GEMM_TILES}
 
 MAX_GROUPS = 8
 ST_STEP, ST_GRAD_NORM, ST_CLIP_COEF, ST_LR_SCALE, ST_BC1, ST_BC2_SQRT = range(6)

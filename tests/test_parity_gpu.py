@@ -116,3 +116,35 @@ def test_dropout_changes_step_to_step(cuda, pkg):
     _, a = e0.forward_backward(nb)
     _, b = e0.forward_backward(nb)
     assert a == b
+
+
+def test_pipelined_resnet_step_is_bit_identical(cuda, pkg):
+    """The pipelined engine (next batch's frozen ResNet beside this step) trains on
+    exactly the same (text, image) pairs and produces the same bits as the plain
+    engine, eager and graph-replayed, over a sequence of distinct batches."""
+    import torch
+    B, L, H = 2, 32, 64
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    batches = [pkg.synthetic.make_batch(B, L, H, seed=10 + i) for i in range(4)]
+    ref = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=20)
+    losses = []
+    for nb in batches[:3]:
+        ref.load_batch(nb)
+        ref.train_step()
+        losses.append(float(ref.LOSS.item()))
+    for graph in (False, True):
+        eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=20, pipeline=True)
+        eng.prime(batches[0]["image_tensors"])
+        if graph:
+            eng.F4.copy_(eng.F4N)
+            eng.load_batch(batches[0], next_images=batches[1]["image_tensors"])
+            eng.capture()
+            eng.prime(batches[0]["image_tensors"])
+        got = []
+        for i in range(3):
+            eng.load_batch(batches[i], next_images=batches[i + 1]["image_tensors"])
+            eng.train_step()
+            got.append(float(eng.LOSS.item()))
+        torch.cuda.synchronize()
+        assert got == losses, (graph, got, losses)
+        assert torch.equal(eng.P32, ref.P32), graph
