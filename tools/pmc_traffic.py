@@ -18,7 +18,7 @@ from collections import defaultdict
 
 KERNELS = {
     "adamw_kernel": "adamw_kernel",
-    "convT_dW": "gemm_kernel<128, 64, 2, false, false, false, true>",
+    "convT_dW": "false, false, false, true>",          # the only b_conv (implicit-im2col B) GEMM: ConvT dW
     "sqnorm_kernel": "sqnorm_kernel",
 }
 
