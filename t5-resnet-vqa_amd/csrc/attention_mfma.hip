@@ -124,6 +124,30 @@ __device__ __forceinline__ void store_tr(bf16_t* base, long ld, int row, bool ok
 
 constexpr int WPB = 2;                                  // waves (= (b, h) pairs) per block
 
+// Values row[key] for this lane's 16 X-layout keys of 32-key tile t (keys 32t + 8g +
+// 4h + 0..3 for register group g), loaded unconditionally at clamped keys: 4 float4
+// loads when the row is 16-B aligned and lk % 4 == 0, else 16 scalar loads.
+__device__ __forceinline__ void load_xrow(const float* row, int lk, int t, bool vec, float (&out)[16]) {
+  const int h5 = (threadIdx.x & 63) >> 5;
+  if (vec) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 v = *reinterpret_cast<const float4*>(row + min(32 * t + 8 * g + 4 * h5, lk - 4));
+      out[4 * g] = v.x; out[4 * g + 1] = v.y; out[4 * g + 2] = v.z; out[4 * g + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[r] = row[min(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5, lk - 1)];
+  }
+}
+
+// bit k = key k is kept by the padding mask (one load + one ballot per wave; lk <= 64)
+__device__ __forceinline__ unsigned long long key_bits(const long long* mrow, int lk) {
+  const int l = threadIdx.x & 63;
+  const long long m = mrow[min(l, lk - 1)];
+  return __ballot(m != 0 && l < lk);
+}
+
 template <int DH>
 struct Geo {
   static constexpr int KS = DH / 16;                    // k-steps over the head dim
@@ -132,69 +156,70 @@ struct Geo {
 };
 
 // ------------------------------------------------------------------ forward
-template <int DH>
+// NT = number of 32-key tiles (1: lk <= 32, 2: lk <= 64), a template parameter so the
+// lk <= 32 shapes (T5, SGA blocks 1-2) issue no work for a second tile.
+template <int DH, int NT>
 __global__ __launch_bounds__(64 * WPB) void attn_fwd_mfma(AttnM P) {
   using G = Geo<DH>;
-  __shared__ __attribute__((aligned(16))) char smem[WPB * 64 * G::ROWB];
+  constexpr int KR = 32 * NT;                            // key rows of the V image
+  __shared__ __attribute__((aligned(16))) char smem[WPB * KR * G::ROWB];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h5 = l >> 5, l31 = l & 31;
   const int pair = blockIdx.x * WPB + w;
   const bool live = pair < P.pairs;
   const int b = live ? pair / P.heads : 0, hh = live ? pair - b * P.heads : 0;
-  const int lq = P.lq, lk = P.lk, nt = (lk + 31) / 32;
-  lds_char* vimg = (lds_char*)smem + w * 64 * G::ROWB;
+  const int lq = P.lq, lk = P.lk;
+  lds_char* vimg = (lds_char*)smem + w * KR * G::ROWB;
   const bf16_t* Q = P.q + (long)b * lq * P.ldq + hh * DH;
   const bf16_t* K = P.k + (long)b * lk * P.ldk + hh * DH;
   const bf16_t* V = P.v + (long)b * lk * P.ldv + hh * DH;
 
   // fragments with k = head dim straight from global (16 B per lane per k-step)
-  bf16x8_t qf[G::KS], kf[2][G::KS];
-  const int qr = min(l31, lq - 1), kr0 = min(l31, lk - 1), kr1 = min(32 + l31, lk - 1);   // clamped rows
+  bf16x8_t qf[G::KS], kf[NT][G::KS];
+  const int qr = min(l31, lq - 1);                                  // clamped rows
 #pragma unroll
   for (int s = 0; s < G::KS; ++s) {
     qf[s] = ld_frag(Q + (long)qr * P.ldq + 16 * s + 8 * h5, live && l31 < lq);
-    kf[0][s] = ld_frag(K + (long)kr0 * P.ldk + 16 * s + 8 * h5, live && l31 < lk);
-    kf[1][s] = ld_frag(K + (long)kr1 * P.ldk + 16 * s + 8 * h5, live && 32 + l31 < lk);
-  }
-  stage_img<DH, 64, G::ROWB>(vimg, V, P.ldv, live ? lk : 0);
-  // additive score terms (rel-bias row, key-padding mask) for this lane's 32 keys,
-  // loaded up front at clamped indices (uniform pointer tests only)
-  const int i = l31;
-  float add[2][16];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NT; ++t)
+      kf[t][s] = ld_frag(K + (long)min(32 * t + l31, lk - 1) * P.ldk + 16 * s + 8 * h5, live && 32 * t + l31 < lk);
+  }
+  stage_img<DH, KR, G::ROWB>(vimg, V, P.ldv, live ? lk : 0);
+  // additive score terms for this lane's keys: rel-bias row (float4 row loads) and the
+  // key-padding mask (one ballot)
+  const int i = l31;
+  float add[NT][16];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) add[t][r] = 0.f;
   if (P.bias) {
     const float* brow = P.bias + ((long)hh * lq + min(i, lq - 1)) * lk;
+    const bool vec = (lk & 3) == 0 && ((uintptr_t)P.bias & 15) == 0;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) add[t][r] = brow[min(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5, lk - 1)];
+    for (int t = 0; t < NT; ++t) load_xrow(brow, lk, t, vec, add[t]);
   }
   if (P.mask) {
-    const long long* mrow = P.mask + (long)b * lk;
+    const unsigned long long kb = key_bits(P.mask + (long)b * lk, lk);
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        add[t][r] += mrow[min(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5, lk - 1)] == 0 ? MASK_MIN : 0.f;
+        add[t][r] += ((kb >> (32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5)) & 1ull) ? 0.f : MASK_MIN;
   }
 
   // S^T tiles (X layout: lane = query, registers = keys)
-  f32x16_t sa[2];
+  f32x16_t sa[NT];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < NT; ++t) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) sa[t][e] = 0.f;
-    if (t < nt) {
 #pragma unroll
-      for (int s = 0; s < G::KS; ++s) sa[t] = mfma(kf[t][s], qf[s], sa[t]);
-    }
+    for (int s = 0; s < G::KS; ++s) sa[t] = mfma(kf[t][s], qf[s], sa[t]);
   }
   // softmax over keys for query i = l31
   float mx = -INFINITY;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5;
@@ -205,7 +230,7 @@ __global__ __launch_bounds__(64 * WPB) void attn_fwd_mfma(AttnM P) {
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   float z = 0.f;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float e = sa[t][r] == -INFINITY ? 0.f : __expf(sa[t][r] - mx);
@@ -218,7 +243,7 @@ __global__ __launch_bounds__(64 * WPB) void attn_fwd_mfma(AttnM P) {
   const long prow = (((long)b * P.heads + hh) * lq + i) * lk;   // element index of P[b, h, i, 0]
   const bool qok = live && i < lq;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int key0 = 32 * t + 8 * g + 4 * h5;
@@ -238,26 +263,25 @@ __global__ __launch_bounds__(64 * WPB) void attn_fwd_mfma(AttnM P) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) oa[e] = 0.f;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      if (s < 2 * nt) oa = mfma(tr_frag<G::ROWB>(vimg, s, et * 32), regs_frag(sa[s >> 1], s), oa);
-    }
+    for (int s = 0; s < 2 * NT; ++s) oa = mfma(tr_frag<G::ROWB>(vimg, s, et * 32), regs_frag(sa[s >> 1], s), oa);
     store_tr(P.o + (long)b * lq * P.ldo + hh * DH, P.ldo, i, qok, et * 32, oa, 1.f);
   }
 }
 
 // ------------------------------------------------------------------ backward
-template <int DH>
+template <int DH, int NT>
 __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
   using G = Geo<DH>;
-  constexpr int IMG = (64 + 32 + 32) * G::ROWB;         // K [64], dO [32], Q [32] images
+  constexpr int KR = 32 * NT;
+  constexpr int IMG = (KR + 32 + 32) * G::ROWB;         // K [32*NT], dO [32], Q [32] images
   __shared__ __attribute__((aligned(16))) char smem[WPB * (IMG + 32 * 4)];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h5 = l >> 5, l31 = l & 31;
   const int pair = blockIdx.x * WPB + w;
   const bool live = pair < P.pairs;
   const int b = live ? pair / P.heads : 0, hh = live ? pair - b * P.heads : 0;
-  const int lq = P.lq, lk = P.lk, nt = (lk + 31) / 32;
+  const int lq = P.lq, lk = P.lk;
   lds_char* kimg = (lds_char*)smem + w * (IMG + 128);
-  lds_char* oimg = kimg + 64 * G::ROWB;
+  lds_char* oimg = kimg + KR * G::ROWB;
   lds_char* qimg = oimg + 32 * G::ROWB;
   float* dis = (float*)(qimg + 32 * G::ROWB);           // D_i per query
   const bf16_t* Q = P.q + (long)b * lq * P.ldq + hh * DH;
@@ -266,15 +290,16 @@ __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
   const bf16_t* dO = P.dout + (long)b * lq * P.lddo + hh * DH;
   const float* Pg = P.p + ((long)b * P.heads + hh) * lq * lk;
 
-  bf16x8_t of[G::KS], vf[2][G::KS];
-  const int qr = min(l31, lq - 1), kr0 = min(l31, lk - 1), kr1 = min(32 + l31, lk - 1);   // clamped rows
+  bf16x8_t of[G::KS], vf[NT][G::KS];
+  const int qr = min(l31, lq - 1);                      // clamped rows
 #pragma unroll
   for (int s = 0; s < G::KS; ++s) {
     of[s] = ld_frag(dO + (long)qr * P.lddo + 16 * s + 8 * h5, live && l31 < lq);
-    vf[0][s] = ld_frag(V + (long)kr0 * P.ldv + 16 * s + 8 * h5, live && l31 < lk);
-    vf[1][s] = ld_frag(V + (long)kr1 * P.ldv + 16 * s + 8 * h5, live && 32 + l31 < lk);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      vf[t][s] = ld_frag(V + (long)min(32 * t + l31, lk - 1) * P.ldv + 16 * s + 8 * h5, live && 32 * t + l31 < lk);
   }
-  stage_img<DH, 64, G::ROWB>(kimg, K, P.ldk, live ? lk : 0);
+  stage_img<DH, KR, G::ROWB>(kimg, K, P.ldk, live ? lk : 0);
   stage_img<DH, 32, G::ROWB>(oimg, dO, P.lddo, live ? lq : 0);
   stage_img<DH, 32, G::ROWB>(qimg, Q, P.ldq, live ? lq : 0);
   const DropK dk = drop_init(P.drop);
@@ -283,28 +308,22 @@ __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
   // ---- X layout (lane = query): dP^T, D_i, dS^T -> dQ^T
   const int i = l31;
   const bool qok = live && i < lq;
-  f32x16_t xa[2];
+  f32x16_t xa[NT];
   float di = 0.f;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < NT; ++t) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) xa[t][e] = 0.f;
-    if (t < nt) {
 #pragma unroll
-      for (int s = 0; s < G::KS; ++s) xa[t] = mfma(vf[t][s], of[s], xa[t]);   // dP^T[key][query]
-    }
+    for (int s = 0; s < G::KS; ++s) xa[t] = mfma(vf[t][s], of[s], xa[t]);     // dP^T[key][query]
   }
-  float px[2][16];
+  float px[NT][16];
   const float* prow = Pg + (long)min(i, lq - 1) * lk;   // saved P of this lane's query (clamped row)
+  const bool pvec = (lk & 3) == 0 && ((uintptr_t)P.p & 15) == 0;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < NT; ++t) load_xrow(prow, lk, t, pvec, px[t]);   // unconditional loads, masked below
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5;
-      px[t][r] = prow[min(key, lk - 1)];                // unconditional loads, masked below
-    }
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5;
@@ -318,7 +337,7 @@ __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
   di += __shfl_xor(di, 32, 64);
   if (h5 == 0) dis[i] = di;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float ds = px[t][r] * (xa[t][r] - di);
@@ -334,15 +353,13 @@ __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-      if (s < 2 * nt) acc = mfma(tr_frag<G::ROWB>(kimg, s, et * 32), regs_frag(xa[s >> 1], s), acc);
+    for (int s = 0; s < 2 * NT; ++s) acc = mfma(tr_frag<G::ROWB>(kimg, s, et * 32), regs_frag(xa[s >> 1], s), acc);
     store_tr(P.dq + (long)b * lq * P.lddq + hh * DH, P.lddq, i, qok, et * 32, acc, P.scale);
   }
 
   // ---- Y layout (lane = key, registers = queries): dP, dS, dropout(P) -> dV^T, dK^T
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    if (t >= nt) continue;
+  for (int t = 0; t < NT; ++t) {
     const int key = 32 * t + l31;
     const bool kok = live && key < lk;
     f32x16_t ya;
@@ -410,8 +427,14 @@ int vqa_attn_fwd_mfma(const vqa_attn_desc* d, hipStream_t s) {
   AttnM M;
   fillm(M, d);
   const dim3 grid(vqa::cdiv(M.pairs, WPB));
-  if (d->dh == 64) hipLaunchKernelGGL(attn_fwd_mfma<64>, grid, dim3(64 * WPB), 0, s, M);
-  else hipLaunchKernelGGL(attn_fwd_mfma<96>, grid, dim3(64 * WPB), 0, s, M);
+  const bool two = d->lk > 32;
+  if (d->dh == 64) {
+    if (two) hipLaunchKernelGGL((attn_fwd_mfma<64, 2>), grid, dim3(64 * WPB), 0, s, M);
+    else hipLaunchKernelGGL((attn_fwd_mfma<64, 1>), grid, dim3(64 * WPB), 0, s, M);
+  } else {
+    if (two) hipLaunchKernelGGL((attn_fwd_mfma<96, 2>), grid, dim3(64 * WPB), 0, s, M);
+    else hipLaunchKernelGGL((attn_fwd_mfma<96, 1>), grid, dim3(64 * WPB), 0, s, M);
+  }
   return vqa::check_launch("vqa_attn_fwd (mfma)");
 }
 
@@ -419,7 +442,13 @@ int vqa_attn_bwd_mfma(const vqa_attn_desc* d, hipStream_t s) {
   AttnM M;
   fillm(M, d);
   const dim3 grid(vqa::cdiv(M.pairs, WPB));
-  if (d->dh == 64) hipLaunchKernelGGL(attn_bwd_mfma<64>, grid, dim3(64 * WPB), 0, s, M);
-  else hipLaunchKernelGGL(attn_bwd_mfma<96>, grid, dim3(64 * WPB), 0, s, M);
+  const bool two = d->lk > 32;
+  if (d->dh == 64) {
+    if (two) hipLaunchKernelGGL((attn_bwd_mfma<64, 2>), grid, dim3(64 * WPB), 0, s, M);
+    else hipLaunchKernelGGL((attn_bwd_mfma<64, 1>), grid, dim3(64 * WPB), 0, s, M);
+  } else {
+    if (two) hipLaunchKernelGGL((attn_bwd_mfma<96, 2>), grid, dim3(64 * WPB), 0, s, M);
+    else hipLaunchKernelGGL((attn_bwd_mfma<96, 1>), grid, dim3(64 * WPB), 0, s, M);
+  }
   return vqa::check_launch("vqa_attn_bwd (mfma)");
 }

@@ -5,7 +5,7 @@ sys.path.insert(0, ROOT)
 import torch
 from __graft_entry__ import load_package
 pkg = load_package(); ops = pkg.ops; L = pkg.lib
-shapes = [(2048, 768, 768), (2048, 3072, 768), (2048, 768, 3072), (2048, 2304, 768), (3136, 768, 18432), (4096, 4096, 4096), (8192, 8192, 8192)]
+shapes = [(2048, 768, 768), (2048, 3072, 768), (2048, 768, 3072), (2048, 2304, 768), (2048, 1536, 768), (3136, 1536, 768)]
 cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["1", "3"]          # "<config>[s<splitk>]"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 s = L.stream_handle()
