@@ -274,16 +274,20 @@ __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
   using G = Geo<DH>;
   constexpr int KR = 32 * NT;
   constexpr int IMG = (KR + 32 + 32) * G::ROWB;         // K [32*NT], dO [32], Q [32] images
-  __shared__ __attribute__((aligned(16))) char smem[WPB * (IMG + 32 * 4)];
+  constexpr int PR = KR + 1;                             // row stride of the P / mask transposes (bank spread)
+  constexpr int TRB = 2 * 32 * PR * 4;                   // saved P and dropout multipliers, [query][key] fp32
+  __shared__ __attribute__((aligned(16))) char smem[WPB * (IMG + 32 * 4 + TRB)];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h5 = l >> 5, l31 = l & 31;
   const int pair = blockIdx.x * WPB + w;
   const bool live = pair < P.pairs;
   const int b = live ? pair / P.heads : 0, hh = live ? pair - b * P.heads : 0;
   const int lq = P.lq, lk = P.lk;
-  lds_char* kimg = (lds_char*)smem + w * (IMG + 128);
+  lds_char* kimg = (lds_char*)smem + w * (IMG + 128 + TRB);
   lds_char* oimg = kimg + KR * G::ROWB;
   lds_char* qimg = oimg + 32 * G::ROWB;
   float* dis = (float*)(qimg + 32 * G::ROWB);           // D_i per query
+  float* plds = dis + 32;                               // P[query][key] (masked, pre-dropout)
+  float* mlds = plds + 32 * PR;                         // dropout multiplier [query][key]
   const bf16_t* Q = P.q + (long)b * lq * P.ldq + hh * DH;
   const bf16_t* K = P.k + (long)b * lk * P.ldk + hh * DH;
   const bf16_t* V = P.v + (long)b * lk * P.ldv + hh * DH;
@@ -329,7 +333,10 @@ __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
       const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5;
       const bool ok = qok && key < lk;
       const float pr = px[t][r] * (ok ? 1.f : 0.f);
-      const float dp = ok ? xa[t][r] * drop_mul(dk, (uint32_t)(pbase + (long)i * lk + key)) : 0.f;
+      const float m = ok ? drop_mul(dk, (uint32_t)(pbase + (long)i * lk + key)) : 0.f;
+      const float dp = xa[t][r] * m;
+      plds[i * PR + key] = pr;                          // transposed for the Y-layout phase
+      mlds[i * PR + key] = m;
       px[t][r] = pr;
       xa[t][r] = dp;                                    // dP (gradient w.r.t. the pre-dropout P)
       di += pr * dp;
@@ -368,19 +375,13 @@ __global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
 #pragma unroll
     for (int s = 0; s < G::KS; ++s) ya = mfma(of[s], vf[t][s], ya);        // dP[query][key]
     f32x16_t pd, dsy;
-    float pv[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r)                          // unconditional loads at clamped (query, key)
-      pv[r] = Pg[(long)min((r & 3) + 8 * (r >> 2) + 4 * h5, lq - 1) * lk + min(key, lk - 1)];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qi = (r & 3) + 8 * (r >> 2) + 4 * h5;
-      const bool ok = kok && qi < lq;
-      const long e = pbase + (long)qi * lk + key;
-      const float pr = pv[r] * (ok ? 1.f : 0.f);
-      const float m = ok ? drop_mul(dk, (uint32_t)e) : 0.f;
+    for (int r = 0; r < 16; ++r) {                        // P and its dropout multiplier from the X phase
+      const int qi = (r & 3) + 8 * (r >> 2) + 4 * h5;     // (zero outside the valid (query, key) range)
+      const float pr = plds[qi * PR + key];
+      const float m = mlds[qi * PR + key];
       pd[r] = pr * m;                                   // dropout(P)
-      dsy[r] = ok ? pr * (ya[r] * m - dis[qi]) : 0.f;   // dS
+      dsy[r] = pr * (ya[r] * m - dis[qi]);              // dS
     }
 #pragma unroll
     for (int et = 0; et < G::ET; ++et) {
