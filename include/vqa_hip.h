@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 4
+#define VQA_ABI_VERSION 5
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -208,6 +208,11 @@ int vqa_colsum_batched(const vqa_colsum_job* jobs, int njobs, int nblocks, hipSt
 /* ---------------------------------------------------------- elementwise ---
  * vqa_image_to_nhwc8: NCHW fp32 [N,3,H,W] (collate ToTensor,
  *   resnet_vqa_daquar_dataset.py:131-137) -> NHWC bf16 [N,H,W,8], ch 3..7 = 0.
+ * vqa_image_to_s2d16: the same image as the stem's space-to-depth input
+ *   Z [N,H/2+1,W/2+1,16] bf16, Z[b,u,v,(2p+q)*3+c] = img[b,c,2u+p-1,2v+q-1]
+ *   (0 outside, ch 12..15 = 0); conv7x7/2 pad 3 over img == conv4x4/1 pad 1
+ *   over Z with W'[o,a,e,(2p+q)*3+c] = W[o,c,2a+p,2e+q] (0 at index 7).
+ *   H and W must be even.
  * vqa_maxpool3x3s2_nhwc: torchvision ResNet maxpool (3, 2, pad 1), bf16 NHWC.
  * vqa_colsum: out[c] = beta*out[c] + sum_r x[r*ld + c] (bias gradients of
  *   every nn.Linear / ConvTranspose2d), ws = vqa_colsum_workspace_floats().
@@ -217,6 +222,7 @@ int vqa_colsum_batched(const vqa_colsum_job* jobs, int njobs, int nblocks, hipSt
  *   precomputed bucket map [Lq*Lk] (TF modeling_t5.py:217-279) and its
  *   scatter-add gradient (dtable zeroed by the caller). */
 int vqa_image_to_nhwc8(const float* img, void* out, int n, int h, int w, hipStream_t stream);
+int vqa_image_to_s2d16(const float* img, void* out, int n, int h, int w, hipStream_t stream);
 int vqa_maxpool3x3s2_nhwc(const void* x, void* y, int n, int h, int w, int c, int oh, int ow, hipStream_t stream);
 int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long long ld, float* out, float beta, float* ws,
                hipStream_t stream);

@@ -21,6 +21,44 @@ __global__ __launch_bounds__(256) void image_to_nhwc8_kernel(const float* __rest
   reinterpret_cast<uint4*>(out)[i] = u;
 }
 
+// NCHW fp32 [N,3,H,W] -> the stem's space-to-depth image Z, NHWC bf16 [N,H/2+1,W/2+1,16]:
+//   Z[b,u,v,(2p+q)*3+c] = img[b,c,2u+p-1,2v+q-1] (0 outside), channels 12..15 = 0.
+// The 7x7 stride-2 pad-3 conv over img equals a 4x4 stride-1 pad-1 conv over Z with
+// W'[o,a,e,(2p+q)*3+c] = W[o,c,2a+p,2e+q] (0 where 2a+p or 2e+q is 7): K = 256
+// instead of 7*7*8 = 392, and every tap is 32 contiguous bytes.
+__global__ __launch_bounds__(256) void image_to_s2d16_kernel(const float* __restrict__ img, bf16_t* __restrict__ out,
+                                                             int n, int h, int w, int hz, int wz) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)n * hz * wz) return;
+  const int v = (int)(i % wz);
+  const long t = i / wz;
+  const int u = (int)(t % hz), b = (int)(t / hz);
+  const float* src = img + (long)b * 3 * h * w;
+  float z[16];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int y = 2 * u + p - 1, x = 2 * v + q - 1;
+      const bool ok = y >= 0 && y < h && x >= 0 && x < w;
+      const long o = ok ? (long)y * w + x : 0;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) z[(2 * p + q) * 3 + c] = ok ? src[(long)c * h * w + o] : 0.f;
+    }
+#pragma unroll
+  for (int c = 12; c < 16; ++c) z[c] = 0.f;
+  uint4 lo, hi;
+  lo.x = (uint32_t)f2bf(z[0]) | ((uint32_t)f2bf(z[1]) << 16);
+  lo.y = (uint32_t)f2bf(z[2]) | ((uint32_t)f2bf(z[3]) << 16);
+  lo.z = (uint32_t)f2bf(z[4]) | ((uint32_t)f2bf(z[5]) << 16);
+  lo.w = (uint32_t)f2bf(z[6]) | ((uint32_t)f2bf(z[7]) << 16);
+  hi.x = (uint32_t)f2bf(z[8]) | ((uint32_t)f2bf(z[9]) << 16);
+  hi.y = (uint32_t)f2bf(z[10]) | ((uint32_t)f2bf(z[11]) << 16);
+  hi.z = 0; hi.w = 0;
+  reinterpret_cast<uint4*>(out)[2 * i] = lo;
+  reinterpret_cast<uint4*>(out)[2 * i + 1] = hi;
+}
+
 // torchvision MaxPool2d(3, 2, 1) on NHWC bf16; 8 channels per thread
 __global__ __launch_bounds__(256) void maxpool3s2_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int n,
                                                          int h, int w, int c, int oh, int ow) {
@@ -308,6 +346,16 @@ __global__ __launch_bounds__(256) void zero_kernel(uint4* __restrict__ p, long n
 }
 
 }  // namespace
+
+extern "C" int vqa_image_to_s2d16(const float* img, void* out, int n, int h, int w, hipStream_t s) {
+  VQA_REQUIRE(img && out && n > 0 && h > 1 && w > 1 && h % 2 == 0 && w % 2 == 0,
+              "vqa_image_to_s2d16: bad arguments (H and W must be even)");
+  const int hz = h / 2 + 1, wz = w / 2 + 1;
+  const long total = (long)n * hz * wz;
+  hipLaunchKernelGGL(image_to_s2d16_kernel, dim3(vqa::cdiv(total, 256)), dim3(256), 0, s, img, (bf16_t*)out, n, h, w,
+                     hz, wz);
+  return vqa::check_launch("vqa_image_to_s2d16");
+}
 
 extern "C" int vqa_image_to_nhwc8(const float* img, void* out, int n, int h, int w, hipStream_t s) {
   VQA_REQUIRE(img && out && n > 0 && h > 0 && w > 0, "vqa_image_to_nhwc8: bad arguments");

@@ -150,14 +150,21 @@ struct Loader {
       ihw = 1.f / (float)(g.oh * g.ow);
       iow = 1.f / (float)g.ow;
     }
+    // ... and when one kernel row is exactly one K-tile (the space-to-depth stem: C 16,
+    // 4 taps), a chunk's (kw, c) is its offset inside the tile: the row is contiguous
+    bool rfast = false;
     if constexpr (KC && GATHER) {
       cfast = (g.c & (BK - 1)) == 0;
+      rfast = !cfast && g.c * g.kw == BK;
       if (cfast) {
         const int tap = k0 / g.c;
         tc0 = k0 - tap * g.c;
         tkh = tap / g.kw;
         tkw = tap - tkh * g.kw;
         toff = (long)(tkh * g.w + tkw) * g.c + tc0;
+      } else if (rfast) {
+        tkh = k0 / BK;
+        toff = (long)tkh * g.w * g.c;
       }
     }
 #pragma unroll
@@ -170,6 +177,9 @@ struct Loader {
         } else if constexpr (KC && GATHER) {
           if (cfast) {                                  // the K-tile lies inside one tap
             const int ih = g1[j] + tkh, iw = g2[j] + tkw;
+            if (ih >= 0 && ih < g.h && iw >= 0 && iw < g.w) src = base + off[j] + toff;
+          } else if (rfast) {                           // the K-tile is kernel row tkh
+            const int ih = g1[j] + tkh, iw = g2[j] + kof[j] / g.c;
             if (ih >= 0 && ih < g.h && iw >= 0 && iw < g.w) src = base + off[j] + toff;
           } else {
             const int tap = kk / g.c;

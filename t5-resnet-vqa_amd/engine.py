@@ -56,6 +56,17 @@ def sga_site(block, kind):
     return 128 + 8 * block + kind
 
 
+def stem_s2d_weight(wf):
+    """The 7x7 stride-2 stem conv weight [Cout, 7, 7, 3] (NHWC order) as the 4x4 stride-1
+    weight [Cout, 4, 4, 16] over vqa_image_to_s2d16's image:
+    W'[o, a, e, (2p+q)*3 + c] = W[o, 2a+p, 2e+q, c], zero where 2a+p or 2e+q is 7."""
+    co, kh, kw, ci = wf.shape
+    w8 = np.zeros((co, 8, 8, ci), np.float32)
+    w8[:, :kh, :kw] = wf
+    w = w8.reshape(co, 4, 2, 4, 2, ci).transpose(0, 1, 3, 2, 4, 5).reshape(co, 4, 4, 4 * ci)
+    return np.concatenate([w, np.zeros((co, 4, 4, 16 - 4 * ci), np.float32)], 3)
+
+
 _TUNE_CACHE = {}
 SPLITS = (1, 2, 3, 4, 6, 8)        # split-K counts the tuner tries for small grids
 
@@ -84,6 +95,7 @@ class VQAEngine:
         self.p_drop, self.seed = float(dropout), int(seed)
         self.dev = torch.device(device)
         self.vision, self.B, self.L, self.H = vision, batch, seq_len, image_size
+        assert image_size % 2 == 0, "the space-to-depth stem needs an even image size"
         self.NB, self.A = num_blocks, answer_spaces
         self.warmup, self.total, self.max_norm = warmup, total, max_norm
         self.betas, self.eps, self.wd = betas, eps, weight_decay
@@ -147,13 +159,13 @@ class VQAEngine:
         self._res_keep = []
         convs = []                                   # (name_conv, name_bn, stride, pad, relu, role)
 
-        def conv_w(cname, bname, cin_pad=None):
+        def conv_w(cname, bname, s2d=False):
             w = sd[vm + cname + ".weight"].astype(np.float32)
             wf, bf = fold_bn(w, sd[vm + bname + ".weight"], sd[vm + bname + ".bias"],
                              sd[vm + bname + ".running_mean"], sd[vm + bname + ".running_var"])
             wf = wf.transpose(0, 2, 3, 1)            # [Cout, kh, kw, Cin]
-            if cin_pad and cin_pad > wf.shape[3]:
-                wf = np.concatenate([wf, np.zeros(wf.shape[:3] + (cin_pad - wf.shape[3],), np.float32)], 3)
+            if s2d:
+                wf = stem_s2d_weight(wf)
             w16 = torch.from_numpy(np.ascontiguousarray(wf)).to(self.dev).to(BF16)
             b32 = torch.from_numpy(bf).to(self.dev)
             self._res_keep += [w16, b32]
@@ -178,7 +190,8 @@ class VQAEngine:
         self.fh, self.fc = hh, cin                    # layer4 spatial size / channels
         self.V_TOK = B * hh * hh
         self.IMG = self._t((B, 3, H, H))
-        self.IMG8 = self._t((B, H, H, 8), BF16)
+        hz = H // 2 + 1                               # space-to-depth stem image (vqa_image_to_s2d16)
+        self.IMG8 = self._t((B, hz, hz, 16), BF16)
         bufs = [self._t(maxel, BF16) for _ in range(5)]
         self.res_bufs = bufs
         self.F4 = self._t((B, hh, hh, cin), BF16)
@@ -187,10 +200,11 @@ class VQAEngine:
         self.F4N = self._t((B, hh, hh, cin), BF16) if self.pipeline else self.F4
 
         # stem: conv7x7/2 + BN + ReLU, then maxpool 3x3/2
-        w16, b32 = conv_w("conv1", "bn1", cin_pad=8)
-        self.res_calls.append(ops.Call("vqa_image_to_nhwc8", self.IMG.data_ptr(), self.IMG8.data_ptr(), B, H, H))
-        g = ops.conv_geom(B, H, H, 8, h1, h1, 7, 7, 2, 3)
-        self._gemm(self.res_calls, self.IMG8, w16, B * h1 * h1, 64, 7 * 7 * 8, lda=392, ldb=392, ga=g,
+        # (as a 4x4 stride-1 conv over the space-to-depth image: K 256 instead of 7*7*8 = 392)
+        w16, b32 = conv_w("conv1", "bn1", s2d=True)
+        self.res_calls.append(ops.Call("vqa_image_to_s2d16", self.IMG.data_ptr(), self.IMG8.data_ptr(), B, H, H))
+        g = ops.conv_geom(B, hz, hz, 16, h1, h1, 4, 4, 1, 1)
+        self._gemm(self.res_calls, self.IMG8, w16, B * h1 * h1, 64, 256, lda=256, ldb=256, ga=g,
                    c16=bufs[0], ldc16=64, bias=b32, relu=True)
         self.res_calls.append(ops.Call("vqa_maxpool3x3s2_nhwc", bufs[0].data_ptr(), bufs[1].data_ptr(), B, h1, h1,
                                        64, h2, h2))

@@ -151,6 +151,7 @@ register("vqa_rng_advance", P)
 register("vqa_dropout_mask", P, P, c_ll)
 register("vqa_colsum_partials", P, c_int, c_ll, c_int, P, c_float)
 register("vqa_image_to_nhwc8", P, P, c_int, c_int, c_int)
+register("vqa_image_to_s2d16", P, P, c_int, c_int, c_int)
 register("vqa_maxpool3x3s2_nhwc", P, P, c_int, c_int, c_int, c_int, c_int, c_int)
 register("vqa_colsum", P, c_int, c_int, c_int, c_ll, P, c_float, P)
 register("vqa_embedding_fwd", P, P, P, c_int, c_int, c_int, P)

@@ -221,6 +221,23 @@ def test_image_and_maxpool(k):
     ref = torch.zeros(2, 20, 20, 8, device="cuda")
     ref[..., :3] = img.permute(0, 2, 3, 1)
     assert torch.equal(out, ref.to(torch.bfloat16))
+    # space-to-depth stem image: exact layout, and the 4x4/1 conv over it equals the 7x7/2 conv
+    for hw in (20, 224):
+        img = torch.rand(2, 3, hw, hw, device="cuda")
+        hz = hw // 2 + 1
+        z = torch.empty(2, hz, hz, 16, device="cuda", dtype=torch.bfloat16)
+        run(k, "vqa_image_to_s2d16", img, z, 2, hw, hw)
+        xp = F.pad(img, (1, 1, 1, 1))                      # x index 2v+q-1 -> padded 2v+q
+        ref = torch.zeros(2, hz, hz, 16, device="cuda")
+        for p in range(2):
+            for q in range(2):
+                ref[..., (2 * p + q) * 3:(2 * p + q) * 3 + 3] = xp[:, :, p:p + 2 * hz:2, q:q + 2 * hz:2].permute(0, 2, 3, 1)
+        assert torch.equal(z, ref.to(torch.bfloat16))
+        w = torch.randn(64, 3, 7, 7)
+        w2 = torch.from_numpy(k.engine.stem_s2d_weight(w.permute(0, 2, 3, 1).numpy()))   # [64, 4, 4, 16]
+        y_ref = F.conv2d(img.to(torch.bfloat16).float().cpu().double(), w.double(), stride=2, padding=3)
+        y_s2d = F.conv2d(z.float().cpu().permute(0, 3, 1, 2).double(), w2.permute(0, 3, 1, 2).double(), padding=1)
+        torch.testing.assert_close(y_s2d, y_ref, rtol=1e-9, atol=1e-9)
     x = rnd((2, 21, 21, 64), 36, dtype=torch.bfloat16)
     y = torch.empty(2, 11, 11, 64, device="cuda", dtype=torch.bfloat16)
     run(k, "vqa_maxpool3x3s2_nhwc", x, y, 2, 21, 21, 64, 11, 11)

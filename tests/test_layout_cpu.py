@@ -59,3 +59,25 @@ def test_bn_fold(pkg):
     wf, bf = pkg.layout.fold_bn(w.numpy(), bw.numpy(), bb.numpy(), rm.numpy(), rv.numpy())
     got = F.conv2d(x, torch.as_tensor(wf), torch.as_tensor(bf), padding=1)
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_stem_space_to_depth_equals_7x7_stride2(pkg):
+    """engine.stem_s2d_weight + the vqa_image_to_s2d16 layout (restated here in torch):
+    the 4x4 stride-1 pad-1 conv over the space-to-depth image is the torchvision stem
+    conv (7x7, stride 2, pad 3, resnet_vqa_model.py:51-58 via torchvision) exactly."""
+    import torch
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(0)
+    for hw in (16, 30):
+        img = torch.rand(2, 3, hw, hw, generator=g, dtype=torch.float64)
+        w = torch.randn(8, 3, 7, 7, generator=g, dtype=torch.float64)
+        hz = hw // 2 + 1
+        xp = F.pad(img, (1, 1, 1, 1))
+        z = torch.zeros(2, 16, hz, hz, dtype=torch.float64)
+        for p in range(2):
+            for q in range(2):
+                z[:, (2 * p + q) * 3:(2 * p + q) * 3 + 3] = xp[:, :, p:p + 2 * hz:2, q:q + 2 * hz:2]
+        w2 = torch.from_numpy(pkg.engine.stem_s2d_weight(w.permute(0, 2, 3, 1).float().numpy())).double()
+        y = F.conv2d(z, w2.permute(0, 3, 1, 2), padding=1)
+        ref = F.conv2d(img, w.float().double(), stride=2, padding=3)
+        torch.testing.assert_close(y, ref, rtol=1e-12, atol=1e-12)

@@ -47,3 +47,5 @@ for s, e in iv[1:]:
         ce = max(ce, e)
 busy += ce - cs
 print(f"step {(t1 - t0) / 1e3:.1f} us, union busy {busy / 1e3:.1f} us, idle {(t1 - t0 - busy) / 1e3:.1f} us")
+tot = sum(e - s for s, e, n, q in win)
+print(f"sum of kernel durations {tot / 1e3:.1f} us (> union busy = overlap)")
