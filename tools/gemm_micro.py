@@ -6,6 +6,8 @@ import torch
 from __graft_entry__ import load_package
 pkg = load_package(); ops = pkg.ops; L = pkg.lib
 shapes = [(2048, 768, 768), (2048, 3072, 768), (2048, 768, 3072), (2048, 2304, 768), (2048, 1536, 768), (3136, 1536, 768)]
+if len(sys.argv) > 3:                                                        # "MxNxK,MxNxK"
+    shapes = [tuple(int(v) for v in t.split("x")) for t in sys.argv[3].split(",")]
 cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["1", "3"]          # "<config>[s<splitk>]"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 s = L.stream_handle()
