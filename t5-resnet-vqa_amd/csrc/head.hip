@@ -16,58 +16,66 @@ namespace {
 
 constexpr int MAXA = 1024;
 
-// ------------------------------------------------------------ pooler
-// block-wide reduction of NV per-thread vectors of length L (one value per row t)
-template <int LMAX>
-__device__ __forceinline__ void block_row_sums(float (&part)[LMAX], int L, float* red /*[4][LMAX]*/,
-                                               float* out /*[LMAX]*/) {
-  constexpr int SH = LMAX == 16 ? 2 : (LMAX == 32 ? 1 : 0);     // lane >> SH = row index after the scatter
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const float v = wave_sum_scatter<LMAX>(part);
-  if ((l & ((1 << SH) - 1)) == 0) red[wv * LMAX + (l >> SH)] = v;
-  __syncthreads();
-  for (int t = threadIdx.x; t < L; t += 256) out[t] = red[t] + red[LMAX + t] + red[2 * LMAX + t] + red[3 * LMAX + t];
-  __syncthreads();
-}
-
 // Loads whose row/column may fall outside the tensor are issued UNconditionally
 // at a clamped index and masked by a multiply: a "cond ? load : 0" (or a select
 // of a loaded value, which hipcc sinks back into a branch) makes every load its
 // own branch + vmcnt(0) wait (one L2 round trip per element,
 // cdna_hip_programming.md §5 'Three .s-level traps' (c)).
 //
-// The whole forward head of one sample in one workgroup (resnet_vqa_model.py:152-160):
-// pooler (scores, softmax over L, weighted sum) -> pooled row in LDS -> 170 logits, one wave per
-// answer at a time, lanes striding the D-long dot so the Wc row read is one
-// coalesced 256-B access per step -> log_softmax over the answers in LDS -> NLL.
-template <int LMAX>
-__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wp,
-                                                       const float* __restrict__ bp, const float* __restrict__ wc,
-                                                       const float* __restrict__ bc, const long long* __restrict__ tgt,
-                                                       float* __restrict__ att, float* __restrict__ pooled,
-                                                       float* __restrict__ logp, float* __restrict__ nll, int L, int D,
-                                                       int A) {
-  constexpr int NC = 3;
-  __shared__ float red[4 * LMAX], sc[LMAX], lg[MAXA], r4[4];
-  __shared__ __attribute__((aligned(16))) float pr[768];
-  const int b = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
-  const float* xb = x + (long)b * L * D;
-  float xr[LMAX][NC], part[LMAX];
-  float w[NC];
-#pragma unroll
-  for (int j = 0; j < NC; ++j) w[j] = (tid + 256 * j < D) ? wp[tid + 256 * j] : 0.f;
-#pragma unroll
-  for (int t = 0; t < LMAX; ++t) {
-    part[t] = 0.f;
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      const int d = tid + 256 * j;
-      const float v = xb[(long)min(t, L - 1) * D + min(d, D - 1)];   // unconditional load, masked value
-      xr[t][j] = v * ((t < L && d < D) ? 1.f : 0.f);
-      part[t] = fmaf(xr[t][j], w[j], part[t]);
-    }
+// Forward, three launches (resnet_vqa_model.py:152-160):
+//   head_pool_fwd      one workgroup per sample: scores, softmax over L, pooled row
+//   head_logits        (8 answers) x (16 samples) per workgroup: logits = pooled Wc^T + bc
+//   head_lse           one workgroup: log_softmax over the answers, NLL, mean loss
+// Backward, three launches:
+//   head_dpooled       dlogits = (softmax - onehot)/B and dpooled = dlogits Wc, 64 columns x
+//                      16 samples per workgroup, the answer sum split over the 4 waves
+//   head_pool_bwd      one workgroup per sample: pooler backward -> dx, and the sample's
+//                      pooler-weight partial sum_l dscore_l x_l (the thread owns its columns)
+//   head_wgrad         classifier dWc / dbc tiles (16 answers x 256 columns) and the fixed-order
+//                      sum of the per-sample pooler partials, in one two-role launch
+// Pooler kernels: 768 threads = 4 row groups x 192 float4 columns (D <= 768, D % 4 == 0);
+// a thread holds RPG = LMAX/4 rows of one float4 column in registers, so each sample is
+// read once with 16-B loads and the 12 waves of the workgroup share the instruction stream
+// (one wave per SIMD spent ~4x longer issuing the scalar-load form).  Row sums: a
+// reduce-scatter inside each wave, then the 3 waves of the row group in a fixed order.
+constexpr int PC4 = 192;                               // float4 columns per row group
+template <int RPG>
+__device__ __forceinline__ void pool_row_sums(float (&part)[RPG], float* red /*[12][RPG]*/, float* out, int L) {
+  constexpr int SH = RPG == 4 ? 4 : (RPG == 8 ? 3 : 2);   // lane >> SH = row index after the scatter
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const float v = wave_sum_scatter<RPG>(part);
+  if ((l & ((1 << SH) - 1)) == 0) red[wv * RPG + (l >> SH)] = v;
+  __syncthreads();
+  if (threadIdx.x < 4 * RPG) {                          // row r = group * RPG + i: waves 3g, 3g+1, 3g+2
+    const int g = threadIdx.x / RPG, i = threadIdx.x - g * RPG;
+    if (g * RPG + i < L)
+      out[g * RPG + i] = (red[(3 * g) * RPG + i] + red[(3 * g + 1) * RPG + i]) + red[(3 * g + 2) * RPG + i];
   }
-  block_row_sums<LMAX>(part, L, red, sc);
+  __syncthreads();
+}
+
+template <int LMAX>
+__global__ __launch_bounds__(768) void head_pool_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wp,
+                                                            const float* __restrict__ bp, float* __restrict__ att,
+                                                            float* __restrict__ pooled, int L, int D) {
+  constexpr int RPG = LMAX / 4;
+  __shared__ float red[12 * RPG], sc[LMAX];
+  __shared__ __attribute__((aligned(16))) float4 pr[4][PC4];
+  const int b = blockIdx.x, tid = threadIdx.x, g = tid / PC4, c4 = tid - g * PC4, C4 = D / 4;
+  const float cm = c4 < C4 ? 1.f : 0.f;
+  const float4* xb = reinterpret_cast<const float4*>(x + (long)b * L * D) + min(c4, C4 - 1);
+  const float4 w = reinterpret_cast<const float4*>(wp)[min(c4, C4 - 1)];
+  float4 xr[RPG];
+  float part[RPG];
+#pragma unroll
+  for (int i = 0; i < RPG; ++i) {
+    const int r = g * RPG + i;
+    const float4 v = xb[(long)min(r, L - 1) * C4];       // unconditional load, masked value
+    const float m = (r < L) ? cm : 0.f;
+    xr[i] = make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
+    part[i] = xr[i].x * w.x + xr[i].y * w.y + xr[i].z * w.z + xr[i].w * w.w;
+  }
+  pool_row_sums<RPG>(part, red, sc, L);
   if (tid < 64) {                                     // softmax over the sequence (Softmax(dim=1))
     const float s = tid < L ? sc[tid] + bp[0] : -INFINITY;
     const float m = wave_max(s);
@@ -76,223 +84,319 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
     if (tid < L) { sc[tid] = e / z; att[(long)b * L + tid] = e / z; }
   }
   __syncthreads();
+  float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int j = 0; j < NC; ++j) {
-    const int d = tid + 256 * j;
-    if (d >= D) continue;
-    float p = 0.f;
-#pragma unroll
-    for (int t = 0; t < LMAX; ++t)
-      if (t < L) p = fmaf(sc[t], xr[t][j], p);
-    pooled[(long)b * D + d] = p;
-    pr[d] = p;
+  for (int i = 0; i < RPG; ++i) {
+    const float a = g * RPG + i < L ? sc[g * RPG + i] : 0.f;
+    p.x = fmaf(a, xr[i].x, p.x); p.y = fmaf(a, xr[i].y, p.y); p.z = fmaf(a, xr[i].z, p.z); p.w = fmaf(a, xr[i].w, p.w);
   }
+  pr[g][c4] = p;
   __syncthreads();
-  // logits = pooled Wc^T + bc: each wave takes 8 answers per pass; a lane holds 12
-  // pooled values (float4 columns lane, lane+64, lane+128) and issues its 24 Wc float4
-  // loads before the first FMA, so a pass costs one L2 round trip (D <= 768)
-  {
-    float4 pv[3];
+  if (g == 0 && c4 < C4) {                            // fixed order over the 4 row groups
+    float4 o = pr[0][c4];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) { o.x += pr[q][c4].x; o.y += pr[q][c4].y; o.z += pr[q][c4].z; o.w += pr[q][c4].w; }
+    reinterpret_cast<float4*>(pooled + (long)b * D)[c4] = o;
+  }
+}
+
+// logits[b, a] = pooled[b, :] . Wc[a, :] + bc[a] for 8 answers x 16 samples per workgroup:
+// a lane holds float4 columns (lane, lane+64, lane+128) of the 8 Wc rows, each wave takes
+// 4 samples; one wave_sum_scatter<8> per sample finishes 8 dots at once (D <= 768, D % 4 == 0)
+__global__ __launch_bounds__(256) void head_logits_kernel(const float* __restrict__ pooled,
+                                                          const float* __restrict__ wc, const float* __restrict__ bc,
+                                                          float* __restrict__ logits, int B, int D, int A) {
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int a0 = blockIdx.x * 8, s0 = blockIdx.y * 16 + wv * 4;
+  float4 wr[8][3];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int k = 4 * (l + 64 * j), a = a0 + u;
+      const float4 t = *reinterpret_cast<const float4*>(wc + (long)min(a, A - 1) * D + min(k, D - 4));
+      const float m = (a < A && k < D) ? 1.f : 0.f;
+      wr[u][j] = make_float4(t.x * m, t.y * m, t.z * m, t.w * m);
+    }
+  float4 pv[4][3];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int k = 4 * (l + 64 * j);
-      pv[j] = k < D ? *reinterpret_cast<const float4*>(pr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 t = *reinterpret_cast<const float4*>(pooled + (long)min(s0 + q, B - 1) * D + min(k, D - 4));
+      const float m = k < D ? 1.f : 0.f;
+      pv[q][j] = make_float4(t.x * m, t.y * m, t.z * m, t.w * m);
     }
-    for (int a0 = 8 * wv; a0 < A; a0 += 32) {
-      float4 wr[8][3];
+  const int a = a0 + (l >> 3);
+  const float bias = bc[min(a, A - 1)];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+  for (int q = 0; q < 4; ++q) {
+    float sv[8];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const int k = 4 * (l + 64 * j), a = a0 + u;
-          const float4 t = *reinterpret_cast<const float4*>(wc + (long)min(a, A - 1) * D + min(k, D - 4));
-          const float m = (a < A && k < D) ? 1.f : 0.f;
-          wr[u][j] = make_float4(t.x * m, t.y * m, t.z * m, t.w * m);
-        }
-      float sv[8];
+    for (int u = 0; u < 8; ++u) {
+      float s = 0.f;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        float s = 0.f;
+      for (int j = 0; j < 3; ++j)
+        s += pv[q][j].x * wr[u][j].x + pv[q][j].y * wr[u][j].y + pv[q][j].z * wr[u][j].z + pv[q][j].w * wr[u][j].w;
+      sv[u] = s;
+    }
+    const float s = wave_sum_scatter<8>(sv);          // lane group l>>3 holds answer a0 + (l>>3)
+    if ((l & 7) == 0 && a < A && s0 + q < B) logits[(long)(s0 + q) * A + a] = s + bias;
+  }
+}
+
+// log_softmax over the answers (in place: logits -> log-probs), NLL of the target and the
+// mean loss, one 1024-thread workgroup: wave w takes samples w, w+16, ... (A <= 1024)
+template <int NI>                                      // answers per lane: A <= 64 * NI
+__global__ __launch_bounds__(1024) void head_lse_kernel(float* __restrict__ lp, const long long* __restrict__ tgt,
+                                                        float* __restrict__ nll, float* __restrict__ loss, int B,
+                                                        int A) {
+  __shared__ float nl[1024];
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int b0 = wv * 4; b0 < B; b0 += 64) {            // 4 samples per wave and pass, all loads first
+    float v[4][NI];
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          s += pv[j].x * wr[u][j].x + pv[j].y * wr[u][j].y + pv[j].z * wr[u][j].z + pv[j].w * wr[u][j].w;
-        sv[u] = s;
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < NI; ++i) v[q][i] = lp[(long)min(b0 + q, B - 1) * A + min(l + 64 * i, A - 1)];
+    int t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = tgt ? (int)tgt[min(b0 + q, B - 1)] : -1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int b = b0 + q;
+      float m = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        if (l + 64 * i < A) m = fmaxf(m, v[q][i]);
+      m = wave_max(m);
+      float z = 0.f, vt = 0.f;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        if (l + 64 * i < A) z += __expf(v[q][i] - m);
+        if (l + 64 * i == t[q]) vt = v[q][i];
       }
-      const float s = wave_sum_scatter<8>(sv);          // lane group l>>3 holds answer a0 + (l>>3)
-      const int a = a0 + (l >> 3);
-      if ((l & 7) == 0 && a < A) lg[a] = s + bc[a];
+      const float lse = m + __logf(wave_sum(z));
+      vt = wave_sum(vt);                                // the one lane holding the target
+      if (b < B) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          if (l + 64 * i < A) lp[(long)b * A + l + 64 * i] = v[q][i] - lse;
+        if (tgt && l == 0) { nl[b & 1023] = -(vt - lse); nll[b] = -(vt - lse); }
+      }
     }
   }
+  if (!tgt) return;
   __syncthreads();
-  float m = -INFINITY;
-  for (int c = tid; c < A; c += 256) m = fmaxf(m, lg[c]);
-  m = wave_max(m);
-  if (l == 0) r4[wv] = m;
-  __syncthreads();
-  m = fmaxf(fmaxf(r4[0], r4[1]), fmaxf(r4[2], r4[3]));
-  __syncthreads();
-  float z = 0.f;
-  for (int c = tid; c < A; c += 256) z += __expf(lg[c] - m);
-  z = wave_sum(z);
-  if (l == 0) r4[wv] = z;
-  __syncthreads();
-  const float lse = m + __logf(r4[0] + r4[1] + r4[2] + r4[3]);
-  for (int c = tid; c < A; c += 256) logp[(long)b * A + c] = lg[c] - lse;
-  if (tid == 0 && tgt) nll[b] = -(lg[tgt[b]] - lse);
+  if (threadIdx.x == 0) {                             // fixed-order mean (NLLLoss reduction='mean')
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += nl[b];
+    loss[0] = s / (float)B;
+  }
 }
 
-// fixed-order mean / sum of n values by one workgroup
-__global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ v, int n, float scale,
-                                                     float* __restrict__ out) {
-  __shared__ float red[4];
-  float s = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) s += v[i];
-  s = block_sum<256>(s, red);
-  if (threadIdx.x == 0) out[0] = s * scale;
+// dlogits (kept for the classifier weight gradient) and dpooled = dlogits Wc.
+// Workgroup = 64 columns x 16 samples; wave w sums answers [w*AQ, (w+1)*AQ) with all of its
+// Wc loads in flight, then the four wave partials are added in a fixed order through LDS.
+constexpr int DP_AQ = 48;                             // answers per wave (4 * 48 >= A)
+__global__ __launch_bounds__(256) void head_dpooled_kernel(const float* __restrict__ lp,
+                                                           const long long* __restrict__ tgt,
+                                                           const float* __restrict__ wc, float* __restrict__ dl_out,
+                                                           float* __restrict__ dpooled, int B, int D, int A,
+                                                           float inv_b) {
+  constexpr int AP = 4 * DP_AQ;                       // padded answer row in LDS
+  __shared__ __attribute__((aligned(16))) float dl[16][AP];
+  __shared__ float red[4][16][64];
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int c = blockIdx.x * 64 + l, s0 = blockIdx.y * 16;
+  constexpr int FI = 16 * AP / 256;                   // fill elements per thread (all loads first)
+  float ev[FI];
+  int tv[FI];
+#pragma unroll
+  for (int k = 0; k < FI; ++k) {
+    const int i = tid + 256 * k, q = i / AP, a = i - q * AP, b = min(s0 + q, B - 1);
+    ev[k] = lp[(long)b * A + min(a, A - 1)];
+    tv[k] = (int)tgt[b];
+  }
+#pragma unroll
+  for (int k = 0; k < FI; ++k) {
+    const int i = tid + 256 * k, q = i / AP, a = i - q * AP, b = s0 + q;
+    const float g = (b < B && a < A) ? (__expf(ev[k]) - (a == tv[k] ? 1.f : 0.f)) * inv_b : 0.f;
+    dl[q][a] = g;
+    if (blockIdx.x == 0 && b < B && a < A) dl_out[(long)b * A + a] = g;
+  }
+  float w[DP_AQ];
+#pragma unroll
+  for (int i = 0; i < DP_AQ; ++i)
+    w[i] = wc[(long)min(wv * DP_AQ + i, A - 1) * D + min(c, D - 1)];   // masked through dl = 0 past A
+  __syncthreads();
+  float acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < DP_AQ; i += 4) {
+      const float4 g = *reinterpret_cast<const float4*>(&dl[q][wv * DP_AQ + i]);
+      s = fmaf(g.x, w[i], s);
+      s = fmaf(g.y, w[i + 1], s);
+      s = fmaf(g.z, w[i + 2], s);
+      s = fmaf(g.w, w[i + 3], s);
+    }
+    acc[q] = s;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) red[wv][q][l] = acc[q];
+  __syncthreads();
+  for (int i = tid; i < 16 * 64; i += 256) {
+    const int q = i >> 6, cl = i & 63, b = s0 + q, cc = blockIdx.x * 64 + cl;
+    const float v = ((red[0][q][cl] + red[1][q][cl]) + red[2][q][cl]) + red[3][q][cl];
+    if (b < B && cc < D) dpooled[(long)b * D + cc] = v;
+  }
 }
 
-// Backward of one sample in one workgroup: dlogits = (softmax - onehot)/B (kept
-// for the classifier weight gradient), dpooled = dlogits Wc (each thread its
-// D/256 columns, Wc rows read coalesced), then the pooler backward:
-// da = x dpooled ; dscore = a (da - sum a da) ; dx = a dpooled^T + dscore wp^T.
+// Pooler backward of one sample: da = x dpooled ; dscore = a (da - sum a da) ;
+// dx = a dpooled^T + dscore wp^T ; and the sample's pooler weight / bias partials
+// part[b, d] = sum_l dscore_l x[l, d], pbp[b] = sum_l dscore_l (summed over b by head_wgrad).
+// Same 4 row groups x 192 float4 columns layout as head_pool_fwd_kernel.
 template <int LMAX>
-__global__ __launch_bounds__(256) void head_bwd_sample_kernel(
-    const float* __restrict__ x, const float* __restrict__ att, const float* __restrict__ logp,
-    const long long* __restrict__ tgt, const float* __restrict__ wc, const float* __restrict__ wp,
-    float* __restrict__ dl_out, float* __restrict__ dx32, bf16_t* __restrict__ dx16, float* __restrict__ dscore, int L,
-    int D, int A, float inv_b) {
-  constexpr int NC = 3;
-  __shared__ float red[4 * LMAX], da[LMAX], a[LMAX], dl[MAXA];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const long long t = tgt[b];
-  for (int c = tid; c < A; c += 256) {
-    const float g = (__expf(logp[(long)b * A + c]) - (c == t ? 1.f : 0.f)) * inv_b;
-    dl[c] = g;
-    dl_out[(long)b * A + c] = g;
+__global__ __launch_bounds__(768) void head_pool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ att,
+                                                            const float* __restrict__ dpooled,
+                                                            const float* __restrict__ wp, float* __restrict__ dx32,
+                                                            bf16_t* __restrict__ dx16, float* __restrict__ part,
+                                                            float* __restrict__ pbp, int L, int D) {
+  constexpr int RPG = LMAX / 4;
+  __shared__ float red[12 * RPG], da[LMAX], a[LMAX];
+  __shared__ __attribute__((aligned(16))) float4 pr[4][PC4];
+  const int b = blockIdx.x, tid = threadIdx.x, g = tid / PC4, c4 = tid - g * PC4, C4 = D / 4;
+  const float cm = c4 < C4 ? 1.f : 0.f;
+  if (tid < L) a[tid] = att[(long)b * L + tid];
+  const float4* xb = reinterpret_cast<const float4*>(x + (long)b * L * D) + min(c4, C4 - 1);
+  const float4 w = reinterpret_cast<const float4*>(wp)[min(c4, C4 - 1)];
+  float4 dp = reinterpret_cast<const float4*>(dpooled + (long)b * D)[min(c4, C4 - 1)];
+  dp = make_float4(dp.x * cm, dp.y * cm, dp.z * cm, dp.w * cm);
+  float4 xr[RPG];
+  float pt[RPG];
+#pragma unroll
+  for (int i = 0; i < RPG; ++i) {
+    const int r = g * RPG + i;
+    const float4 v = xb[(long)min(r, L - 1) * C4];       // unconditional load, masked value
+    const float m = (r < L) ? cm : 0.f;
+    xr[i] = make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
+    pt[i] = xr[i].x * dp.x + xr[i].y * dp.y + xr[i].z * dp.z + xr[i].w * dp.w;
   }
-  for (int s = tid; s < L; s += 256) a[s] = att[(long)b * L + s];
-  __syncthreads();
-  // dpooled: 16 answers x 3 columns of Wc in flight per thread (coalesced rows)
-  float dp[NC] = {0.f, 0.f, 0.f}, w[NC];
-  for (int c0 = 0; c0 < A; c0 += 16) {
-    float wv[16][NC];
-#pragma unroll
-    for (int u = 0; u < 16; ++u)
-#pragma unroll
-      for (int j = 0; j < NC; ++j) {
-        const int d = tid + 256 * j;
-        const float v = wc[(long)min(c0 + u, A - 1) * D + min(d, D - 1)];
-        wv[u][j] = v * ((c0 + u < A && d < D) ? 1.f : 0.f);
-      }
-#pragma unroll
-    for (int u = 0; u < 16; ++u)
-#pragma unroll
-      for (int j = 0; j < NC; ++j) dp[j] = fmaf(c0 + u < A ? dl[c0 + u] : 0.f, wv[u][j], dp[j]);
-  }
-#pragma unroll
-  for (int j = 0; j < NC; ++j) w[j] = tid + 256 * j < D ? wp[tid + 256 * j] : 0.f;
-  const float* xb = x + (long)b * L * D;
-  float xr[LMAX][NC], part[LMAX];
-#pragma unroll
-  for (int s = 0; s < LMAX; ++s) {
-    part[s] = 0.f;
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      const int d = tid + 256 * j;
-      const float v = xb[(long)min(s, L - 1) * D + min(d, D - 1)];   // unconditional load, masked value
-      xr[s][j] = v * ((s < L && d < D) ? 1.f : 0.f);
-      part[s] = fmaf(xr[s][j], dp[j], part[s]);
-    }
-  }
-  block_row_sums<LMAX>(part, L, red, da);
+  pool_row_sums<RPG>(pt, red, da, L);
   if (tid < 64) {
     const float ai = tid < L ? a[tid] : 0.f, dai = tid < L ? da[tid] : 0.f;
     const float s = wave_sum(ai * dai);
-    if (tid < L) {
-      const float ds = ai * (dai - s);
-      da[tid] = ds;
-      dscore[(long)b * L + tid] = ds;
-    }
+    const float ds = tid < L ? ai * (dai - s) : 0.f;
+    if (tid < L) da[tid] = ds;
+    const float tot = wave_sum(ds);
+    if (tid == 0) pbp[b] = tot;
   }
   __syncthreads();
+  float4 pw = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int s = 0; s < LMAX; ++s) {
-    if (s >= L) continue;
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      const int d = tid + 256 * j;
-      if (d >= D) continue;
-      const float g = a[s] * dp[j] + da[s] * w[j];
-      dx32[((long)b * L + s) * D + d] = g;
-      if (dx16) dx16[((long)b * L + s) * D + d] = f2bf(g);
+  for (int i = 0; i < RPG; ++i) {
+    const int r = g * RPG + i;
+    if (r >= L) continue;
+    const float ar = a[r], dr = da[r];
+    pw.x = fmaf(dr, xr[i].x, pw.x); pw.y = fmaf(dr, xr[i].y, pw.y);
+    pw.z = fmaf(dr, xr[i].z, pw.z); pw.w = fmaf(dr, xr[i].w, pw.w);
+    if (c4 >= C4) continue;
+    const float4 o = make_float4(ar * dp.x + dr * w.x, ar * dp.y + dr * w.y, ar * dp.z + dr * w.z,
+                                 ar * dp.w + dr * w.w);
+    const long e = ((long)b * L + r) * D + 4 * c4;
+    *reinterpret_cast<float4*>(dx32 + e) = o;
+    if (dx16) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(o.x) | ((uint32_t)f2bf(o.y) << 16);
+      u.y = (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16);
+      *reinterpret_cast<uint2*>(dx16 + e) = u;
     }
+  }
+  pr[g][c4] = pw;
+  __syncthreads();
+  if (g == 0 && c4 < C4) {                            // fixed order over the 4 row groups
+    float4 o = pr[0][c4];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) { o.x += pr[q][c4].x; o.y += pr[q][c4].y; o.z += pr[q][c4].z; o.w += pr[q][c4].w; }
+    reinterpret_cast<float4*>(part + (long)b * D)[c4] = o;
   }
 }
 
-// Weight gradients of the head, two workgroup roles in one launch:
-//   blocks [0, A): classifier row a: dWc[a, :] = sum_b dl[b, a] pooled[b, :], dbc[a] = sum_b dl[b, a]
-//   blocks [A, A + parts): pooler partials over a 64-row chunk p:
-//     part[p, :] = sum_rows dscore[row] x[row, :], pbp[p] = sum_rows dscore[row]
-// (fixed-order sums; the partials are reduced by head_pool_final_kernel)
+// Two roles, fixed-order sums over the B samples:
+//   blocks [0, nca * ncd): dWc[a, c] = sum_b dl[b, a] pooled[b, c] for 16 answers x 256 columns
+//     (thread = column, 16 accumulators), dbc[a] = sum_b dl[b, a] (column block 0)
+//   blocks [nca * ncd, + ncd): dWp[c] = sum_b part[b, c], dbp = sum_b pbp[b]
 __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict__ dl, const float* __restrict__ pooled,
-                                                         const float* __restrict__ x, const float* __restrict__ ds,
+                                                         const float* __restrict__ part, const float* __restrict__ pbp,
                                                          float* __restrict__ dwc, float* __restrict__ dbc,
-                                                         float* __restrict__ part, float* __restrict__ pbp, int B,
-                                                         int A, int rows, int D) {
-  // both roles: out[d] = sum_{r in [r0, r1)} coef[r] * src[r, d] for the thread's 3
-  // columns, 16 rows x 3 columns of loads in flight per thread (fixed row order)
-  const int blk = blockIdx.x, tid = threadIdx.x;
-  __shared__ float cf[64];
-  const bool cls = blk < A;
-  const int r0 = cls ? 0 : (blk - A) * 64, r1 = cls ? B : min(rows, r0 + 64);
-  const float* srcm = cls ? pooled : x;
-  float acc[3] = {0.f, 0.f, 0.f}, csum = 0.f;
-  for (int c0 = r0; c0 < r1; c0 += 64) {             // coefficient chunks of 64 rows
-    const int cn = min(64, r1 - c0);
-    __syncthreads();
-    for (int r = tid; r < cn; r += 256) cf[r] = cls ? dl[(long)(c0 + r) * A + blk] : ds[c0 + r];
-    __syncthreads();
-    for (int q0 = 0; q0 < cn; q0 += 16) {
-      float v[16][3];
+                                                         float* __restrict__ dwp, float* __restrict__ dbp, int B, int A,
+                                                         int D) {
+  __shared__ __attribute__((aligned(16))) float cf[64][16];
+  const int tid = threadIdx.x, ncd = (D + 255) / 256, nca = (A + 15) / 16;
+  const int blk = blockIdx.x;
+  if (blk < nca * ncd) {
+    const int a0 = (blk / ncd) * 16, c = (blk % ncd) * 256 + tid;
+    float acc[16], csum = 0.f;
 #pragma unroll
-      for (int u = 0; u < 16; ++u)
+    for (int u = 0; u < 16; ++u) acc[u] = 0.f;
+    for (int b0 = 0; b0 < B; b0 += 64) {
+      const int bn = min(64, B - b0);
+      __syncthreads();
+      for (int i = tid; i < 64 * 16; i += 256) {
+        const int q = i >> 4, u = i & 15;
+        const float v = dl[(long)(b0 + min(q, bn - 1)) * A + min(a0 + u, A - 1)];
+        cf[q][u] = (q < bn && a0 + u < A) ? v : 0.f;
+      }
+      __syncthreads();
+      if (tid < 16)                                     // dbc: the staged coefficients, fixed order
+        for (int q = 0; q < 64; ++q) csum += cf[q][tid];
+      float pv[64];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const int d = tid + 256 * j;
-          const float t = srcm[(long)(c0 + min(q0 + u, cn - 1)) * D + min(d, D - 1)];
-          v[u][j] = t * ((q0 + u < cn && d < D) ? 1.f : 0.f);
+      for (int q = 0; q < 64; ++q) pv[q] = pooled[(long)(b0 + min(q, bn - 1)) * D + min(c, D - 1)];
+#pragma unroll
+      for (int q = 0; q < 64; ++q) {
+#pragma unroll
+        for (int u = 0; u < 16; u += 4) {
+          const float4 g = *reinterpret_cast<const float4*>(&cf[q][u]);   // zero past bn / A
+          acc[u] = fmaf(g.x, pv[q], acc[u]);
+          acc[u + 1] = fmaf(g.y, pv[q], acc[u + 1]);
+          acc[u + 2] = fmaf(g.z, pv[q], acc[u + 2]);
+          acc[u + 3] = fmaf(g.w, pv[q], acc[u + 3]);
         }
+      }
+    }
+    if (c < D)
 #pragma unroll
       for (int u = 0; u < 16; ++u)
+        if (a0 + u < A) dwc[(long)(a0 + u) * D + c] = acc[u];
+    if (blk % ncd == 0 && tid < 16 && a0 + tid < A) dbc[a0 + tid] = csum;
+  } else {
+    const int c = (blk - nca * ncd) * 256 + tid;
+    float s = 0.f;
+    for (int b0 = 0; b0 < B; b0 += 16) {
+      float v[16];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[j] = fmaf(q0 + u < cn ? cf[q0 + u] : 0.f, v[u][j], acc[j]);
+      for (int u = 0; u < 16; ++u) v[u] = part[(long)min(b0 + u, B - 1) * D + min(c, D - 1)];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (b0 + u < B) s += v[u];
     }
-    if (tid == 0)
-      for (int r = 0; r < cn; ++r) csum += cf[r];
-  }
-  float* out = cls ? dwc + (long)blk * D : part + (long)(blk - A) * D;
-#pragma unroll
-  for (int j = 0; j < 3; ++j)
-    if (tid + 256 * j < D) out[tid + 256 * j] = acc[j];
-  if (tid == 0) {
-    if (cls) dbc[blk] = csum; else pbp[blk - A] = csum;
-  }
-}
-
-// dWp[d] = sum_p part[p, d], dbp = sum_p pbp[p]   (fixed order)
-__global__ __launch_bounds__(256) void head_pool_final_kernel(const float* __restrict__ part,
-                                                              const float* __restrict__ pbp, int parts, int D,
-                                                              float* __restrict__ dwp, float* __restrict__ dbp) {
-  const int d = blockIdx.x * 256 + threadIdx.x;
-  if (d < D) {
-    float s = 0.f;
-    for (int p = 0; p < parts; ++p) s += part[(long)p * D + d];
-    dwp[d] = s;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float s = 0.f;
-    for (int p = 0; p < parts; ++p) s += pbp[p];
-    dbp[0] = s;
+    if (c < D) dwp[c] = s;
+    if (blk == nca * ncd) {                           // dbp: stage pbp in LDS, one thread sums in order
+      for (int b0 = 0; b0 < B; b0 += 256) {
+        __syncthreads();
+        if (b0 + tid < B) cf[tid >> 4][tid & 15] = pbp[b0 + tid];
+        __syncthreads();
+        if (tid == 0) {
+          float t = b0 ? dbp[0] : 0.f;
+          for (int q = 0; q < min(256, B - b0); ++q) t += cf[q >> 4][q & 15];
+          dbp[0] = t;
+        }
+      }
+    }
   }
 }
 
@@ -306,51 +410,58 @@ int with_lmax(int L, F f) {
 }  // namespace
 
 extern "C" int vqa_head_workspace_floats(int batch, int seq, int d, int answers) {
-  return 2 * batch * answers + batch * d + batch * seq + vqa::cdiv(batch * seq, 64) * d;
+  (void)seq;
+  return batch + batch * answers + 2 * batch * d;
 }
 
-// ws layout: logits | dlogits [B*A] each, dpooled [B*D], dscore [B*L], dWp partials
+// logits go through `logp` (head_logits writes them, head_lse turns them into log-probs in place)
 extern "C" int vqa_head_fwd(const float* x, const float* wp, const float* bp, const float* wc, const float* bc,
                             const long long* targets, float* att, float* pooled, float* logp, float* nll, float* loss,
                             int batch, int seq, int d, int answers, hipStream_t s) {
   VQA_REQUIRE(x && wp && bp && wc && bc && att && pooled && logp, "vqa_head_fwd: null argument");
-  VQA_REQUIRE(seq <= 64 && d <= 768 && d % 4 == 0 && answers <= MAXA,
-              "vqa_head_fwd: shape out of range (L<=64, D<=768, D%4==0)");
+  VQA_REQUIRE(seq <= 64 && d <= 768 && d % 4 == 0 && answers <= MAXA && batch <= 1024,
+              "vqa_head_fwd: shape out of range (L<=64, D<=768, D%4==0, A<=1024, B<=1024)");
   VQA_REQUIRE(!targets || (nll && loss), "vqa_head_fwd: targets need nll and loss outputs");
   int rc = with_lmax(seq, [&](auto lm) {
-    hipLaunchKernelGGL(head_fwd_kernel<decltype(lm)::value>, dim3(batch), dim3(256), 0, s, x, wp, bp, wc, bc, targets,
-                       att, pooled, logp, nll, seq, d, answers);
-    return vqa::check_launch("vqa_head_fwd");
+    hipLaunchKernelGGL(head_pool_fwd_kernel<decltype(lm)::value>, dim3(batch), dim3(768), 0, s, x, wp, bp, att, pooled,
+                       seq, d);
+    return vqa::check_launch("vqa_head_fwd/pool");
   });
   if (rc) return rc;
-  if (targets) {
-    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, s, nll, batch, 1.0f / batch, loss);
-    return vqa::check_launch("vqa_head_fwd/mean");
-  }
-  return VQA_OK;
+  hipLaunchKernelGGL(head_logits_kernel, dim3(vqa::cdiv(answers, 8), vqa::cdiv(batch, 16)), dim3(256), 0, s, pooled, wc,
+                     bc, logp, batch, d, answers);
+  if ((rc = vqa::check_launch("vqa_head_fwd/logits"))) return rc;
+  if (answers <= 256)
+    hipLaunchKernelGGL(head_lse_kernel<4>, dim3(1), dim3(1024), 0, s, logp, targets, nll, loss, batch, answers);
+  else
+    hipLaunchKernelGGL(head_lse_kernel<16>, dim3(1), dim3(1024), 0, s, logp, targets, nll, loss, batch, answers);
+  return vqa::check_launch("vqa_head_fwd/lse");
 }
 
+// ws layout: pbp [B] | dlogits [B*A] | dpooled [B*D] | pooler partials [B*D]
 extern "C" int vqa_head_bwd(const float* x, const float* att, const float* pooled, const float* logp,
                             const long long* targets, const float* wp, const float* wc, float* dx32, void* dx16,
                             float* dwp, float* dbp, float* dwc, float* dbc, float* ws, int batch, int seq, int d,
                             int answers, hipStream_t s) {
   VQA_REQUIRE(x && att && pooled && logp && targets && wp && wc && dx32 && dwp && dbp && dwc && dbc && ws,
               "vqa_head_bwd: null argument");
-  VQA_REQUIRE(seq <= 64 && d <= 768 && answers <= MAXA, "vqa_head_bwd: shape out of range");
-  const int rows = batch * seq, parts = vqa::cdiv(rows, 64);
-  float* pbp = ws;                                   // [parts] (parts <= batch*answers)
-  float* dl = ws + batch * answers;                  // [B, A]
-  float* dsc = dl + batch * answers + batch * d;     // [B*L]
-  float* part = dsc + batch * seq;                   // [parts, D]
-  int rc = with_lmax(seq, [&](auto lm) {
-    hipLaunchKernelGGL(head_bwd_sample_kernel<decltype(lm)::value>, dim3(batch), dim3(256), 0, s, x, att, logp,
-                       targets, wc, wp, dl, dx32, (bf16_t*)dx16, dsc, seq, d, answers, 1.0f / batch);
-    return vqa::check_launch("vqa_head_bwd/sample");
+  VQA_REQUIRE(seq <= 64 && d <= 768 && answers <= 4 * DP_AQ, "vqa_head_bwd: shape out of range (A <= 192)");
+  float* pbp = ws;
+  float* dl = pbp + batch;
+  float* dpool = dl + batch * answers;
+  float* part = dpool + batch * d;
+  hipLaunchKernelGGL(head_dpooled_kernel, dim3(vqa::cdiv(d, 64), vqa::cdiv(batch, 16)), dim3(256), 0, s, logp, targets,
+                     wc, dl, dpool, batch, d, answers, 1.0f / batch);
+  int rc = vqa::check_launch("vqa_head_bwd/dpooled");
+  if (rc) return rc;
+  rc = with_lmax(seq, [&](auto lm) {
+    hipLaunchKernelGGL(head_pool_bwd_kernel<decltype(lm)::value>, dim3(batch), dim3(768), 0, s, x, att, dpool, wp, dx32,
+                       (bf16_t*)dx16, part, pbp, seq, d);
+    return vqa::check_launch("vqa_head_bwd/pool");
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(head_wgrad_kernel, dim3(answers + parts), dim3(256), 0, s, dl, pooled, x, dsc, dwc, dbc, part, pbp,
-                     batch, answers, rows, d);
-  if ((rc = vqa::check_launch("vqa_head_bwd/wgrad"))) return rc;
-  hipLaunchKernelGGL(head_pool_final_kernel, dim3(vqa::cdiv(d, 256)), dim3(256), 0, s, part, pbp, parts, d, dwp, dbp);
-  return vqa::check_launch("vqa_head_bwd/final");
+  const int ncd = vqa::cdiv(d, 256), nca = vqa::cdiv(answers, 16);
+  hipLaunchKernelGGL(head_wgrad_kernel, dim3(nca * ncd + ncd), dim3(256), 0, s, dl, pooled, part, pbp, dwc, dbc, dwp, dbp,
+                     batch, answers, d);
+  return vqa::check_launch("vqa_head_bwd/wgrad");
 }

@@ -143,8 +143,9 @@ def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5, pd):
         torch.testing.assert_close(red - 3.0, bf.grad, rtol=1e-3, atol=1e-3)
 
 
-def test_head_fwd_bwd(k):
-    B, L, D, A = 8, 32, 768, 170
+@pytest.mark.parametrize("B,L,A", [(8, 32, 170), (64, 32, 170), (37, 49, 13), (5, 16, 192)])
+def test_head_fwd_bwd(k, B, L, A):
+    D = 768
     x = rnd((B, L, D), 20)
     wp, bp = 0.03 * rnd(D, 21), 0.1 * rnd(1, 22)
     wc, bc = 0.03 * rnd((A, D), 23), 0.1 * rnd(A, 24)
