@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 5
+#define VQA_ABI_VERSION 6
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -109,6 +109,12 @@ typedef struct vqa_gemm_desc {
   int splitk;
   void* workspace;
   long long workspace_bytes;
+  /* batched launches of distinct layers (the 3 SGA blocks' self-attention halves):
+   * bias of batch z at bias + z*stride_bias; drop_site_stride != 0 gives batch z its
+   * own dropout site (drop.site + z*drop_site_stride) with element indices restarting
+   * at 0, i.e. exactly the masks of z separate launches (0: one site, index (z*m+row)*n+col) */
+  long long stride_bias;
+  int drop_site_stride;
 } vqa_gemm_desc;
 
 /* tile configs: 1 128x128/3 stages, 2 128x64/4, 3 64x64/4, 4 64x64/2, 5 64x64/3, 6 128x64/2,
@@ -172,6 +178,9 @@ int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t stream);
  *   rmsnorm_bwd drop_dy: the incoming dy is masked (backward of that dropout);
  *     drop_dx32 / drop_dx16: mask applied to that output only (the residual
  *     branch gradient of `h + dropout(f(h))`, or the embedding dropout)
+ *   layernorm_bwd: dres is added into dx32 only (a running sum of residual
+ *     gradients, e.g. the text gradient of the SGA blocks); dx16 and dsum see
+ *     the LayerNorm input gradient alone.
  *   layernorm_bwd drop_dx16: mask on the bf16 output only (SGA dropout1..3);
  *     dsum (may be NULL) = column sums of that masked branch gradient in fp32,
  *     i.e. the bias gradient of the Linear feeding the dropout (fused). */

@@ -49,6 +49,8 @@ struct GemmParams {
   int splitk, kper;        // K slices and 64-deep k-tiles per slice (splitk <= 1: no split)
   float* slab;             // [batch][tile][slice][BM*BN] fp32 partials, fragment order
   unsigned* cnt;           // [batch][tile] arrival counters (zero between launches)
+  long sbias;              // bias stride per batch element
+  int dsite;               // != 0: batch z uses dropout site + z*dsite, element indices from 0
 };
 
 // byte offset of 16-B chunk `ch` of row `row` in a k-contig image ([rows][64 bf16])
@@ -473,8 +475,12 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
   const bf16_t* R16 = P.res16 ? P.res16 + (long)z * P.sres : nullptr;
   const bf16_t* MK = P.mask16 ? P.mask16 + (long)z * P.sres : nullptr;
   const bool beta = P.beta != 0.f && C32;
-  const DropK dk = drop_init(P.drop);
-  const uint32_t ebase = (uint32_t)z * (uint32_t)P.m;  // dropout element index = (z*m + row)*n + col
+  vqa_dropout dz = P.drop;
+  if (P.dsite) dz.site += (unsigned)(z * P.dsite);
+  const DropK dk = drop_init(dz);
+  // dropout element index = (z*m + row)*n + col (one site), or row*n + col at site + z*dsite
+  const uint32_t ebase = P.dsite ? 0u : (uint32_t)z * (uint32_t)P.m;
+  const float* BIAS = P.bias ? P.bias + (long)z * P.sbias : nullptr;
   const int rl = l & 31, ch = l >> 5;
   if (P.vec) {
     // Staged through LDS (the ring is idle now): each wave parks alpha*acc of its
@@ -536,9 +542,9 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
 #pragma unroll
           for (int t = 0; t < 8; ++t) kf[t] *= drop_mul(dk, e + t);
         }
-        if (P.bias) {
-          const float4 b0 = *reinterpret_cast<const float4*>(P.bias + col);
-          const float4 b1 = *reinterpret_cast<const float4*>(P.bias + col + 4);
+        if (BIAS) {
+          const float4 b0 = *reinterpret_cast<const float4*>(BIAS + col);
+          const float4 b1 = *reinterpret_cast<const float4*>(BIAS + col + 4);
           const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
           for (int t = 0; t < 8; ++t) v[t] += bb[t];
@@ -597,7 +603,7 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
           float kf = 1.f;
           if (MK && !(bf2f(MK[(long)row * P.ldmask + col]) > 0.f)) kf = 0.f;
           if (dk.on) kf *= drop_mul(dk, (ebase + (uint32_t)row) * (uint32_t)P.n + (uint32_t)col);
-          float v = kf * (acc[i][j][e] * P.alpha + (P.bias ? P.bias[col] : 0.f));
+          float v = kf * (acc[i][j][e] * P.alpha + (BIAS ? BIAS[col] : 0.f));
           if (R32) v += R32[(long)row * P.ldres + col];
           if (R16) v += bf2f(R16[(long)row * P.ldres + col]);
           if (P.relu) v = fmaxf(v, 0.f);
@@ -760,6 +766,8 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
   P.ga = d->ga; P.gb = d->gb;
   P.sa = d->stride_a; P.sb = d->stride_b; P.sc32 = d->stride_c32; P.sc16 = d->stride_c16; P.sres = d->stride_res;
   P.drop = d->drop;
+  P.sbias = d->stride_bias;
+  P.dsite = d->drop_site_stride;
   P.splitk = 1;
   P.kper = 0;
   P.slab = nullptr;
@@ -783,7 +791,8 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
           (!d->c16 || (d->ldc16 % 8 == 0 && al(d->c16, 16) && d->stride_c16 % 8 == 0)) &&
           (!d->res32 || (d->ldres % 8 == 0 && al(d->res32, 16))) && (!d->res16 || (d->ldres % 8 == 0 && al(d->res16, 16))) &&
           (!d->mask16 || (d->ldmask % 8 == 0 && al(d->mask16, 16))) &&
-          (!(d->res32 || d->res16 || d->mask16) || d->stride_res % 8 == 0) && al(d->bias, 16);
+          (!(d->res32 || d->res16 || d->mask16) || d->stride_res % 8 == 0) && al(d->bias, 16) &&
+          d->stride_bias % 4 == 0;
   return VQA_OK;
 }
 

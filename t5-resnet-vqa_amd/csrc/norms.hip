@@ -216,10 +216,10 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   for (int row = r0 + wv; row < r1; row += ROWS_PER_BLOCK) {
-    float d[NV][4], v[NV][4], o[NV][4];
+    float d[NV][4], v[NV][4], o[NV][4], rr[NV][4];
     load_row<NV>(dy + (long)row * D, d);
     load_row<NV>(x + (long)row * D, v);
-    if (dres) load_row<NV>(dres + (long)row * D, o);   // issued with dy and x: one round trip per row
+    if (dres) load_row<NV>(dres + (long)row * D, rr);  // issued with dy and x: one round trip per row
     const float mu = mean[row], r = rstd[row];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -239,10 +239,12 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
     for (int i = 0; i < NV; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float t = r * (g[i][j] * d[i][j] - s1 - v[i][j] * s2);
-        o[i][j] = dres ? o[i][j] + t : t;
+        o[i][j] = r * (g[i][j] * d[i][j] - s1 - v[i][j] * s2);
+        if (dres) rr[i][j] += o[i][j];
       }
-    if (dx32) store_row32<NV>(dx32 + (long)row * D, o);
+    // post-LN: dres is an accumulator that only the fp32 output carries; the branch
+    // gradient (dx16, dsum) is the LayerNorm input gradient alone
+    if (dx32) store_row32<NV>(dx32 + (long)row * D, dres ? rr : o);
     if (dx16 || with_dsum) {
       drop_row<NV>(k16, row, o);                           // the branch gradient (masked)
       if (dx16) store_row16<NV>(dx16 + (long)row * D, o);

@@ -275,15 +275,18 @@ class VQAEngine:
         self.R1 = [t(T) for _ in range(nl)]
         self.RF = t(T)
         self.TXT32, self.TXT16 = t((T, D)), t((T, D), BF16)
-        # SGA blocks
+        # SGA blocks; the self-attention halves of all blocks share batched buffers:
+        # q|k|v of block n in columns [n*2304, (n+1)*2304) of QKV1A, merge in/out in [n]
+        self.QKV1A = t((T, NB * 3 * D), BF16)
+        self.O1A, self.S1A = t((NB, T, D), BF16), t((NB, T, D))
         self.sga = []
         for n in range(NB):
             ly = V if n == 0 else T
             lk = self.fh * self.fh if n == 0 else Lq
             self.sga.append(dict(
                 ly=ly, lk=lk,
-                QKV1=t((T, 3 * D), BF16), P1=t((B, S.SGA_HEADS, Lq, Lq)), O1=t((T, D), BF16),
-                S1=t((T, D)), X1=t((T, D)), X1h=t((T, D), BF16), MU1=t(T), RS1=t(T),
+                P1=t((B, S.SGA_HEADS, Lq, Lq)), O1=self.O1A[n], S1=self.S1A[n],
+                X1=t((T, D)), X1h=t((T, D), BF16), MU1=t(T), RS1=t(T),
                 Q2=t((T, D), BF16), KV2=t((ly, 2 * D), BF16), P2=t((B, S.SGA_HEADS, Lq, lk)), O2=t((T, D), BF16),
                 S2=t((T, D)), X2=t((T, D)), X2h=t((T, D), BF16), MU2=t(T), RS2=t(T),
                 FFh=t((T, D), BF16), S3=t((T, D)), OUT=t((T, D)), OUTh=t((T, D), BF16), MU3=t(T), RS3=t(T)))
@@ -296,6 +299,9 @@ class VQAEngine:
         self.dA32 = t((T, D))
         self._gbufs = {}
         self.dC32 = t((T, D))
+        self.dTA = [t((T, D)), t((T, D))]              # running text gradient of the SGA norm1s (ping-pong)
+        self.dA1A, self.dO1A = t((NB, T, D), BF16), t((NB, T, D), BF16)
+        self.dQKV1A = t((T, NB * 3 * D), BF16)
         self.dO16 = t((T, D), BF16)
         self.dTXT = t((T, D))
         self.dVIS32, self.dVIS16 = t((V, D)), t((V, D), BF16)
@@ -315,19 +321,35 @@ class VQAEngine:
     # buffer can be freed while a prepared call still points at it.  Raw int
     # addresses (sub-views made with ops.addr) must come from tensors that are
     # passed too or are engine attributes.
-    def _gemm(self, lst, a, b, m, n, k, **kw):
-        ts = [a, b] + [v for v in kw.values() if isinstance(v, torch.Tensor)]
+    def _gemm(self, lst, a, b, m, n, k, keep=(), **kw):
+        ts = [a, b] + [v for v in kw.values() if isinstance(v, torch.Tensor)] + list(keep)
         lst.append(ops.gemm_call(ops.gemm_desc(a, b, m, n, k, **kw), [t for t in ts if isinstance(t, torch.Tensor)]))
+
+    def _sga_self_keep(self):
+        """The flat-arena views the batched SGA self-attention launches read past: the
+        blocks' q|k|v and merge weights, biases and gradients sit side by side (layout.py)."""
+        names = [f"sga{n}.{w}" for w in ("qkv1_w", "qkv1_b", "m1_w", "m1_b") for n in range(self.NB)]
+        for w in ("qkv1_w", "qkv1_b", "m1_w", "m1_b"):
+            segs = [self.lay[f"sga{n}.{w}"] for n in range(self.NB)]
+            assert all(b.offset == a.offset + a.numel for a, b in zip(segs, segs[1:])), w
+        return tuple(self.p16[k] for k in names if k in self.p16) + tuple(self.p32[k] for k in names) + \
+            tuple(self.g32[k] for k in names)
+
+    def _set_drop(self, call, site):
+        d = self._drop(site)
+        if d is not None:
+            call.desc.drop = d
+            call.keep = call.keep + (self.RNG,)
 
     def _call(self, lst, name, *args, extra=()):
         ts = tuple(a for a in args if isinstance(a, torch.Tensor)) + tuple(extra)
         lst.append(ops.Call(name, *[ops.addr(a) if isinstance(a, torch.Tensor) else a for a in args], keep=ts))
 
-    def _attn(self, lst, fn, drop=None, **kw):
+    def _attn(self, lst, fn, drop=None, keep=(), **kw):
         d = L.AttnDesc()
         for k, v in kw.items():
             setattr(d, k, ops.addr(v) if isinstance(v, torch.Tensor) else v)
-        ts = tuple(v for v in kw.values() if isinstance(v, torch.Tensor))
+        ts = tuple(v for v in kw.values() if isinstance(v, torch.Tensor)) + tuple(keep)
         dd = self._drop(drop) if drop is not None else None
         if dd is not None:
             d.drop = dd
@@ -473,16 +495,29 @@ class VQAEngine:
         # SGA blocks: x = text always, y chained
         y16 = self.VIS16
         sc = 1.0 / math.sqrt(S.SGA_DHEAD)
-        for n in range(self.NB):
+        # self-attention halves of all blocks first (they only read the T5 output): one q|k|v
+        # projection with N = 3 * 2304, the blocks' attentions, one batched merge
+        NB, W3 = self.NB, 3 * D
+        self._gemm(f, self.TXT16, self.p16["sga0.qkv1_w"], T, NB * W3, D, lda=D, ldb=D, c16=self.QKV1A,
+                   ldc16=NB * W3, bias=self.p32["sga0.qkv1_b"], keep=self._sga_self_keep())
+        for n in range(NB):
+            s, c0 = self.sga[n], n * W3
+            q = self.QKV1A
+            self._attn(f, "vqa_attn_fwd", q=ops.addr(q, c0), ldq=NB * W3, k=ops.addr(q, c0 + D), ldk=NB * W3,
+                       v=ops.addr(q, c0 + 2 * D), ldv=NB * W3, o=s["O1"], ldo=D, p=s["P1"], batch=B,
+                       heads=S.SGA_HEADS, lq=Lq, lk=Lq, dh=S.SGA_DHEAD, scale=sc, drop=sga_site(n, 0),
+                       keep=(q,))
+        self._gemm(f, self.O1A, self.p16["sga0.m1_w"], T, D, D, lda=D, ldb=D, c32=self.S1A, ldc32=D,
+                   bias=self.p32["sga0.m1_b"], res32=self.TXT32, ldres=D, batch=NB, stride_a=T * D,
+                   stride_b=D * D, stride_c32=T * D, stride_res=0, stride_bias=D,
+                   drop_site_stride=sga_site(1, 1) - sga_site(0, 1), keep=self._sga_self_keep())
+        self._set_drop(f[-1], sga_site(0, 1))
+        for n in range(NB):
             s, p = self.sga[n], f"sga{n}."
-            self._linear(f, self.TXT16, p + "qkv1_w", T, out16=s["QKV1"])
-            q = s["QKV1"]
-            self._attn(f, "vqa_attn_fwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
-                       ldv=3 * D, o=s["O1"], ldo=D, p=s["P1"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=Lq,
-                       dh=S.SGA_DHEAD, scale=sc, drop=sga_site(n, 0))
-            self._linear(f, s["O1"], p + "m1_w", T, out32=s["S1"], res32=self.TXT32, drop=sga_site(n, 1))
             self._call(f, "vqa_layernorm_fwd", s["S1"], self.p32[p + "ln1_g"], self.p32[p + "ln1_b"], s["X1"],
                        s["X1h"], s["MU1"], s["RS1"], T, D, 1e-5)
+        for n in range(NB):
+            s, p = self.sga[n], f"sga{n}."
             self._linear(f, s["X1h"], p + "q2_w", T, out16=s["Q2"])
             self._linear(f, y16, p + "kv2_w", s["ly"], out16=s["KV2"])
             kv = s["KV2"]
@@ -538,9 +573,9 @@ class VQAEngine:
             # every bf16 gradient a weight-gradient GEMM reads gets its own buffer, so the dW
             # GEMMs can trail the dX chain on another stream without write-after-read hazards
             g = lambda nm, shape: self._gbuf(f"{p}{nm}", shape)
-            dA3, dA2, dA1 = g("dA3", (T, D)), g("dA2", (T, D)), g("dA1", (T, D))
+            dA3, dA2 = g("dA3", (T, D)), g("dA2", (T, D))
             dB, dQ = g("dB", (T, D)), g("dQ", (T, D))
-            dKV, dQKV = g("dKV", (s["ly"], 2 * D)), g("dQKV", (T, 3 * D))
+            dKV = g("dKV", (s["ly"], 2 * D))
             # norm3 + FFN: dA32 = grad of x + dropout3(ffn(x)) (the residual), dA16 = its dropout3 branch;
             # the fc2 bias gradient (column sums of the branch) is fused into the LayerNorm backward
             kp = []
@@ -571,25 +606,49 @@ class VQAEngine:
                 self._dxdw(b, dKV, y16, p + "kv2_w", s["ly"], bias_from=dKV, out32=self.dVIS32, out16=self.dVIS16)
             else:
                 self._dxdw(b, dKV, y16, p + "kv2_w", s["ly"], bias_from=dKV, out32=self.dY[(n - 1) & 1])
-            # norm1 + self attention
+            # norm1: its residual input is the T5 output, so the text gradient of the blocks
+            # accumulates here (dres = the running sum); the merge branch goes to dA1A[n]
             kp = []
             ws = self._norm_ws()
-            self._call(b, "vqa_layernorm_bwd", self.dC32, s["S1"], s["MU1"], s["RS1"], self.p32[p + "ln1_g"], None,
-                       self.dA32, dA1, None, None, ws, T, D,
-                       self._dptr(sga_site(n, 1), kp), self.g32[p + "m1_b"], extra=kp + [self.RNG])
+            self._call(b, "vqa_layernorm_bwd", self.dC32, s["S1"], s["MU1"], s["RS1"], self.p32[p + "ln1_g"],
+                       None if n == NB - 1 else self.dTA[(n + 1) & 1], self.dTA[n & 1], self.dA1A[n], None, None,
+                       ws, T, D, self._dptr(sga_site(n, 1), kp), self.g32[p + "m1_b"], extra=kp + [self.RNG])
             for j, nm in enumerate(("ln1_g", "ln1_b", "m1_b")):      # ws = [parts][dgamma | dbeta | dsum]
                 self._defer(ws, nparts, 3 * D, D, self.g32[p + nm], offset=j * D)
-            self._dxdw(b, dA1, s["O1"], p + "m1_w", T, out16=self.dO16)
-            q = s["QKV1"]
-            dq = dQKV
-            self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
-                       ldv=3 * D, p=s["P1"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=Lq, dh=S.SGA_DHEAD, scale=sc,
-                       dout=self.dO16, lddo=D, dq=dq, lddq=3 * D, dk=ops.addr(dq, D), lddk=3 * D,
-                       dv=ops.addr(dq, 2 * D), lddv=3 * D, drop=sga_site(n, 0))
-            # text gradient accumulates over the three blocks (x is the T5 output for every block)
-            self._dxdw(b, dq, self.TXT16, p + "qkv1_w", T, bias_from=dq, out32=self.dTXT, res32=self.dA32,
-                       beta=0.0 if n == NB - 1 else 1.0)
             mark(f"sga{n}.ln3_b")
+        # the blocks' self-attention halves, batched: merge dX / dW (batch NB), the
+        # attentions, then ONE q|k|v dX GEMM over K = NB * 2304 (it also sums the blocks'
+        # text gradients, plus the norm1 residual sum as res32) paired with ONE q|k|v dW GEMM
+        W3 = 3 * D
+        keep = self._sga_self_keep()
+        self._gemm(b, self.dA1A, self.p16["sga0.m1_w"], T, D, D, lda=D, ldb=D, b_trans=True, c16=self.dO1A,
+                   ldc16=D, batch=NB, stride_a=T * D, stride_b=D * D, stride_c16=T * D, keep=keep)
+        self._gemm(b, self.dA1A, self.O1A, D, D, T, lda=D, ldb=D, a_trans=True, b_trans=True,
+                   c32=self.g32["sga0.m1_w"], ldc32=D, batch=NB, stride_a=T * D, stride_b=T * D,
+                   stride_c32=D * D, keep=keep)
+        b[-1].side = True
+        dq = self.dQKV1A
+        for n in reversed(range(NB)):
+            s, c0 = self.sga[n], n * W3
+            q = self.QKV1A
+            self._attn(b, "vqa_attn_bwd", q=ops.addr(q, c0), ldq=NB * W3, k=ops.addr(q, c0 + D), ldk=NB * W3,
+                       v=ops.addr(q, c0 + 2 * D), ldv=NB * W3, p=s["P1"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=Lq,
+                       dh=S.SGA_DHEAD, scale=sc, dout=self.dO1A[n], lddo=D, dq=ops.addr(dq, c0), lddq=NB * W3,
+                       dk=ops.addr(dq, c0 + D), lddk=NB * W3, dv=ops.addr(dq, c0 + 2 * D), lddv=NB * W3,
+                       drop=sga_site(n, 0), keep=(q, dq))
+        tmp = []
+        self._gemm(tmp, dq, self.p16["sga0.qkv1_w"], T, D, NB * W3, lda=NB * W3, ldb=D, b_trans=True,
+                   c32=self.dTXT, ldc32=D, res32=self.dTA[0], ldres=D, keep=keep)
+        self._gemm(tmp, dq, self.TXT16, NB * W3, D, T, lda=NB * W3, ldb=D, a_trans=True, b_trans=True,
+                   c32=self.g32["sga0.qkv1_w"], ldc32=D, keep=keep)
+        tmp[1].side = True                         # not paired: the K = NB * 2304 dX wants split-K
+        b.extend(tmp)
+        lib = L.load()
+        ws = self._t(lib.vqa_colsum_workspace_floats(T, NB * W3))
+        self._call(b, "vqa_colsum", dq, 1, T, NB * W3, NB * W3, None, 0.0, ws)
+        self._defer(ws, lib.vqa_colsum_parts(T), NB * W3, NB * W3, self.g32["sga0.qkv1_b"])
+        self._jobs[-1] = self._jobs[-1][:-1] + (self._jobs[-1][-1] + keep,)
+        mark(f"sga{NB - 1}.m1_b")
         # ConvTranspose2d scaler weight/bias gradient: implicit im2col of layer4 as the B operand
         # (vision branch: independent of the T5 backward below; its own colsum workspace)
         self._bsplit = [len(b)]

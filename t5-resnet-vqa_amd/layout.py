@@ -62,11 +62,7 @@ class ParamLayout:
         add("pool_b", (1,), "attention_pooler", ["attention_pooler.attention.0.bias"])
         for n in reversed(range(num_blocks)):
             p = f"sga_modules.{n}."
-            m1, m2 = p + "mhatt1.", p + "mhatt2."
-            add(f"sga{n}.qkv1_w", (3 * D, D), "sga_modules", [m1 + f"linear_{x}.weight" for x in "qkv"])
-            add(f"sga{n}.qkv1_b", (3 * D,), "sga_modules", [m1 + f"linear_{x}.bias" for x in "qkv"])
-            add(f"sga{n}.m1_w", (D, D), "sga_modules", [m1 + "linear_merge.weight"])
-            add(f"sga{n}.m1_b", (D,), "sga_modules", [m1 + "linear_merge.bias"])
+            m2 = p + "mhatt2."
             add(f"sga{n}.q2_w", (D, D), "sga_modules", [m2 + "linear_q.weight"])
             add(f"sga{n}.q2_b", (D,), "sga_modules", [m2 + "linear_q.bias"])
             add(f"sga{n}.kv2_w", (2 * D, D), "sga_modules", [m2 + f"linear_{x}.weight" for x in "kv"])
@@ -79,6 +75,19 @@ class ParamLayout:
             for ln in (1, 2, 3):
                 add(f"sga{n}.ln{ln}_g", (D,), "sga_modules", [p + f"norm{ln}.norm.weight"])
                 add(f"sga{n}.ln{ln}_b", (D,), "sga_modules", [p + f"norm{ln}.norm.bias"])
+        # the self-attention halves of the blocks (x = the T5 output for every block)
+        # run as batched launches after the blocks' sequential parts: their weights sit side
+        # by side in block order, so the three q|k|v projections form one [3*2304, 768] matrix
+        # and the three merges one batch with a constant stride
+        m1 = lambda n: f"sga_modules.{n}.mhatt1."
+        for n in range(num_blocks):
+            add(f"sga{n}.qkv1_w", (3 * D, D), "sga_modules", [m1(n) + f"linear_{x}.weight" for x in "qkv"])
+        for n in range(num_blocks):
+            add(f"sga{n}.qkv1_b", (3 * D,), "sga_modules", [m1(n) + f"linear_{x}.bias" for x in "qkv"])
+        for n in range(num_blocks):
+            add(f"sga{n}.m1_w", (D, D), "sga_modules", [m1(n) + "linear_merge.weight"])
+        for n in range(num_blocks):
+            add(f"sga{n}.m1_b", (D,), "sga_modules", [m1(n) + "linear_merge.bias"])
         add("scaler_w", (D, 3, 3, self.scaler_cin), "scaler", [self.scaler + ".weight"], kind="convT")
         add("scaler_b", (D,), "scaler", [self.scaler + ".bias"])
         t5 = "lang_model."

@@ -47,6 +47,7 @@ class GemmDesc(ctypes.Structure):
         ("stride_c16", c_ll), ("stride_res", c_ll), ("config", c_int),
         ("drop", Dropout),
         ("splitk", c_int), ("workspace", c_void_p), ("workspace_bytes", c_ll),
+        ("stride_bias", c_ll), ("drop_site_stride", c_int),
     ]
 
 

@@ -68,6 +68,14 @@ def test_layernorm_fwd_bwd(k, rows):
     torch.testing.assert_close(dx, xr.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dg, gr.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-3)
+    # dres accumulates into dx32 only; the bf16 branch output and dsum are the LN gradient alone
+    dres, dx16, dsum = rnd((rows, D), 9), torch.empty(rows, D, device="cuda", dtype=torch.bfloat16), \
+        torch.empty(D, device="cuda")
+    run(k, "vqa_layernorm_bwd", dy, x, mu, rs, g, dres, dx, dx16, dg, db, ws, rows, D, None, dsum)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dx, xr.grad + dres, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dx16.float(), xr.grad.to(torch.bfloat16).float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dsum, xr.grad.sum(0), rtol=1e-4, atol=1e-3)
 
 
 def attn_ref(q, kk, v, scale, bias, mask, mult=None):
