@@ -184,6 +184,24 @@ def main():
     kflop = 2.0 * wg_call.desc.m * wg_call.desc.n * wg_call.desc.k
     k_tflops = kflop / kdur / 1e12
 
+    # north_star's SGA figure: MFMA utilisation of the SGA blocks' GEMM-shaped launches (the
+    # linear layers of MHAtt / FFN and the attention cores, forward and backward): their FLOP
+    # per step over the sum of their launch times, each replayed alone between HIP events
+    # (no neighbour overlap, so slightly optimistic against the in-graph schedule)
+    sga_calls = [c for c in eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
+                 if c.name in ("vqa_gemm", "vqa_gemm_pair", "vqa_attn_fwd", "vqa_attn_bwd")]
+
+    def call_flop(c):
+        if c.name == "vqa_gemm":
+            return 2.0 * c.desc.m * c.desc.n * c.desc.k * max(1, c.desc.batch)
+        if c.name == "vqa_gemm_pair":
+            return sum(2.0 * d.m * d.n * d.k for d in c.desc)
+        d = c.desc
+        return (4.0 if c.name == "vqa_attn_fwd" else 8.0) * d.batch * d.heads * d.lq * d.lk * d.dh
+    sga_flop = sum(call_flop(c) for c in sga_calls)
+    sga_time = sum(time_kernel(c, 10, stream) for c in sga_calls)
+    sga_tflops = sga_flop / sga_time / 1e12
+
     pairs = world * B * args.steps
     value = pairs / dt
     out = {
@@ -207,6 +225,9 @@ def main():
                           "traffic": (round(pmc["convT_dW"]["traffic_bytes"]) if "convT_dW" in pmc else None),
                           "kernel_avg_us": round(kdur * 1e6, 2), "flop_per_launch": kflop,
                           "step_mfma_frac": round(value / world * FLOP_PER_PAIR / (MFMA_PEAK_TFLOPS * 1e12), 4)},
+        "sga_mfma": {"launches": len(sga_calls), "flop_per_step": sga_flop, "kernel_us_per_step": round(sga_time * 1e6, 1),
+                     "achieved": round(sga_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(sga_tflops / MFMA_PEAK_TFLOPS, 4), "target_frac": 0.40},
         "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
