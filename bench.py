@@ -95,7 +95,8 @@ def main():
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)       # identical init on every rank
     pipe = not args.no_pipeline
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev,
-                               warmup=10, total=100000, dropout=0.1, seed=rank, pipeline=pipe)
+                               warmup=10, total=100000, dropout=0.1, seed=rank, pipeline=pipe,
+                               t5_dw_group=None if world == 1 else 4)
     del sd
     pool = []
     for i in range(4):

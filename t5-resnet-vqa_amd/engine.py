@@ -28,6 +28,7 @@ Design (MI355X-first, not a translation of eager PyTorch):
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 
 import numpy as np
@@ -87,7 +88,8 @@ def _gemm_key(d):
 class VQAEngine:
     def __init__(self, state_dict, vision="resnet50", batch=64, seq_len=32, image_size=224, device="cuda:0",
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
-                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0, pipeline=False):
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0, pipeline=False,
+                 t5_dw_group=None):
         L.load()
         # pipeline: the frozen ResNet (no trainable input) of the NEXT batch runs on its own
         # stream beside this step's T5 / SGA / backward / optimizer (see train_step)
@@ -101,7 +103,14 @@ class VQAEngine:
         self.betas, self.eps, self.wd = betas, eps, weight_decay
         self.grad_scale = grad_scale
         self.group_lr = {}                # per-group LR overrides (trainer optimizer_kwargs)
-        self.pair_bwd = True              # dX + dW of a layer as one paired GEMM launch
+        # dX + dW of a layer as one paired GEMM launch (VQA_PAIR_BWD=0: separate launches, A/B only)
+        self.pair_bwd = os.environ.get("VQA_PAIR_BWD", "1") != "0"
+        # T5 weight gradients batched over groups of this many layers (1: paired per layer).
+        # Single GPU: all 12 in one batch per weight (measured 6.88 vs 7.13 ms per step paired);
+        # DP passes a smaller group so the T5 gradient buckets still become final, and get
+        # all-reduced, while the rest of the backward runs.  VQA_T5_DW_GROUP overrides (A/B).
+        g = os.environ.get("VQA_T5_DW_GROUP")
+        self.t5_dw_group = int(g) if g else (int(t5_dw_group) if t5_dw_group else S.T5_LAYERS)
         self.T = batch * seq_len
         self.lay = ParamLayout(vision, answer_spaces, num_blocks)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
@@ -264,13 +273,17 @@ class VQAEngine:
         nl = S.T5_LAYERS
         self.PB = t((S.T5_HEADS, Lq, Lq))
         self.HS = [t((T, D)) for _ in range(nl + 1)]
-        self.N0 = [t((T, D), BF16) for _ in range(nl)]
+        # GEMM inputs the weight gradients read, stacked in backward order (slot = 11 - layer) so
+        # a group of consecutive layers' dW is one batched launch with constant strides
+        self.N0S, self.OS, self.N1S = t((nl, T, D), BF16), t((nl, T, D), BF16), t((nl, T, D), BF16)
+        self.FFS = t((nl, T, S.T5_DFF), BF16)
+        self.N0 = [self.N0S[nl - 1 - i] for i in range(nl)]
         self.QKV = [t((T, 3 * D), BF16) for _ in range(nl)]
         self.PT = [t((B, S.T5_HEADS, Lq, Lq)) for _ in range(nl)]
-        self.O = [t((T, D), BF16) for _ in range(nl)]
+        self.O = [self.OS[nl - 1 - i] for i in range(nl)]
         self.HM = [t((T, D)) for _ in range(nl)]
-        self.N1 = [t((T, D), BF16) for _ in range(nl)]
-        self.FF = [t((T, S.T5_DFF), BF16) for _ in range(nl)]
+        self.N1 = [self.N1S[nl - 1 - i] for i in range(nl)]
+        self.FF = [self.FFS[nl - 1 - i] for i in range(nl)]
         self.R0 = [t(T) for _ in range(nl)]
         self.R1 = [t(T) for _ in range(nl)]
         self.RF = t(T)
@@ -661,8 +674,12 @@ class VQAEngine:
         self._bsplit.append(len(b))
         # T5 encoder backward.  dH32 is the gradient of the residual stream h_i; dH16 the
         # dropout-masked gradient of the FF branch that produced it (T5LayerFF :140).
-        g = lambda nm, shape: self._gbuf(nm, shape)
-        dH16 = [g(f"t5.{i}.dH", (T, D)) for i in range(S.T5_LAYERS)]     # FF-branch grad of layer i
+        nl = S.T5_LAYERS
+        # per-layer bf16 gradients the weight gradients read, stacked like the inputs (slot 11 - i)
+        self.dH16S, self.dHMS = self._t((nl, T, D), BF16), self._t((nl, T, D), BF16)
+        self.dFS, self.dQKVS = self._t((nl, T, S.T5_DFF), BF16), self._t((nl, T, 3 * D), BF16)
+        dH16 = [self.dH16S[nl - 1 - i] for i in range(nl)]               # FF-branch grad of layer i
+        G = self.t5_dw_group
         kp = []
         ws = self._norm_ws()
         self._call(b, "vqa_rmsnorm_bwd", self.dTXT, self.HS[-1], self.RF, self.p32["t5.final_ln"], None, self.dH32,
@@ -671,17 +688,21 @@ class VQAEngine:
                    extra=kp + [self.RNG])
         self._defer(ws, nparts, D, D, self.g32["t5.final_ln"])
         mark("t5.final_ln")
-        for i in reversed(range(S.T5_LAYERS)):
-            dF, dHM, dQKV = g(f"t5.{i}.dF", (T, S.T5_DFF)), g(f"t5.{i}.dHM", (T, D)), g(f"t5.{i}.dQKV", (T, 3 * D))
-            self._dxdw(b, dH16[i], self.FF[i], f"t5.{i}.wo", T, out16=dF, mask16=self.FF[i], alpha=ks)
-            self._dxdw(b, dF, self.N1[i], f"t5.{i}.wi", T, out32=self.dC32)
+        # G > 1: the layers' input gradients chain alone and every G layers ONE batched launch
+        # per weight (wo, wi, o, qkv) computes the group's weight gradients (4 x G GEMMs of
+        # K = 2048 as 4 launches); G == 1: each layer's dX + dW as paired launches
+        dxdw = self._dxdw if G == 1 else (lambda lst, dy, x, w, rows, **kw: self._dx(lst, dy, w, rows, **kw))
+        for i in reversed(range(nl)):
+            dF, dHM, dQKV = self.dFS[nl - 1 - i], self.dHMS[nl - 1 - i], self.dQKVS[nl - 1 - i]
+            dxdw(b, dH16[i], self.FF[i], f"t5.{i}.wo", T, out16=dF, mask16=self.FF[i], alpha=ks)
+            dxdw(b, dF, self.N1[i], f"t5.{i}.wi", T, out32=self.dC32)
             kp = []
             ws = self._norm_ws()
             self._call(b, "vqa_rmsnorm_bwd", self.dC32, self.HM[i], self.R1[i], self.p32[f"t5.{i}.ln1"], self.dH32,
                        self.dHM32, dHM, None, 0.0, ws, T, D,
                        None, None, self._dptr(t5_site(i, 1), kp), extra=kp + [self.RNG])
             self._defer(ws, nparts, D, D, self.g32[f"t5.{i}.ln1"])
-            self._dxdw(b, dHM, self.O[i], f"t5.{i}.o_w", T, out16=self.dO16)
+            dxdw(b, dHM, self.O[i], f"t5.{i}.o_w", T, out16=self.dO16)
             q = self.QKV[i]
             dq = dQKV
             self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
@@ -689,7 +710,7 @@ class VQAEngine:
                        lk=Lq, dh=S.T5_DKV, scale=1.0, dout=self.dO16, lddo=D, dq=dq, lddq=3 * D,
                        dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dSB[i],
                        drop=t5_site(i, 0))
-            self._dxdw(b, dq, self.N0[i], f"t5.{i}.qkv_w", T, out32=self.dC32)
+            dxdw(b, dq, self.N0[i], f"t5.{i}.qkv_w", T, out32=self.dC32)
             # layer 0: dH32 becomes the embedding gradient (masked by the embedding dropout :725);
             # otherwise dH16 is the FF branch gradient of layer i-1
             kp = []
@@ -700,7 +721,12 @@ class VQAEngine:
                        self.dH32, dH16[i - 1] if i > 0 else None, None, 0.0, ws, T, D,
                        None, d32, d16, extra=kp + [self.RNG])
             self._defer(ws, nparts, D, D, self.g32[f"t5.{i}.ln0"])
-            mark(f"t5.{i}.ln1")
+            done = nl - i                                   # layers finished so far (11 .. i)
+            if G == 1:
+                mark(f"t5.{i}.ln1")
+            elif done % G == 0 or i == 0:
+                self._t5_group_dw(b, i + (done - 1) % G, i)
+                mark(f"t5.{i}.ln1")
         # the relative-position bias is shared by all 12 layers: dPB = sum over (layer, sample) of dS,
         # one fixed-order reduction after the last layer instead of one per layer
         self._call(b, "vqa_batch_sum", self.dSB, S.T5_LAYERS * B, S.T5_HEADS * Lq * Lq, self.dPB, 0.0)
@@ -711,6 +737,22 @@ class VQAEngine:
         # embedding rows last (DP replaces this call by an all-gather of (id, dH row) pairs)
         self._call(b, "vqa_embedding_bwd", self.IDS, self.dH32, self.g32["t5.embed"], T, D, S.T5_VOCAB, self.WS_EMB)
         self.emb_call = b[-1]
+
+    def _t5_group_dw(self, lst, i_hi, i_lo):
+        """Weight gradients of T5 layers i_hi >= .. >= i_lo: per weight one launch batched over
+        the layers (stack slot 11 - i, consecutive gradient segments at a constant stride)."""
+        nl, T = S.T5_LAYERS, self.T
+        cnt, s0 = i_hi - i_lo + 1, nl - 1 - i_hi
+        for w, dys, xs in (("wo", self.dH16S, self.FFS), ("wi", self.dFS, self.N1S), ("o_w", self.dHMS, self.OS),
+                           ("qkv_w", self.dQKVS, self.N0S)):
+            nout, kin = self.g32[f"t5.{i_hi}.{w}"].shape
+            segs = [self.lay[f"t5.{i}.{w}"] for i in range(i_hi, i_lo - 1, -1)]
+            lstride = segs[1].offset - segs[0].offset if cnt > 1 else 0
+            assert all(b.offset - a.offset == lstride for a, b in zip(segs, segs[1:])), w
+            self._gemm(lst, ops.addr(dys, s0 * T * nout), ops.addr(xs, s0 * T * kin), nout, kin, T, lda=nout,
+                       ldb=kin, a_trans=True, b_trans=True, c32=self.g32[f"t5.{i_hi}.{w}"], ldc32=kin, batch=cnt,
+                       stride_a=T * nout, stride_b=T * kin, stride_c32=lstride, keep=(dys, xs, self.G32))
+            lst[-1].side = True
 
     # ------------------------------------------------------------------ optimizer plan
     def _plan_optimizer(self):

@@ -148,3 +148,20 @@ def test_pipelined_resnet_step_is_bit_identical(cuda, pkg):
         torch.cuda.synchronize()
         assert got == losses, (graph, got, losses)
         assert torch.equal(eng.P32, ref.P32), graph
+
+
+def test_t5_weight_gradient_grouping_is_bit_identical(cuda, pkg):
+    """The T5 weight gradients as per-layer paired launches (group 1), batched over groups
+    of 4 layers (the DP default) and over all 12 layers (single GPU) give the same bits:
+    the same dot products in the same 64-deep K order, only scheduled differently."""
+    import torch
+    B, L, H = 2, 32, 64
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    nb = pkg.synthetic.make_batch(B, L, H, seed=3)
+    grads = []
+    for g in (1, 4, 12):
+        eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=20, dropout=0.1, seed=1,
+                                   t5_dw_group=g)
+        eng.forward_backward(nb)
+        grads.append(eng.G32.clone())
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
