@@ -111,6 +111,8 @@ class VQAEngine:
         # all-reduced, while the rest of the backward runs.  VQA_T5_DW_GROUP overrides (A/B).
         g = os.environ.get("VQA_T5_DW_GROUP")
         self.t5_dw_group = int(g) if g else (int(t5_dw_group) if t5_dw_group else S.T5_LAYERS)
+        # SGA blocks' q2 / m2 / fc1 / fc2 weight gradients batched over the blocks
+        self.sga_dw_batch = os.environ.get("VQA_SGA_DW_BATCH", "1") != "0"
         self.T = batch * seq_len
         self.lay = ParamLayout(vision, answer_spaces, num_blocks)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
@@ -292,6 +294,9 @@ class VQAEngine:
         # q|k|v of block n in columns [n*2304, (n+1)*2304) of QKV1A, merge in/out in [n]
         self.QKV1A = t((T, NB * 3 * D), BF16)
         self.O1A, self.S1A = t((NB, T, D), BF16), t((NB, T, D))
+        # inputs of the blocks' q2 / m2 / fc1 / fc2 weight gradients, stacked in backward order
+        # (slot NB-1-n) for the batched dW launches
+        self.X1hS, self.O2S, self.X2hS, self.FFhS = (t((NB, T, D), BF16) for _ in range(4))
         self.sga = []
         for n in range(NB):
             ly = V if n == 0 else T
@@ -299,10 +304,10 @@ class VQAEngine:
             self.sga.append(dict(
                 ly=ly, lk=lk,
                 P1=t((B, S.SGA_HEADS, Lq, Lq)), O1=self.O1A[n], S1=self.S1A[n],
-                X1=t((T, D)), X1h=t((T, D), BF16), MU1=t(T), RS1=t(T),
-                Q2=t((T, D), BF16), KV2=t((ly, 2 * D), BF16), P2=t((B, S.SGA_HEADS, Lq, lk)), O2=t((T, D), BF16),
-                S2=t((T, D)), X2=t((T, D)), X2h=t((T, D), BF16), MU2=t(T), RS2=t(T),
-                FFh=t((T, D), BF16), S3=t((T, D)), OUT=t((T, D)), OUTh=t((T, D), BF16), MU3=t(T), RS3=t(T)))
+                X1=t((T, D)), X1h=self.X1hS[NB - 1 - n], MU1=t(T), RS1=t(T),
+                Q2=t((T, D), BF16), KV2=t((ly, 2 * D), BF16), P2=t((B, S.SGA_HEADS, Lq, lk)),
+                O2=self.O2S[NB - 1 - n], S2=t((T, D)), X2=t((T, D)), X2h=self.X2hS[NB - 1 - n], MU2=t(T), RS2=t(T),
+                FFh=self.FFhS[NB - 1 - n], S3=t((T, D)), OUT=t((T, D)), OUTh=t((T, D), BF16), MU3=t(T), RS3=t(T)))
         # head
         self.ATT, self.POOLED = t((B, Lq)), t((B, D))
         self.LOGP, self.NLL, self.LOSS = t((B, self.A)), t(B), t(1)
@@ -450,6 +455,14 @@ class VQAEngine:
             self._gbufs[name] = self._t(shape, BF16)
         return self._gbufs[name]
 
+    def _bias_colsum(self, lst, dy16, rows, bname):
+        """A Linear bias gradient = column sums of its bf16 output gradient (deferred)."""
+        lib = L.load()
+        n = dy16.shape[-1]
+        ws = self._t(lib.vqa_colsum_workspace_floats(rows, n))
+        self._call(lst, "vqa_colsum", dy16, 1, rows, n, n, None, 0.0, ws)
+        self._defer(ws, lib.vqa_colsum_parts(rows), n, n, self.g32[bname])
+
     def _dw(self, lst, dy16, x16, wname, rows, bias_from=None, bias_bf16=True):
         """dW[n, k] = dY[rows, n]^T X[rows, k]; optional bias grad = colsum(dY).
         Tagged `side`: nothing on the dX chain reads them, so the step graph runs
@@ -579,6 +592,12 @@ class VQAEngine:
         mark("pool_b")
         sc = 1.0 / math.sqrt(S.SGA_DHEAD)
         ks = self.drop_scale if self.p_drop > 0.0 else 1.0      # relu-mask dX: kept elements carry 1/(1-p)
+        # the blocks' q2 / m2 / fc1 / fc2 weight gradients (768 x 768, K = 2048 each) are left
+        # out of the sequential block chain and computed after it as one launch per weight
+        # batched over the blocks (the block chain then runs its input gradients alone)
+        self.dA3S, self.dBS, self.dA2S, self.dQS = (self._t((NB, T, D), BF16) for _ in range(4))
+        batched = self.sga_dw_batch
+        dxdw = (lambda lst, dy, x, w, rows, **kw: self._dx(lst, dy, w, rows, **kw)) if batched else self._dxdw
         for n in reversed(range(NB)):
             s, p = self.sga[n], f"sga{n}."
             dy = self.dY[n & 1]
@@ -586,8 +605,8 @@ class VQAEngine:
             # every bf16 gradient a weight-gradient GEMM reads gets its own buffer, so the dW
             # GEMMs can trail the dX chain on another stream without write-after-read hazards
             g = lambda nm, shape: self._gbuf(f"{p}{nm}", shape)
-            dA3, dA2 = g("dA3", (T, D)), g("dA2", (T, D))
-            dB, dQ = g("dB", (T, D)), g("dQ", (T, D))
+            slot = NB - 1 - n
+            dA3, dA2, dB, dQ = self.dA3S[slot], self.dA2S[slot], self.dBS[slot], self.dQS[slot]
             dKV = g("dKV", (s["ly"], 2 * D))
             # norm3 + FFN: dA32 = grad of x + dropout3(ffn(x)) (the residual), dA16 = its dropout3 branch;
             # the fc2 bias gradient (column sums of the branch) is fused into the LayerNorm backward
@@ -598,8 +617,12 @@ class VQAEngine:
                        self._dptr(sga_site(n, 5), kp), self.g32[p + "fc2_b"], extra=kp + [self.RNG])
             for j, nm in enumerate(("ln3_g", "ln3_b", "fc2_b")):      # ws = [parts][dgamma | dbeta | dsum]
                 self._defer(ws, nparts, 3 * D, D, self.g32[p + nm], offset=j * D)
-            self._dxdw(b, dA3, s["FFh"], p + "fc2_w", T, out16=dB, mask16=s["FFh"], alpha=ks)
-            self._dxdw(b, dB, s["X2h"], p + "fc1_w", T, bias_from=dB, out32=self.dC32, res32=self.dA32)
+            dxdw(b, dA3, s["FFh"], p + "fc2_w", T, out16=dB, mask16=s["FFh"], alpha=ks)
+            if batched:
+                self._dx(b, dB, p + "fc1_w", T, out32=self.dC32, res32=self.dA32)
+                self._bias_colsum(b, dB, T, p + "fc1_b")
+            else:
+                self._dxdw(b, dB, s["X2h"], p + "fc1_w", T, bias_from=dB, out32=self.dC32, res32=self.dA32)
             # norm2 + cross attention (q from x, k/v from y)
             kp = []
             ws = self._norm_ws()
@@ -608,13 +631,17 @@ class VQAEngine:
                        self._dptr(sga_site(n, 3), kp), self.g32[p + "m2_b"], extra=kp + [self.RNG])
             for j, nm in enumerate(("ln2_g", "ln2_b", "m2_b")):      # ws = [parts][dgamma | dbeta | dsum]
                 self._defer(ws, nparts, 3 * D, D, self.g32[p + nm], offset=j * D)
-            self._dxdw(b, dA2, s["O2"], p + "m2_w", T, out16=self.dO16)
+            dxdw(b, dA2, s["O2"], p + "m2_w", T, out16=self.dO16)
             kv = s["KV2"]
             self._attn(b, "vqa_attn_bwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
                        p=s["P2"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=s["lk"], dh=S.SGA_DHEAD, scale=sc,
                        dout=self.dO16, lddo=D, dq=dQ, lddq=D, dk=dKV, lddk=2 * D,
                        dv=ops.addr(dKV, D), lddv=2 * D, drop=sga_site(n, 2))
-            self._dxdw(b, dQ, s["X1h"], p + "q2_w", T, bias_from=dQ, out32=self.dC32, res32=self.dA32)
+            if batched:
+                self._dx(b, dQ, p + "q2_w", T, out32=self.dC32, res32=self.dA32)
+                self._bias_colsum(b, dQ, T, p + "q2_b")
+            else:
+                self._dxdw(b, dQ, s["X1h"], p + "q2_w", T, bias_from=dQ, out32=self.dC32, res32=self.dA32)
             if n == 0:
                 self._dxdw(b, dKV, y16, p + "kv2_w", s["ly"], bias_from=dKV, out32=self.dVIS32, out16=self.dVIS16)
             else:
@@ -628,7 +655,18 @@ class VQAEngine:
                        ws, T, D, self._dptr(sga_site(n, 1), kp), self.g32[p + "m1_b"], extra=kp + [self.RNG])
             for j, nm in enumerate(("ln1_g", "ln1_b", "m1_b")):      # ws = [parts][dgamma | dbeta | dsum]
                 self._defer(ws, nparts, 3 * D, D, self.g32[p + nm], offset=j * D)
-            mark(f"sga{n}.ln3_b")
+            if not batched:
+                mark(f"sga{n}.ln3_b")
+        if batched:
+            for w, dys, xs in (("fc2_w", self.dA3S, self.FFhS), ("fc1_w", self.dBS, self.X2hS),
+                               ("m2_w", self.dA2S, self.O2S), ("q2_w", self.dQS, self.X1hS)):
+                segs = [self.lay[f"sga{n}.{w}"] for n in reversed(range(NB))]
+                lstride = segs[1].offset - segs[0].offset if NB > 1 else 0
+                assert all(b_.offset - a_.offset == lstride for a_, b_ in zip(segs, segs[1:])), w
+                self._gemm(b, dys, xs, D, D, T, lda=D, ldb=D, a_trans=True, b_trans=True,
+                           c32=self.g32[f"sga{NB - 1}.{w}"], ldc32=D, batch=NB, stride_a=T * D, stride_b=T * D,
+                           stride_c32=lstride, keep=(self.G32,))
+                b[-1].side = True
         # the blocks' self-attention halves, batched: merge dX / dW (batch NB), the
         # attentions, then ONE q|k|v dX GEMM over K = NB * 2304 (it also sums the blocks'
         # text gradients, plus the norm1 residual sum as res32) paired with ONE q|k|v dW GEMM

@@ -38,9 +38,9 @@ def _spawn(fn, world, *args):
 def test_plan_buckets_cover_prefix(pkg):
     lay = pkg.layout.ParamLayout("resnet50")
     emb = lay["t5.embed"].offset
-    # marks as the engine emits them: head, 3 SGA blocks, their batched self-attention halves,
-    # scaler, final LN, 12 layers, relbias
-    names = ["pool_b"] + [f"sga{n}.ln3_b" for n in (2, 1, 0)] + ["sga2.m1_b", "scaler_b", "t5.final_ln"] + \
+    # marks as the engine emits them (DP: T5 weight gradients in groups): head, the SGA
+    # blocks, scaler, final LN, T5 layers, relbias
+    names = ["pool_b", "sga2.m1_b", "scaler_b", "t5.final_ln"] + \
         [f"t5.{i}.ln1" for i in reversed(range(12))] + ["t5.relbias"]
     marks = [(10 * (i + 1), lay[n].offset + (lay[n].numel + 63) // 64 * 64) for i, n in enumerate(names)]
     bks = pkg.dp.plan_buckets(marks, emb, 24 << 20)

@@ -33,11 +33,13 @@ def test_dp_world1_matches_single_gpu(pg, pkg, graph):
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
     nb = pkg.synthetic.make_batch(B, L, H, seed=1)
     e1 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20)
-    e2 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20)
+    # the DP engine batches the T5 weight gradients in groups of 4 layers (bench.py), the
+    # single-GPU one over all 12: same bits, different bucket boundaries
+    e2 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, t5_dw_group=4)
     e1.load_batch(nb)
     e2.load_batch(nb)
     step = pkg.dp.DataParallelStep(e2, bucket_mb=8, use_graph=graph)
-    assert len(step.buckets) > 5
+    assert len(step.buckets) >= 5
     for _ in range(3):
         e1.train_step()
         step.step()

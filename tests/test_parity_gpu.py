@@ -150,16 +150,18 @@ def test_pipelined_resnet_step_is_bit_identical(cuda, pkg):
         assert torch.equal(eng.P32, ref.P32), graph
 
 
-def test_t5_weight_gradient_grouping_is_bit_identical(cuda, pkg):
+def test_t5_weight_gradient_grouping_is_bit_identical(cuda, pkg, monkeypatch):
     """The T5 weight gradients as per-layer paired launches (group 1), batched over groups
-    of 4 layers (the DP default) and over all 12 layers (single GPU) give the same bits:
+    of 4 layers (the DP default) and over all 12 layers (single GPU), and the SGA blocks'
+    weight gradients paired per block or batched over the blocks, give the same bits:
     the same dot products in the same 64-deep K order, only scheduled differently."""
     import torch
     B, L, H = 2, 32, 64
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
     nb = pkg.synthetic.make_batch(B, L, H, seed=3)
     grads = []
-    for g in (1, 4, 12):
+    for g, sga in ((1, "0"), (4, "1"), (12, "1")):
+        monkeypatch.setenv("VQA_SGA_DW_BATCH", sga)
         eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=20, dropout=0.1, seed=1,
                                    t5_dw_group=g)
         eng.forward_backward(nb)
