@@ -491,6 +491,9 @@ class VQAEngine:
         g = ops.conv_geom(B, fh, fh, cin, fh, fh, 3, 3, 1, 1)
         self._gemm(f, self.F4, self.p16["scaler_w"], self.V_TOK, D, 9 * cin, lda=9 * cin, ldb=9 * cin, ga=g,
                    c32=self.VIS32, ldc32=D, c16=self.VIS16, ldc16=D, bias=self.p32["scaler_b"])
+        # SGA block 0's key/value projection reads only the vision tokens: it runs here, on the
+        # vision branch beside the T5 encoder, instead of on the chain after it
+        self._linear(f, self.VIS16, "sga0.kv2_w", self.sga[0]["ly"], out16=self.sga[0]["KV2"])
         # T5 encoder (independent of the vision branch until the SGA blocks)
         self._fsplit.append(len(f))
         kp = []
@@ -545,7 +548,8 @@ class VQAEngine:
         for n in range(NB):
             s, p = self.sga[n], f"sga{n}."
             self._linear(f, s["X1h"], p + "q2_w", T, out16=s["Q2"])
-            self._linear(f, y16, p + "kv2_w", s["ly"], out16=s["KV2"])
+            if n > 0:
+                self._linear(f, y16, p + "kv2_w", s["ly"], out16=s["KV2"])
             kv = s["KV2"]
             self._attn(f, "vqa_attn_fwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
                        o=s["O2"], ldo=D, p=s["P2"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=s["lk"], dh=S.SGA_DHEAD,
