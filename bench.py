@@ -189,7 +189,7 @@ def main():
     # linear layers of MHAtt / FFN and the attention cores, forward and backward): their FLOP
     # per step over the sum of their launch times, each replayed alone between HIP events
     # (no neighbour overlap, so slightly optimistic against the in-graph schedule)
-    sga_calls = [c for c in eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
+    sga_calls = [c for c in eng.sga_vision_calls + eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
                  if c.name in ("vqa_gemm", "vqa_gemm_pair", "vqa_attn_fwd", "vqa_attn_bwd")]
 
     def call_flop(c):

@@ -178,74 +178,92 @@ __global__ __launch_bounds__(256) void embedding_zero_rows_kernel(long long* __r
 }
 
 // Deterministic dense embedding gradient (nn.Embedding sparse=False), no atomics:
-//   1. one workgroup bitonic-sorts the keys (id << 16 | position) in LDS, which
-//      groups equal ids with their positions in token order, and finds each
-//      id-run's end with a max-scan of the run starts (no serial run walks);
+//   1. one workgroup bitonic-sorts the keys (id << 16 | position), which groups
+//      equal ids with their positions in token order, and finds each id-run's
+//      end by a binary search of the sorted ids from the run start;
 //   2. one workgroup per (run start, column slab) sums the run's dh rows in
 //      that fixed order and writes the table row once.
 // Bit-identical run to run (DP ranks stay in lockstep, graph replay == eager).
 // ws: [0, T) sorted positions, [T, 2T) sorted ids (clamped), [2T, 3T) run end
 // (valid at run starts).
+// Bitonic network over n = max(pow2 >= tokens, 1024) keys, E = n/1024 per thread
+// (element i = q*1024 + thread): stages with j < 64 exchange inside a wave by
+// shuffles, 64 <= j < 1024 through LDS, j >= 1024 between a thread's own slots.
+// Run ends by binary search of the sorted ids (one per run start).
+__device__ __forceinline__ unsigned long long shfl_xor64(unsigned long long v, int m) {
+  const int lo = __shfl_xor((int)(unsigned)(v & 0xffffffffu), m, 64);
+  const int hi = __shfl_xor((int)(unsigned)(v >> 32), m, 64);
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+template <int E>
 __global__ __launch_bounds__(1024) void embedding_sort_kernel(const long long* __restrict__ ids, int tokens, int vocab,
                                                               int* __restrict__ ws) {
   extern __shared__ unsigned long long key[];
-  int n = 1;
-  while (n < tokens) n <<= 1;
-  for (int t = threadIdx.x; t < n; t += blockDim.x) {
-    if (t < tokens) {
-      long long id = ids[t];
-      id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
-      key[t] = ((unsigned long long)id << 16) | (unsigned long long)t;
-    } else {
-      key[t] = ~0ull;
-    }
+  constexpr int n = E * 1024;
+  const int t = threadIdx.x;
+  unsigned long long v[E];
+#pragma unroll
+  for (int q = 0; q < E; ++q) {
+    const int i = q * 1024 + t;
+    long long id = ids[min(i, tokens - 1)];
+    id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+    v[q] = i < tokens ? (((unsigned long long)id << 16) | (unsigned long long)i) : ~0ull;
   }
-  __syncthreads();
   for (int k = 2; k <= n; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int p = i ^ j;
-        if (p > i) {
-          const unsigned long long a = key[i], b = key[p];
+      if (j >= 1024) {                                  // partner: another slot of this thread
+        const int qj = j >> 10;
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+          if (q & qj) continue;
+          const int i = q * 1024 + t;
           const bool up = (i & k) == 0;
-          if ((a > b) == up) { key[i] = b; key[p] = a; }
+          const unsigned long long a = v[q], c = v[q | qj];
+          v[q] = up ? (a < c ? a : c) : (a < c ? c : a);
+          v[q | qj] = up ? (a < c ? c : a) : (a < c ? a : c);
+        }
+      } else if (j >= 64) {                             // partner: another wave, same slot
+#pragma unroll
+        for (int q = 0; q < E; ++q) key[q * 1024 + t] = v[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+          const int i = q * 1024 + t;
+          const unsigned long long c = key[i ^ j];
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          v[q] = keep_min ? (v[q] < c ? v[q] : c) : (v[q] < c ? c : v[q]);
+        }
+        __syncthreads();
+      } else {                                          // partner: a lane of this wave
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+          const int i = q * 1024 + t;
+          const unsigned long long c = shfl_xor64(v[q], j);
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          v[q] = keep_min ? (v[q] < c ? v[q] : c) : (v[q] < c ? c : v[q]);
         }
       }
-      __syncthreads();
     }
   }
-  // run starts: flag[t] = t if id(t) != id(t-1) else 0 (t = 0 always starts)
-  constexpr int MAXT = 8192 / 1024;
-  int st[MAXT];
 #pragma unroll
-  for (int q = 0; q < MAXT; ++q) {
-    const int t = threadIdx.x + q * 1024;
-    st[q] = 0;
-    if (t < tokens) {
-      const unsigned long long kt = key[t];
-      ws[t] = (int)(kt & 0xffff);
-      ws[tokens + t] = (int)(kt >> 16);
-      st[q] = (t == 0 || (key[t - 1] >> 16) != (kt >> 16)) ? t : 0;
-    }
-  }
-  __syncthreads();                                      // keys are dead from here: reuse LDS as 2 int arrays
-  int* s0 = reinterpret_cast<int*>(key);
-  int* s1 = s0 + n;
-#pragma unroll
-  for (int q = 0; q < MAXT; ++q) {
-    const int t = threadIdx.x + q * 1024;
-    if (t < n) s0[t] = st[q];
-  }
+  for (int q = 0; q < E; ++q) key[q * 1024 + t] = v[q];
   __syncthreads();
-  // inclusive max-scan: start(t) = the last run start <= t
-  for (int off = 1; off < n; off <<= 1) {
-    for (int t = threadIdx.x; t < n; t += blockDim.x) s1[t] = t >= off ? max(s0[t], s0[t - off]) : s0[t];
-    __syncthreads();
-    int* tmp = s0; s0 = s1; s1 = tmp;
-  }
-  for (int t = threadIdx.x; t < tokens; t += blockDim.x) {
-    const int a = s0[t];
-    if (t == tokens - 1 || s0[t + 1] != a) ws[2 * tokens + a] = t + 1;      // t is the last of its run
+#pragma unroll
+  for (int q = 0; q < E; ++q) {
+    const int i = q * 1024 + t;
+    if (i >= tokens) continue;
+    const unsigned long long kt = v[q];
+    const unsigned id = (unsigned)(kt >> 16);
+    ws[i] = (int)(kt & 0xffff);
+    ws[tokens + i] = (int)id;
+    if (i == 0 || (unsigned)(key[i - 1] >> 16) != id) {  // run start: end = first slot with a larger id
+      int lo = i + 1, hi = tokens;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((unsigned)(key[mid] >> 16) == id) lo = mid + 1; else hi = mid;
+      }
+      ws[2 * tokens + i] = lo;
+    }
   }
 }
 
@@ -426,10 +444,15 @@ extern "C" int vqa_embedding_bwd(const long long* ids, const float* dh, float* d
   // keys hold the position in 16 bits and the padded sort buffer lives in LDS (<= 64 KiB)
   VQA_REQUIRE(ids && dh && dtable && ws && tokens > 0 && tokens <= 8192 && d % 4 == 0,
               "vqa_embedding_bwd: bad arguments");
-  int n = 1;
-  while (n < tokens) n <<= 1;
-  hipLaunchKernelGGL(embedding_sort_kernel, dim3(1), dim3(1024), n * sizeof(unsigned long long), s, ids, tokens, vocab,
-                     ws);
+  const size_t lds = (tokens <= 1024 ? 1024 : tokens <= 2048 ? 2048 : tokens <= 4096 ? 4096 : 8192) * sizeof(unsigned long long);
+  if (tokens <= 1024)
+    hipLaunchKernelGGL(embedding_sort_kernel<1>, dim3(1), dim3(1024), lds, s, ids, tokens, vocab, ws);
+  else if (tokens <= 2048)
+    hipLaunchKernelGGL(embedding_sort_kernel<2>, dim3(1), dim3(1024), lds, s, ids, tokens, vocab, ws);
+  else if (tokens <= 4096)
+    hipLaunchKernelGGL(embedding_sort_kernel<4>, dim3(1), dim3(1024), lds, s, ids, tokens, vocab, ws);
+  else
+    hipLaunchKernelGGL(embedding_sort_kernel<8>, dim3(1), dim3(1024), lds, s, ids, tokens, vocab, ws);
   if (int rc = vqa::check_launch("vqa_embedding_bwd/sort")) return rc;
   hipLaunchKernelGGL(embedding_bwd_kernel, dim3(tokens, vqa::cdiv(d, 4 * EMB_CL)), dim3(EMB_RL * EMB_CL), 0, s, dh,
                      dtable, ws, tokens, d);

@@ -494,6 +494,7 @@ class VQAEngine:
         # SGA block 0's key/value projection reads only the vision tokens: it runs here, on the
         # vision branch beside the T5 encoder, instead of on the chain after it
         self._linear(f, self.VIS16, "sga0.kv2_w", self.sga[0]["ly"], out16=self.sga[0]["KV2"])
+        self.sga_vision_calls = [f[-1]]                    # SGA work outside the fusion segment (bench)
         # T5 encoder (independent of the vision branch until the SGA blocks)
         self._fsplit.append(len(f))
         kp = []
