@@ -163,7 +163,7 @@ def main():
     # (tools/pmc_traffic.py) when present.
     from vqa_amd import lib as VL
     stream = torch.cuda.current_stream(dev)
-    adam_call = eng.opt_calls[-1]
+    adam_call = eng.adam_full                      # the whole-arena pass (in-step it runs as ranges)
     assert adam_call.name == "vqa_adamw_amsgrad"
     n_par = eng.lay.total
     adam_bytes = 38.0 * n_par

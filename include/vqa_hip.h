@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 6
+#define VQA_ABI_VERSION 7
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -275,9 +275,13 @@ int vqa_head_workspace_floats(int batch, int seq, int d, int answers);
 /* ------------------------------------------------------------- optimiser ---
  * clip_grad_norm_(1.0) + AdamW(amsgrad) + linear warmup/decay schedule
  * (faster_rcnn_vqa_trainer.py:399-404, :231-287; TF optimization.py:101-107),
- * device-resident so a whole step is graph-capturable.  `state` is a float[8]
+ * device-resident so a whole step is graph-capturable.  `state` is a float[16]
  * device block indexed by VQA_ST_*; vqa_optim_finalize reads STEP and writes
- * the rest, then advances STEP. */
+ * the rest, then advances STEP and sets PENDING = 1.  vqa_adamw_amsgrad is a
+ * no-op while PENDING == 0: a caller that defers the update (the engine applies
+ * it segment by segment inside the next forward, each parameter range just
+ * before its first use) clears PENDING (16 bytes at state + 8, vqa_zero) once
+ * every range is applied, so the update is applied exactly once. */
 #define VQA_MAX_GROUPS 8
 #define VQA_ST_STEP 0
 #define VQA_ST_GRAD_NORM 1
@@ -285,6 +289,7 @@ int vqa_head_workspace_floats(int batch, int seq, int d, int answers);
 #define VQA_ST_LR_SCALE 3
 #define VQA_ST_BC1 4
 #define VQA_ST_BC2_SQRT 5
+#define VQA_ST_PENDING 8
 
 typedef struct vqa_adamw_desc {
   float* param; const float* grad;

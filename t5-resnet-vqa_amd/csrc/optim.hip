@@ -52,6 +52,7 @@ __global__ void finalize_kernel(const double* __restrict__ ws, int parts, float 
   st[VQA_ST_BC1] = (float)(1.0 - pow((double)beta1, t));
   st[VQA_ST_BC2_SQRT] = (float)sqrt(1.0 - pow((double)beta2, t));
   st[VQA_ST_STEP] = (float)t;
+  st[VQA_ST_PENDING] = 1.f;
 }
 
 struct AdamArgs {
@@ -68,7 +69,7 @@ struct AdamArgs {
 // stores are non-temporal.
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs A) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= A.n4) return;
+  if (i >= A.n4 || A.st[VQA_ST_PENDING] == 0.f) return;   // nothing to apply (see VQA_ST_PENDING)
   const float coef = A.st[VQA_ST_CLIP_COEF], lam = A.st[VQA_ST_LR_SCALE];
   const float bc1 = A.st[VQA_ST_BC1], bc2s = A.st[VQA_ST_BC2_SQRT];
   const float gmul = A.gscale * coef;

@@ -103,8 +103,8 @@ class DataParallelStep:
         s = torch.cuda.Stream(e.dev)
         s.wait_stream(torch.cuda.current_stream(e.dev))
         saved_rng = e.RNG.clone()
-        with torch.cuda.stream(s):                          # warm-up outside capture
-            e.forward()
+        with torch.cuda.stream(s):                          # warm-up outside capture (no optimizer update)
+            e._run(e.fwd_calls)
             e.backward()
         torch.cuda.current_stream(e.dev).wait_stream(s)
         torch.cuda.synchronize(e.dev)

@@ -113,6 +113,8 @@ class VQAEngine:
         self.t5_dw_group = int(g) if g else (int(t5_dw_group) if t5_dw_group else S.T5_LAYERS)
         # SGA blocks' q2 / m2 / fc1 / fc2 weight gradients batched over the blocks
         self.sga_dw_batch = os.environ.get("VQA_SGA_DW_BATCH", "1") != "0"
+        # AdamW of step k applied inside step k+1's forward (see _plan_optimizer)
+        self.defer_opt = os.environ.get("VQA_DEFER_OPT", "1") != "0"
         self.T = batch * seq_len
         self.lay = ParamLayout(vision, answer_spaces, num_blocks)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
@@ -130,6 +132,7 @@ class VQAEngine:
         self._side = torch.cuda.Stream(self.dev)
         self._wside = torch.cuda.Stream(self.dev)
         self._rstream = torch.cuda.Stream(self.dev)
+        self._ostream = torch.cuda.Stream(self.dev)      # deferred AdamW ranges (run_forward_streams)
         self.dw_stream = False
         self._scratch = None             # split-K workspace used while autotuning
 
@@ -157,7 +160,7 @@ class VQAEngine:
             self.p32[s.name] = self.P32[sl].view(s.shape)
             self.p16[s.name] = self.P16[sl].view(s.shape)
             self.g32[s.name] = self.G32[sl].view(s.shape)
-        self.opt_state = self._t(8, zero=True)
+        self.opt_state = self._t(L.ST_FLOATS, zero=True)
         # dropout RNG state {seed, counter, training}; the forward's first call advances the counter
         self.RNG = torch.from_numpy(np.array([self.seed & 0xFFFFFFFF, 0, 1, 0], np.uint32).view(np.int32)).to(self.dev)
         self.bucket = torch.from_numpy(t5_bucket_map(self.L, self.L)).reshape(-1).to(self.dev)
@@ -486,6 +489,7 @@ class VQAEngine:
         self._fsplit = [len(f)]                              # [pre | vision | text | fusion]
         if not self.pipeline:                                # pipelined: res_calls run beside the step
             f += self.res_calls
+        self._fvis_param = len(f)                            # first vision-branch call reading parameters
         # ConvTranspose2d scaler as implicit GEMM over the layer4 map (+bias) -> vision tokens
         cin, fh = self.fc, self.fh
         g = ops.conv_geom(B, fh, fh, cin, fh, fh, 3, 3, 1, 1)
@@ -501,7 +505,9 @@ class VQAEngine:
         self._call(f, "vqa_embedding_fwd", self.IDS, self.p32["t5.embed"], self.HS[0], T, D, S.T5_VOCAB,
                    self._dptr(SITE_EMBED, kp), extra=kp + [self.RNG])
         self._call(f, "vqa_t5_relbias_fwd", self.p32["t5.relbias"], self.bucket, self.PB, S.T5_HEADS, Lq, Lq)
+        self._t5_layer_start = []
         for i in range(S.T5_LAYERS):
+            self._t5_layer_start.append(len(f))
             self._call(f, "vqa_rmsnorm_fwd", self.HS[i], self.p32[f"t5.{i}.ln0"], None, self.N0[i], self.R0[i], T, D,
                        1e-6, None)
             self._linear(f, self.N0[i], f"t5.{i}.qkv_w", T, out16=self.QKV[i], bias=False)
@@ -818,8 +824,47 @@ class VQAEngine:
         d.grad_scale = self.grad_scale
         d.state = self.opt_state.data_ptr()
         self._adam_desc = d
-        o.append(ops.Call("vqa_adamw_amsgrad", ctypes.byref(d), desc=d,
-                          keep=(self.P32, self.G32, self.M, self.V, self.VMAX, self.P16, self.opt_state)))
+        keep = (self.P32, self.G32, self.M, self.V, self.VMAX, self.P16, self.opt_state)
+        self.adam_full = ops.Call("vqa_adamw_amsgrad", ctypes.byref(d), desc=d, keep=keep)
+        # Deferred update (defer_opt): step k's AdamW runs inside step k+1's forward, one
+        # parameter range at a time on its own stream, each range just before its first use
+        # (the forward reads the layout back to front: T5 layers 0..11, then the scaler / SGA /
+        # head).  The embedding table + rel-bias range is read by the forward's very first
+        # calls, so it is applied at the end of step k instead (the T5 chain would otherwise
+        # start behind its 0.9 GB pass).  Same arithmetic, same order of updates vs uses.
+        lay = self.lay
+        cuts = [("embed", lay["t5.relbias"].offset, n)]
+        for i in range(S.T5_LAYERS):
+            lo = lay[f"t5.{i}.qkv_w"].offset if i < S.T5_LAYERS - 1 else lay["t5.final_ln"].offset
+            hi = lay[f"t5.{i - 1}.qkv_w"].offset if i > 0 else lay["t5.relbias"].offset
+            cuts.append((f"t5.{i}", lo, hi))
+        cuts.append(("rest", 0, lay["t5.final_ln"].offset))
+        assert sum(hi - lo for _, lo, hi in cuts) == n
+        self.adam_segs = []
+        self.adam_embed = None
+        for name, lo, hi in cuts:
+            ds = L.AdamWDesc()
+            ctypes.memmove(ctypes.addressof(ds), ctypes.addressof(d), ctypes.sizeof(d))
+            ds.param, ds.grad = ops.addr(self.P32, lo), ops.addr(self.G32, lo)
+            ds.exp_avg, ds.exp_avg_sq = ops.addr(self.M, lo), ops.addr(self.V, lo)
+            ds.max_exp_avg_sq, ds.param16 = ops.addr(self.VMAX, lo), ops.addr(self.P16, lo)
+            ds.n = hi - lo
+            for i, e in enumerate(ends):
+                ds.group_end[i] = e - lo
+            c = ops.Call("vqa_adamw_amsgrad", ctypes.byref(ds), desc=ds, keep=keep)
+            if name == "embed":
+                self.adam_embed = c
+            else:
+                self.adam_segs.append((name, c))
+        lst = []
+        self._call(lst, "vqa_zero", ops.addr(self.opt_state, L.ST_PENDING), 16, extra=[self.opt_state])
+        self.clear_pending = lst[0]
+        o.append(self.adam_embed if self.defer_opt else self.adam_full)
+
+    def flush_optimizer(self):
+        """Apply a deferred AdamW update now (before reading the parameters outside a step)."""
+        if self.defer_opt:
+            self._run([c for _, c in self.adam_segs] + [self.clear_pending])
 
     def set_training(self, mode=True):
         """model.train() / model.eval(): the dropout kernels read this device flag at run
@@ -883,6 +928,8 @@ class VQAEngine:
         self._run(self.res_calls)
 
     def forward(self):
+        if self.defer_opt:                              # the previous step's update, then the forward
+            self._run([c for _, c in self.adam_segs] + [self.clear_pending])
         self._run(self.fwd_calls)
 
     def backward(self):
@@ -918,18 +965,42 @@ class VQAEngine:
         # ~1 ms into the step).
         hm, hs = L.stream_handle(main), L.stream_handle(side)
         vis, txt = f[p0:p1], f[p1:p2]
+        # deferred AdamW of the previous step: its parameter ranges on their own stream, issued
+        # first; each branch waits for a range right before the first call that reads it
+        vwait, twait, last = {}, {}, None
+        if self.defer_opt:
+            ost = self._ostream
+            ost.wait_event(fork)
+            ev = {}
+            for name, c in self.adam_segs:
+                c(L.stream_handle(ost))
+                ev[name] = torch.cuda.Event()
+                ev[name].record(ost)
+            last = ev[self.adam_segs[-1][0]]
+            for i, at in enumerate(self._t5_layer_start):
+                twait[at - p1] = ev[f"t5.{i}"]
+            vwait[self._fvis_param - p0] = ev["rest"]                       # ConvTranspose2d onwards
         j = 0
         for i, c in enumerate(vis):
+            if i in vwait:
+                main.wait_event(vwait[i])
             c(hm)
             upto = (i + 1) * len(txt) // len(vis)
             while j < upto:
+                if j in twait:
+                    side.wait_event(twait[j])
                 txt[j](hs)
                 j += 1
-        for c in txt[j:]:
-            c(hs)
+        for jj in range(j, len(txt)):
+            if jj in twait:
+                side.wait_event(twait[jj])
+            txt[jj](hs)
         join = torch.cuda.Event()
         join.record(side)
         main.wait_event(join)
+        if last is not None:
+            main.wait_event(last)
+            self.clear_pending(hm)                         # the update is applied: once only
         self._run(f[p2:])                                  # SGA + head
 
     def run_backward_streams(self):
@@ -1018,8 +1089,8 @@ class VQAEngine:
         s.wait_stream(torch.cuda.current_stream(self.dev))
         saved, saved_rng = self.opt_state.clone(), self.RNG.clone()
         with torch.cuda.stream(s):
-            if warm:                                    # warm-up launch outside capture
-                self.forward()
+            if warm:                                    # warm-up launch outside capture (no update)
+                self._run(self.fwd_calls)
                 self.backward()
         torch.cuda.current_stream(self.dev).wait_stream(s)
         torch.cuda.synchronize(self.dev)
@@ -1174,6 +1245,7 @@ class VQAEngine:
 
     def state_dict(self):
         """Reference-layout state_dict (SURVEY Appendix B keys), fp32 numpy."""
+        self.flush_optimizer()
         sd = dict(self._frozen)
         sd.update(self.lay.unpack(self.P32.cpu().numpy()))
         specs = S.model_specs(self.vision, self.A, self.NB)

@@ -76,6 +76,7 @@ GEMM_WAVES = {c: ((4, 2) if c in (9, 12) else (2, 4) if c in (10, 11) else (2, 2
 
 MAX_GROUPS = 8
 ST_STEP, ST_GRAD_NORM, ST_CLIP_COEF, ST_LR_SCALE, ST_BC1, ST_BC2_SQRT = range(6)
+ST_PENDING, ST_FLOATS = 8, 16
 
 
 class AdamWDesc(ctypes.Structure):

@@ -270,7 +270,7 @@ def test_adamw_amsgrad_matches_torch(k):
     p, m, v, vm = p0.clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda"), \
         torch.zeros(n, device="cuda")
     p16 = torch.empty(n, device="cuda", dtype=torch.bfloat16)
-    st = torch.zeros(8, device="cuda")
+    st = torch.zeros(16, device="cuda")
     ws = torch.empty(64, device="cuda", dtype=torch.float64)
     L = k.lib
     d = L.AdamWDesc()

@@ -23,15 +23,24 @@ KERNELS = {
 }
 
 
+FULL_GRID_ONLY = {"adamw_kernel"}   # in-step AdamW runs as parameter ranges; keep the whole-arena passes
+
+
 def load(d, counter):
     f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
-    out = defaultdict(list)
+    rows = defaultdict(list)
     for r in csv.DictReader(open(f)):
         if r["Counter_Name"] != counter:
             continue
         for tag, pat in KERNELS.items():
             if pat in r["Kernel_Name"]:
-                out[tag].append(float(r["Counter_Value"]))
+                rows[tag].append((int(r["Grid_Size"]), float(r["Counter_Value"])))
+    out = {}
+    for tag, v in rows.items():
+        if tag in FULL_GRID_ONLY:
+            g = max(x for x, _ in v)
+            v = [x for x in v if x[0] == g]
+        out[tag] = [c for _, c in v]
     return out
 
 
