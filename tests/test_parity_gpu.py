@@ -167,3 +167,39 @@ def test_t5_weight_gradient_grouping_is_bit_identical(cuda, pkg, monkeypatch):
         eng.forward_backward(nb)
         grads.append(eng.G32.clone())
     assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
+
+
+def test_deferred_optimizer_update_is_bit_identical(cuda, pkg, monkeypatch):
+    """AdamW applied inside the next forward (parameter ranges on their own stream, the
+    default) == AdamW at the end of the step: same losses, and the same parameters and
+    optimizer state once the pending update is flushed; an eval forward between steps
+    applies it exactly once (graph-replayed and eager steps)."""
+    import torch
+    B, L, H = 2, 32, 64
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    batches = [pkg.synthetic.make_batch(B, L, H, seed=20 + i) for i in range(4)]
+    res = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("VQA_DEFER_OPT", defer)
+        for graph in (False, True):
+            eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.1, seed=2)
+            assert eng.defer_opt == (defer == "1")
+            losses = []
+            for k, nb in enumerate(batches):
+                eng.load_batch(nb)
+                if graph and eng.graph is None:
+                    eng.capture()
+                eng.train_step()
+                losses.append(float(eng.LOSS.item()))
+                if k == 1:                                  # an eval-mode forward in between
+                    eng.set_training(False)
+                    eng.forward()
+                    losses.append(float(eng.LOSS.item()))
+                    eng.set_training(True)
+            eng.flush_optimizer()
+            torch.cuda.synchronize()
+            res.append((losses, eng.P32.clone(), eng.M.clone(), eng.VMAX.clone(), eng.P16.clone()))
+    for r in res[1:]:
+        assert r[0] == res[0][0]
+        for a, b in zip(r[1:], res[0][1:]):
+            assert torch.equal(a, b)
