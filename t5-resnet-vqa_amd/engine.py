@@ -1157,12 +1157,14 @@ class VQAEngine:
         lib = L.load()
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         chosen = {}
+        timed = []                                         # shapes not in the table: timed here
         extra = self.res_calls if self.pipeline else []
         for c in extra + self.fwd_calls + self.bwd_calls:
             if c.name == "vqa_gemm_pair":
                 d1, d2 = c.desc
                 key = repr(("pair", _gemm_key(d1), _gemm_key(d2)))
                 if key not in _TUNE_CACHE:
+                    timed.append(key)
                     best = None
                     for c1 in (3, 4, 6, 7):
                         for c2 in (3, 4, 6, 7):
@@ -1185,6 +1187,7 @@ class VQAEngine:
             d = c.desc
             key = repr(_gemm_key(d))
             if key not in _TUNE_CACHE:
+                timed.append(key)
                 best = None
                 nk = -(-d.k // 64)
                 for cfg in range(1, lib_gemm_configs() + 1):
@@ -1211,6 +1214,10 @@ class VQAEngine:
             self._apply_choice(c, _TUNE_CACHE[key])
             chosen[key] = _TUNE_CACHE[key]
         torch.cuda.synchronize(self.dev)
+        if timed:
+            import sys
+            print(f"autotune: {len(timed)} GEMM shapes not in the table, timed at start-up "
+                  f"(their choice, and with split-K the rounding, can vary by box): {timed}", file=sys.stderr)
         self._scratch = None
         self.graph = None
         if save:
