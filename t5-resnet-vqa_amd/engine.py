@@ -838,7 +838,8 @@ class VQAEngine:
             lo = lay[f"t5.{i}.qkv_w"].offset if i < S.T5_LAYERS - 1 else lay["t5.final_ln"].offset
             hi = lay[f"t5.{i - 1}.qkv_w"].offset if i > 0 else lay["t5.relbias"].offset
             cuts.append((f"t5.{i}", lo, hi))
-        cuts.append(("rest", 0, lay["t5.final_ln"].offset))
+        cuts.append(("scaler", lay["scaler_w"].offset, lay["t5.final_ln"].offset))
+        cuts.append(("head", 0, lay["scaler_w"].offset))     # classifier, pooler, SGA
         assert sum(hi - lo for _, lo, hi in cuts) == n
         self.adam_segs = []
         self.adam_embed = None
@@ -965,43 +966,80 @@ class VQAEngine:
         # ~1 ms into the step).
         hm, hs = L.stream_handle(main), L.stream_handle(side)
         vis, txt = f[p0:p1], f[p1:p2]
-        # deferred AdamW of the previous step: its parameter ranges on their own stream, issued
-        # first; each branch waits for a range right before the first call that reads it
-        vwait, twait, last = {}, {}, None
         if self.defer_opt:
-            ost = self._ostream
-            ost.wait_event(fork)
-            ev = {}
-            for name, c in self.adam_segs:
-                c(L.stream_handle(ost))
-                ev[name] = torch.cuda.Event()
-                ev[name].record(ost)
-            last = ev[self.adam_segs[-1][0]]
-            for i, at in enumerate(self._t5_layer_start):
-                twait[at - p1] = ev[f"t5.{i}"]
-            vwait[self._fvis_param - p0] = ev["rest"]                       # ConvTranspose2d onwards
+            self._forward_branches_deferred(fork, main, side, vis, txt)
+        else:
+            j = 0
+            for i, c in enumerate(vis):
+                c(hm)
+                upto = (i + 1) * len(txt) // len(vis)
+                while j < upto:
+                    txt[j](hs)
+                    j += 1
+            for c in txt[j:]:
+                c(hs)
+            join = torch.cuda.Event()
+            join.record(side)
+            main.wait_event(join)
+        self._run(f[p2:])                                  # SGA + head
+
+    def _forward_branches_deferred(self, fork, main, side, vis, txt):
+        """The two forward branches with the previous step's AdamW ranges on a third stream.
+        Capture order is submission order for a replayed graph, so the ranges are issued
+        two T5 layers ahead of the layer calls that wait for them (issuing all of them
+        first held the T5 chain back ~0.47 ms); the vision branch's parameter-reading
+        calls wait for the scaler range, the SGA / head for the last range."""
+        hm, hs = L.stream_handle(main), L.stream_handle(side)
+        ost = self._ostream
+        ost.wait_event(fork)
+        hs_o = L.stream_handle(ost)
+        segs = dict(self.adam_segs)
+        order = [n for n, _ in self.adam_segs]
+        ev = {}
+
+        def issue(name):
+            segs[name](hs_o)
+            ev[name] = torch.cuda.Event()
+            ev[name].record(ost)
+        p0, p1 = self._fsplit[0], self._fsplit[1]
+        starts = [at - p1 for at in self._t5_layer_start]
+        nl = len(starts)
+        # ranges in issue order: layers 0, 1, the scaler, the SGA / head range (the vision
+        # branch's SGA block-0 k/v projection reads it), then layer i+2 at layer i
+        issue("t5.0")
+        if nl > 1:
+            issue("t5.1")
+        issue("scaler")
+        issue("head")
+        vpre = vis[:self._fvis_param - p0]                 # frozen ResNet calls (unpipelined engines)
+        vpost = vis[self._fvis_param - p0:]                # ConvTranspose2d + SGA block 0 k/v
+        bounds = starts + [len(txt)]
         j = 0
-        for i, c in enumerate(vis):
-            if i in vwait:
-                main.wait_event(vwait[i])
-            c(hm)
-            upto = (i + 1) * len(txt) // len(vis)
-            while j < upto:
-                if j in twait:
-                    side.wait_event(twait[j])
-                txt[j](hs)
+        for t in range(bounds[0]):                         # embedding + rel-bias: read nothing deferred
+            txt[t](hs)
+        for i in range(nl):
+            if i + 2 < nl:
+                issue(f"t5.{i + 2}")
+            side.wait_event(ev[f"t5.{i}"])
+            for t in range(bounds[i], bounds[i + 1]):
+                txt[t](hs)
+            # the ResNet calls spread over the layers (as in the plain interleave); the
+            # parameter-reading vision calls follow the last of them (they read its output)
+            while j < (i + 1) * len(vpre) // nl:
+                vpre[j](hm)
                 j += 1
-        for jj in range(j, len(txt)):
-            if jj in twait:
-                side.wait_event(twait[jj])
-            txt[jj](hs)
+            if j == len(vpre) and vpost:
+                main.wait_event(ev["scaler"])
+                main.wait_event(ev["head"])
+                for c in vpost:
+                    c(hm)
+                vpost = []
         join = torch.cuda.Event()
         join.record(side)
         main.wait_event(join)
-        if last is not None:
-            main.wait_event(last)
-            self.clear_pending(hm)                         # the update is applied: once only
-        self._run(f[p2:])                                  # SGA + head
+        main.wait_event(ev[f"t5.{nl - 1}"])               # the last range issued (stream order)
+        self.clear_pending(hm)                             # the update is applied: once only
+        assert set(ev) == set(order)
 
     def run_backward_streams(self):
         main = torch.cuda.current_stream(self.dev)
