@@ -990,8 +990,11 @@ class VQAEngine:
         first held the T5 chain back ~0.47 ms); the vision branch's parameter-reading
         calls wait for the scaler range, the SGA / head for the last range."""
         hm, hs = L.stream_handle(main), L.stream_handle(side)
-        ost = self._ostream
-        ost.wait_event(fork)
+        # the ranges run on the vision-branch stream (VQA_OPT_STREAM=1: a stream of their own);
+        # a fourth concurrent stream shares a hardware queue with one of the others anyway
+        ost = self._ostream if os.environ.get("VQA_OPT_STREAM", "0") == "1" else main
+        if ost is not main:
+            ost.wait_event(fork)
         hs_o = L.stream_handle(ost)
         segs = dict(self.adam_segs)
         order = [n for n, _ in self.adam_segs]
