@@ -133,7 +133,7 @@ class VQAEngine:
         self._wside = torch.cuda.Stream(self.dev)
         self._rstream = torch.cuda.Stream(self.dev)
         self._ostream = torch.cuda.Stream(self.dev)      # deferred AdamW ranges (run_forward_streams)
-        self.dw_stream = False
+        self.dw_stream = os.environ.get("VQA_DW_STREAM", "0") == "1"
         self._scratch = None             # split-K workspace used while autotuning
 
     @classmethod
