@@ -115,6 +115,8 @@ class VQAEngine:
         self.sga_dw_batch = os.environ.get("VQA_SGA_DW_BATCH", "1") != "0"
         # AdamW of step k applied inside step k+1's forward (see _plan_optimizer)
         self.defer_opt = os.environ.get("VQA_DEFER_OPT", "1") != "0"
+        # the embedding + rel-bias range deferred too (else applied at the end of the step)
+        self.defer_embed = os.environ.get("VQA_DEFER_EMBED", "0") == "1"
         self.T = batch * seq_len
         self.lay = ParamLayout(vision, answer_spaces, num_blocks)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
@@ -853,14 +855,17 @@ class VQAEngine:
             for i, e in enumerate(ends):
                 ds.group_end[i] = e - lo
             c = ops.Call("vqa_adamw_amsgrad", ctypes.byref(ds), desc=ds, keep=keep)
-            if name == "embed":
+            if name == "embed" and not self.defer_embed:
                 self.adam_embed = c
             else:
                 self.adam_segs.append((name, c))
         lst = []
         self._call(lst, "vqa_zero", ops.addr(self.opt_state, L.ST_PENDING), 16, extra=[self.opt_state])
         self.clear_pending = lst[0]
-        o.append(self.adam_embed if self.defer_opt else self.adam_full)
+        if not self.defer_opt:
+            o.append(self.adam_full)
+        elif self.adam_embed is not None:
+            o.append(self.adam_embed)
 
     def flush_optimizer(self):
         """Apply a deferred AdamW update now (before reading the parameters outside a step)."""
@@ -1009,6 +1014,8 @@ class VQAEngine:
         nl = len(starts)
         # ranges in issue order: layers 0, 1, the scaler, the SGA / head range (the vision
         # branch's SGA block-0 k/v projection reads it), then layer i+2 at layer i
+        if "embed" in segs:                               # defer_embed: the table's range leads
+            issue("embed")
         issue("t5.0")
         if nl > 1:
             issue("t5.1")
@@ -1018,7 +1025,9 @@ class VQAEngine:
         vpost = vis[self._fvis_param - p0:]                # ConvTranspose2d + SGA block 0 k/v
         bounds = starts + [len(txt)]
         j = 0
-        for t in range(bounds[0]):                         # embedding + rel-bias: read nothing deferred
+        if "embed" in ev:
+            side.wait_event(ev["embed"])
+        for t in range(bounds[0]):                         # embedding + rel-bias
             txt[t](hs)
         for i in range(nl):
             if i + 2 < nl:
