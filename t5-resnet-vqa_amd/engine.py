@@ -302,6 +302,7 @@ class VQAEngine:
         # inputs of the blocks' q2 / m2 / fc1 / fc2 weight gradients, stacked in backward order
         # (slot NB-1-n) for the batched dW launches
         self.X1hS, self.O2S, self.X2hS, self.FFhS = (t((NB, T, D), BF16) for _ in range(4))
+        self.Q2S = t((NB, T, D), BF16)                 # the blocks' cross-attention queries (one batched GEMM)
         self.sga = []
         for n in range(NB):
             ly = V if n == 0 else T
@@ -310,7 +311,7 @@ class VQAEngine:
                 ly=ly, lk=lk,
                 P1=t((B, S.SGA_HEADS, Lq, Lq)), O1=self.O1A[n], S1=self.S1A[n],
                 X1=t((T, D)), X1h=self.X1hS[NB - 1 - n], MU1=t(T), RS1=t(T),
-                Q2=t((T, D), BF16), KV2=t((ly, 2 * D), BF16), P2=t((B, S.SGA_HEADS, Lq, lk)),
+                Q2=self.Q2S[NB - 1 - n], KV2=t((ly, 2 * D), BF16), P2=t((B, S.SGA_HEADS, Lq, lk)),
                 O2=self.O2S[NB - 1 - n], S2=t((T, D)), X2=t((T, D)), X2h=self.X2hS[NB - 1 - n], MU2=t(T), RS2=t(T),
                 FFh=self.FFhS[NB - 1 - n], S3=t((T, D)), OUT=t((T, D)), OUTh=t((T, D), BF16), MU3=t(T), RS3=t(T)))
         # head
@@ -554,9 +555,18 @@ class VQAEngine:
             s, p = self.sga[n], f"sga{n}."
             self._call(f, "vqa_layernorm_fwd", s["S1"], self.p32[p + "ln1_g"], self.p32[p + "ln1_b"], s["X1"],
                        s["X1h"], s["MU1"], s["RS1"], T, D, 1e-5)
+        # the blocks' cross-attention queries read only their norm1 outputs: one launch
+        # batched over the blocks (stack slot NB-1-n = the blocks' order in the arena)
+        segs = [self.lay[f"sga{n}.q2_w"] for n in reversed(range(NB))]
+        bsegs = [self.lay[f"sga{n}.q2_b"] for n in reversed(range(NB))]
+        wst = segs[1].offset - segs[0].offset if NB > 1 else 0
+        assert all(b_.offset - a_.offset == wst for a_, b_ in zip(segs, segs[1:]))
+        assert all(b_.offset - a_.offset == wst for a_, b_ in zip(bsegs, bsegs[1:]))
+        self._gemm(f, self.X1hS, self.p16[f"sga{NB - 1}.q2_w"], T, D, D, lda=D, ldb=D, c16=self.Q2S, ldc16=D,
+                   bias=self.p32[f"sga{NB - 1}.q2_b"], batch=NB, stride_a=T * D, stride_b=wst, stride_c16=T * D,
+                   stride_bias=wst, keep=(self.P16, self.P32))
         for n in range(NB):
             s, p = self.sga[n], f"sga{n}."
-            self._linear(f, s["X1h"], p + "q2_w", T, out16=s["Q2"])
             if n > 0:
                 self._linear(f, y16, p + "kv2_w", s["ly"], out16=s["KV2"])
             kv = s["KV2"]
