@@ -117,6 +117,8 @@ class VQAEngine:
         self.defer_opt = os.environ.get("VQA_DEFER_OPT", "1") != "0"
         # the embedding + rel-bias range deferred too (else applied at the end of the step)
         self.defer_embed = os.environ.get("VQA_DEFER_EMBED", "0") == "1"
+        # stream steps: the grad-norm pass over [0, rel-bias) beside the embedding scatter
+        self.sq_overlap = os.environ.get("VQA_SQ_OVERLAP", "1") != "0"
         self.T = batch * seq_len
         self.lay = ParamLayout(vision, answer_spaces, num_blocks)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
@@ -337,8 +339,8 @@ class VQAEngine:
         lib = L.load()
         self.WS_COL2 = t(lib.vqa_colsum_workspace_floats(V, D))
         self.WS_HEAD = t(lib.vqa_head_workspace_floats(B, Lq, D, self.A))
-        self.SQ_PARTS = 1024
-        self.WS_SQ = t(self.SQ_PARTS, torch.float64)
+        self.SQ_PARTS = 1024                              # per sqnorm range (two ranges, §3.7)
+        self.WS_SQ = t(2 * self.SQ_PARTS, torch.float64)
 
     # ------------------------------------------------------------------ call helpers
     # Every helper records the tensors it bakes into a call (ops.Call.keep), so no
@@ -819,8 +821,15 @@ class VQAEngine:
     def _plan_optimizer(self):
         o = self.opt_calls
         n = self.lay.total
-        self._call(o, "vqa_grad_sqnorm", self.G32, n, self.WS_SQ, self.SQ_PARTS)
-        self._call(o, "vqa_optim_finalize", self.WS_SQ, self.SQ_PARTS, float(self.grad_scale), float(self.max_norm),
+        # squared-norm partials over two ranges: [0, rel-bias) is final once the backward's
+        # deferred column sums are flushed, so graph steps run it beside the embedding-gradient
+        # scatter (run_backward_streams); the rel-bias + embedding-table range follows it
+        e0 = self.lay["t5.relbias"].offset
+        assert e0 % 4 == 0 and (n - e0) % 4 == 0
+        self._call(o, "vqa_grad_sqnorm", self.G32, e0, self.WS_SQ, self.SQ_PARTS)
+        self._call(o, "vqa_grad_sqnorm", ops.addr(self.G32, e0), n - e0, ops.addr(self.WS_SQ, self.SQ_PARTS),
+                   self.SQ_PARTS, extra=[self.G32, self.WS_SQ])
+        self._call(o, "vqa_optim_finalize", self.WS_SQ, 2 * self.SQ_PARTS, float(self.grad_scale), float(self.max_norm),
                    int(self.warmup), int(self.total), float(self.betas[0]), float(self.betas[1]), self.opt_state)
         d = L.AdamWDesc()
         d.param, d.grad = self.P32.data_ptr(), self.G32.data_ptr()
@@ -961,9 +970,11 @@ class VQAEngine:
         Buffers of the two branches are disjoint, so the result is the same as
         the sequential order (and bit-identical: no cross-branch reductions)."""
         self.run_forward_streams()
-        self.run_backward_streams()
         if optimizer:
-            self._run(self.opt_calls)
+            self.run_backward_streams(sq_overlap=self.sq_overlap)
+            self._run(self.opt_calls[1:] if self.sq_overlap else self.opt_calls)
+        else:
+            self.run_backward_streams()
 
     def run_forward_streams(self):
         main = torch.cuda.current_stream(self.dev)
@@ -1063,7 +1074,10 @@ class VQAEngine:
         self.clear_pending(hm)                             # the update is applied: once only
         assert set(ev) == set(order)
 
-    def run_backward_streams(self):
+    def run_backward_streams(self, sq_overlap=False):
+        """sq_overlap: also run the optimizer plan's first call (the squared-norm partials of
+        [0, rel-bias), final before the embedding scatter) on `side`, beside that scatter;
+        the caller then runs opt_calls[1:]."""
         main = torch.cuda.current_stream(self.dev)
         side, wside = self._side, self._wside
         b = self.bwd_calls
@@ -1074,7 +1088,18 @@ class VQAEngine:
         side.wait_event(fork2)
         with torch.cuda.stream(side):
             self._run(b[q0:q1])                            # scaler dW / db
-        self._run_tagged(b[q1:], main, wside)              # T5 backward + embedding
+        if sq_overlap:
+            assert b[-1] is self.emb_call
+            self._run_tagged(b[q1:-1], main, wside)        # T5 backward (+ deferred column sums)
+            for st in ((main, wside) if self.dw_stream else (main,)):   # all but the table's are final
+                ev = torch.cuda.Event()
+                ev.record(st)
+                side.wait_event(ev)
+            with torch.cuda.stream(side):
+                self._run(self.opt_calls[:1])
+            self._run(b[-1:])                              # embedding rows
+        else:
+            self._run_tagged(b[q1:], main, wside)          # T5 backward + embedding
         for st in (side, wside):
             join2 = torch.cuda.Event()
             join2.record(st)
@@ -1117,8 +1142,8 @@ class VQAEngine:
         with torch.cuda.stream(self._rstream):
             self._run(self.res_calls)
         self.run_forward_streams()                         # ConvTranspose2d || T5 encoder, then SGA
-        self.run_backward_streams()
-        self._run(self.opt_calls)
+        self.run_backward_streams(sq_overlap=self.sq_overlap)
+        self._run(self.opt_calls[1:] if self.sq_overlap else self.opt_calls)
         join = torch.cuda.Event()
         join.record(self._rstream)
         main.wait_event(join)
