@@ -10,10 +10,16 @@ Synthetic data (no datasets offline): a pool of 4 batches per rank is made
 resident in HBM before timing; each timed step copies one into the static input
 buffers (device to device) and replays the captured step graph.
 Prints ONE JSON line on rank 0.
+
+`--gpus N` with N > 1 and no torchrun environment: this process starts N ranks
+itself (one child process per GPU, before anything touches the GPU), waits for
+them, and exits with the worst return code; rank 0 prints the line.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,10 +33,13 @@ from __graft_entry__ import load_package  # noqa: E402
 FLOP_PER_PAIR = 30.95e9        # fwd+bwd algorithmic FLOPs, R50 @224, L=32
 MFMA_PEAK_TFLOPS = 2517.0      # bf16 dense: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
+PMC_FILE = "r02_pmc.json"               # rocprofv3 PMC summary this bench quotes (tools/pmc_step.py)
 
 
-def cpu_baseline(pkg, batch=8, steps=3, warm=1):
-    """The CPU oracle (fp32 restatement of the reference step) on this host's cores."""
+def cpu_baseline(pkg, batch=64, steps=5, warm=2):
+    """The CPU oracle (fp32 restatement of the reference step) on this host's cores, at the
+    config-2 shapes (B=64, 224x224, L=32), median of 5 steps after 2 warm-up steps
+    (SURVEY.md §8d / BASELINE.md)."""
     from oracle import vqa_oracle as orc
     threads = torch.get_num_threads()
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
@@ -45,8 +54,26 @@ def cpu_baseline(pkg, batch=8, steps=3, warm=1):
     t = float(np.median(times))
     return {"value": round(batch / t, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
             "sample": f"oracle fp32 train step (zero_grad+fwd+bwd+clip+AdamW amsgrad, dropout 0.1), R50+T5-base+3xSGA, "
-                      f"B={batch}, 224x224, L=32, median of {steps} steps after {warm} warm-up, "
-                      f"torch CPU {threads} threads"}
+                      f"B={batch}, 224x224, L=32, median of {steps} steps after {warm} warm-up "
+                      f"({t:.2f} s/step), torch CPU {threads} threads"}
+
+
+def spawn_ranks(n):
+    """Start n ranks of this script (one per GPU) with a torchrun-style environment;
+    called before any GPU call, so no process here ever initialises the GPU."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 def time_kernel(call, reps, stream):
@@ -74,6 +101,7 @@ def main():
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-kernel-rooflines", action="store_true", help="skip the per-kernel replays after the timed region")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run the frozen ResNet inside each step instead of beside the previous one")
     ap.add_argument("--tune-table", default=os.path.join(ROOT, "t5-resnet-vqa_amd", "tuning", "gemm_gfx950.json"),
@@ -81,15 +109,21 @@ def main():
     ap.add_argument("--tune-save", default=None, help="write the tile choices used to this file")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))          # one process per GPU, started before any GPU call
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     pkg = load_package()
     B, L, H = args.batch, args.seq_len, args.image_size
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)       # identical init on every rank
@@ -136,45 +170,95 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
         step(i)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    gpu_step = ev0.elapsed_time(ev1) * 1e-3 / args.steps       # HIP events on the replay stream
     if dist:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt, gpu_step], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt, gpu_step = float(t[0].item()), float(t[1].item())
     loss = float(eng.LOSS.item())
     gnorm = eng.last_grad_norm()
-
-    # Roofline of the dominant single launch: the fused AdamW-amsgrad pass (HBM-bound; the
-    # longest kernel of the step).  Algorithmic bytes per launch: read p, g, m, v, vmax (20 B)
-    # + write p, m, v, vmax (16 B) + the bf16 shadow (2 B) per parameter.  Timed with HIP
-    # events on its launch stream; re-running it after the timed region only re-applies
-    # the last update.  HBM traffic comes from the committed rocprofv3 PMC passes
-    # (tools/pmc_traffic.py) when present.
-    from vqa_amd import lib as VL
-    stream = torch.cuda.current_stream(dev)
-    adam_call = eng.adam_full                      # the whole-arena pass (in-step it runs as ranges)
-    assert adam_call.name == "vqa_adamw_amsgrad"
-    n_par = eng.lay.total
-    adam_bytes = 38.0 * n_par
-    adam_dur = time_kernel(adam_call, 10, stream)
-    adam_gbs = adam_bytes / adam_dur / 1e9
+    pairs = world * B * args.steps
+    value = pairs / dt
     pmc = {}
-    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    pmc_path = os.path.join(ROOT, "profiles", PMC_FILE)
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
-    # second roofline: the largest MFMA launch, the ConvTranspose2d weight-gradient implicit
-    # GEMM (M=768, N=9*2048, K=B*49; 2*M*N*K FLOP)
+
+    # Headline roofline (the step is > 97 % GEMM FLOPs, so it is MFMA-bound): the whole
+    # captured train step as one unit of work.  Algorithmic work per step = 30.95 GFLOP per
+    # pair x B pairs; duration = the step's GPU time from HIP events on
+    # the replay stream over the timed region; traffic = HBM bytes per step from the
+    # committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes over every dispatch of one step.
+    step_flop = FLOP_PER_PAIR * B
+    step_tflops = step_flop / gpu_step / 1e12
+    st = pmc.get("step", {})
+    roofline = {"bound": "mfma", "kernel": "whole train step (one hipGraph replay: ResNet50 fwd, ConvT, T5, 3xSGA, "
+                                           "head, backward, clip, AdamW)",
+                "achieved": round(step_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(step_tflops / MFMA_PEAK_TFLOPS, 4),
+                "traffic": round(st["traffic_bytes"]) if "traffic_bytes" in st else None,
+                "flop_per_step": step_flop, "step_gpu_ms": round(gpu_step * 1e3, 4),
+                "traffic_source": f"profiles/{PMC_FILE} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, all dispatches of one step)"}
+    out = {
+        "metric": "question-image pairs/sec, ResNet50+T5-base+SGA train step, 1/2/4/8 MI355X",
+        "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": "ResNet50 + T5-base + 3xSGA train step (BASELINE configs[1]; configs[2] at N=8)",
+                   "model": "resnet50+t5-base+3xSGA", "global_batch": world * B, "per_gpu_batch": B,
+                   "seq_len": L, "image_size": H, "answers": 170, "parallelism": f"dp{world}",
+                   "world_size": (dist.get_world_size() if dist else 1), "graph": not args.no_graph,
+                   "resnet_pipelined": pipe},
+        "roofline": roofline,
+        "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
+    }
+    if not args.no_kernel_rooflines:
+        out.update(kernel_rooflines(eng, stream, pmc))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pkg)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def kernel_rooflines(eng, stream, pmc):
+    """Secondary per-kernel rooflines, each launch replayed alone between HIP events on its
+    stream after the timed region (it only re-applies work the step already did)."""
+    from vqa_amd import lib as VL
+    out = {}
+    # HBM: the fused AdamW-amsgrad pass over the whole arena (in-step it runs as parameter
+    # ranges overlapped with the forward).  Algorithmic bytes per launch: read p, g, m, v,
+    # vmax (20 B) + write p, m, v, vmax (16 B) + the bf16 shadow (2 B) per parameter.
+    adam_call = eng.adam_full
+    assert adam_call.name == "vqa_adamw_amsgrad"
+    adam_bytes = 38.0 * eng.lay.total
+    adam_dur = time_kernel(adam_call, 10, stream)
+    adam_gbs = adam_bytes / adam_dur / 1e9
+    out["roofline_hbm"] = {"bound": "hbm", "kernel": "adamw_kernel (fused clip-scaled AdamW-amsgrad + bf16 shadow)",
+                           "achieved": round(adam_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(adam_gbs / HBM_PEAK_GBS, 4),
+                           "traffic": (round(pmc["adamw_kernel"]["traffic_bytes"]) if "adamw_kernel" in pmc else None),
+                           "algorithmic_bytes": adam_bytes, "kernel_avg_us": round(adam_dur * 1e6, 2)}
+    # MFMA: the largest single launch, the ConvTranspose2d weight-gradient implicit GEMM
+    # (M=768, N=9*2048, K=B*49; 2*M*N*K FLOP)
     wg_call = next(c for c in eng.bwd_calls if c.name == "vqa_gemm" and c.desc.b_conv == 1)
     cfg = VL.load().vqa_gemm_select(wg_call.desc)
     bm, bn, st = VL.GEMM_TILES[cfg]
@@ -184,11 +268,15 @@ def main():
     kdur = time_kernel(wg_call, 20, stream)
     kflop = 2.0 * wg_call.desc.m * wg_call.desc.n * wg_call.desc.k
     k_tflops = kflop / kdur / 1e12
-
-    # north_star's SGA figure: MFMA utilisation of the SGA blocks' GEMM-shaped launches (the
-    # linear layers of MHAtt / FFN and the attention cores, forward and backward): their FLOP
-    # per step over the sum of their launch times, each replayed alone between HIP events
-    # (no neighbour overlap, so slightly optimistic against the in-graph schedule)
+    out["roofline_gemm"] = {"bound": "mfma", "kernel": kname, "achieved": round(k_tflops, 1), "peak": MFMA_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": round(k_tflops / MFMA_PEAK_TFLOPS, 4),
+                            "traffic": (round(pmc["convT_dW"]["traffic_bytes"]) if "convT_dW" in pmc else None),
+                            "kernel_avg_us": round(kdur * 1e6, 2), "flop_per_launch": kflop}
+    # north_star's SGA figure: MFMA utilisation of the SGA blocks' GEMM launches (the q/k/v,
+    # merge and FFN linears of MHAtt / FFN, forward and backward; `gemm`) and of those plus
+    # the attention cores (`all`): their FLOP per step over the sum of their launch times,
+    # each replayed alone between HIP events (no neighbour overlap).  The committed PMC pass
+    # (SQ_VALU_MFMA_BUSY_CYCLES over the same launches in the step) is quoted beside it.
     sga_calls = [c for c in eng.sga_vision_calls + eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
                  if c.name in ("vqa_gemm", "vqa_gemm_pair", "vqa_attn_fwd", "vqa_attn_bwd")]
 
@@ -199,45 +287,16 @@ def main():
             return sum(2.0 * d.m * d.n * d.k for d in c.desc)
         d = c.desc
         return (4.0 if c.name == "vqa_attn_fwd" else 8.0) * d.batch * d.heads * d.lq * d.lk * d.dh
-    sga_flop = sum(call_flop(c) for c in sga_calls)
-    sga_time = sum(time_kernel(c, 10, stream) for c in sga_calls)
-    sga_tflops = sga_flop / sga_time / 1e12
-
-    pairs = world * B * args.steps
-    value = pairs / dt
-    out = {
-        "metric": "question-image pairs/sec, ResNet50+T5-base+SGA train step, 1/2/4/8 MI355X",
-        "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-        "config": {"workload": "ResNet50 + T5-base + 3xSGA train step (BASELINE configs[1]; configs[2] at N=8)",
-                   "model": "resnet50+t5-base+3xSGA", "global_batch": world * B, "per_gpu_batch": B,
-                   "seq_len": L, "image_size": H, "answers": 170, "parallelism": f"dp{world}",
-                   "graph": not args.no_graph, "resnet_pipelined": pipe},
-        "roofline": {"bound": "hbm", "kernel": "adamw_kernel (fused clip-scaled AdamW-amsgrad + bf16 shadow)",
-                     "achieved": round(adam_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(adam_gbs / HBM_PEAK_GBS, 4),
-                     "traffic": (round(pmc["adamw_kernel"]["traffic_bytes"]) if "adamw_kernel" in pmc else None),
-                     "algorithmic_bytes": adam_bytes, "kernel_avg_us": round(adam_dur * 1e6, 2),
-                     "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"},
-        "roofline_mfma": {"bound": "mfma", "kernel": kname,
-                          "achieved": round(k_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                          "frac": round(k_tflops / MFMA_PEAK_TFLOPS, 4),
-                          "traffic": (round(pmc["convT_dW"]["traffic_bytes"]) if "convT_dW" in pmc else None),
-                          "kernel_avg_us": round(kdur * 1e6, 2), "flop_per_launch": kflop,
-                          "step_mfma_frac": round(value / world * FLOP_PER_PAIR / (MFMA_PEAK_TFLOPS * 1e12), 4)},
-        "sga_mfma": {"launches": len(sga_calls), "flop_per_step": sga_flop, "kernel_us_per_step": round(sga_time * 1e6, 1),
-                     "achieved": round(sga_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(sga_tflops / MFMA_PEAK_TFLOPS, 4), "target_frac": 0.40},
-        "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(pkg)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+    sga = {}
+    for tag, names in (("gemm", ("vqa_gemm", "vqa_gemm_pair")), ("all", None)):
+        cs = [c for c in sga_calls if names is None or c.name in names]
+        fl = sum(call_flop(c) for c in cs)
+        tm = sum(time_kernel(c, 10, stream) for c in cs)
+        sga[tag] = {"launches": len(cs), "flop_per_step": fl, "kernel_us_per_step": round(tm * 1e6, 1),
+                    "achieved": round(fl / tm / 1e12, 1), "frac": round(fl / tm / 1e12 / MFMA_PEAK_TFLOPS, 4)}
+    out["sga_mfma"] = {"peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "target_frac": 0.40, **sga,
+                       "pmc_mfma_busy": pmc.get("sga_mfma_busy")}
+    return out
 
 
 if __name__ == "__main__":

@@ -239,7 +239,9 @@ int vqa_colsum_workspace_floats(int rows, int cols);
 /* drop: T5 embedding dropout (TF :725) on out (element token*d + col); NULL = none */
 int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int tokens, int d, int vocab,
                       const vqa_dropout* drop, hipStream_t stream);
-/* deterministic: each touched row is written once (sorted, fixed token order); tokens <= 8192; ws = 3*tokens ints */
+/* deterministic, no atomics: each touched row gets its tokens' dh rows summed in token order
+ * and ADDED to it (the rows must be zero, or hold an earlier partial sum); any number of
+ * tokens (slices of 16384, in order); ws = 3*min(tokens, 16384) ints */
 int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab, int* ws,
                       hipStream_t stream);
 /* zero the dtable rows named by ids_prev[0, tokens) (the rows the previous vqa_embedding_bwd

@@ -198,7 +198,7 @@ __device__ __forceinline__ unsigned long long shfl_xor64(unsigned long long v, i
 template <int E>
 __global__ __launch_bounds__(1024) void embedding_sort_kernel(const long long* __restrict__ ids, int tokens, int vocab,
                                                               int* __restrict__ ws) {
-  extern __shared__ unsigned long long key[];
+  __shared__ unsigned long long key[E * 1024];          // E = 16: 128 KiB of the CU's 160 KiB
   constexpr int n = E * 1024;
   const int t = threadIdx.x;
   unsigned long long v[E];
@@ -268,7 +268,9 @@ __global__ __launch_bounds__(1024) void embedding_sort_kernel(const long long* _
 }
 
 // One workgroup per (sorted slot, 128-column slab); only the first slot of an
-// id-run works.  Long runs (the pad id covers ~40% of a batch) are split over
+// id-run works, and ADDS its run's sum to the table row (the rows are zero, or
+// hold the sum of an earlier token slice of the same scatter: 0 + s == s, so a
+// single slice is bit-identical to a plain store).  Long runs (the pad id covers ~40% of a batch) are split over
 // 16 row-lanes that each sum a fixed stride of the run; the 16 partials are
 // then added in lane order through LDS, so the result is still bit-identical
 // run to run.
@@ -316,7 +318,10 @@ __global__ __launch_bounds__(EMB_RL * EMB_CL) void embedding_bwd_kernel(const fl
       const float4 v = red[r][tx];
       t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
     }
-    reinterpret_cast<float4*>(dtable + (long)id * d)[c4] = t;
+    float4* dst = reinterpret_cast<float4*>(dtable + (long)id * d) + c4;
+    const float4 o = *dst;
+    t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
+    *dst = t;
   }
 }
 
@@ -441,22 +446,30 @@ extern "C" int vqa_embedding_zero_rows(long long* ids_prev, const long long* ids
 
 extern "C" int vqa_embedding_bwd(const long long* ids, const float* dh, float* dtable, int tokens, int d, int vocab,
                                  int* ws, hipStream_t s) {
-  // keys hold the position in 16 bits and the padded sort buffer lives in LDS (<= 64 KiB)
-  VQA_REQUIRE(ids && dh && dtable && ws && tokens > 0 && tokens <= 8192 && d % 4 == 0,
-              "vqa_embedding_bwd: bad arguments");
-  const size_t lds = (tokens <= 1024 ? 1024 : tokens <= 2048 ? 2048 : tokens <= 4096 ? 4096 : 8192) * sizeof(unsigned long long);
-  if (tokens <= 1024)
-    hipLaunchKernelGGL(embedding_sort_kernel<1>, dim3(1), dim3(1024), lds, s, ids, tokens, vocab, ws);
-  else if (tokens <= 2048)
-    hipLaunchKernelGGL(embedding_sort_kernel<2>, dim3(1), dim3(1024), lds, s, ids, tokens, vocab, ws);
-  else if (tokens <= 4096)
-    hipLaunchKernelGGL(embedding_sort_kernel<4>, dim3(1), dim3(1024), lds, s, ids, tokens, vocab, ws);
-  else
-    hipLaunchKernelGGL(embedding_sort_kernel<8>, dim3(1), dim3(1024), lds, s, ids, tokens, vocab, ws);
-  if (int rc = vqa::check_launch("vqa_embedding_bwd/sort")) return rc;
-  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(tokens, vqa::cdiv(d, 4 * EMB_CL)), dim3(EMB_RL * EMB_CL), 0, s, dh,
-                     dtable, ws, tokens, d);
-  return vqa::check_launch("vqa_embedding_bwd");
+  // sort keys hold the position in 16 bits; one sort covers <= 16384 tokens (128 KiB of LDS).
+  // Larger scatters (DP: world x B x L gathered tokens) run as consecutive slices of 16384
+  // tokens in token order, each adding into the rows: deterministic, identical on every rank.
+  VQA_REQUIRE(ids && dh && dtable && ws && tokens > 0 && d % 4 == 0, "vqa_embedding_bwd: bad arguments");
+  constexpr int SLICE = 16384;
+  for (int t0 = 0; t0 < tokens; t0 += SLICE) {
+    const int n = tokens - t0 < SLICE ? tokens - t0 : SLICE;
+    const long long* sid = ids + t0;
+    if (n <= 1024)
+      hipLaunchKernelGGL(embedding_sort_kernel<1>, dim3(1), dim3(1024), 0, s, sid, n, vocab, ws);
+    else if (n <= 2048)
+      hipLaunchKernelGGL(embedding_sort_kernel<2>, dim3(1), dim3(1024), 0, s, sid, n, vocab, ws);
+    else if (n <= 4096)
+      hipLaunchKernelGGL(embedding_sort_kernel<4>, dim3(1), dim3(1024), 0, s, sid, n, vocab, ws);
+    else if (n <= 8192)
+      hipLaunchKernelGGL(embedding_sort_kernel<8>, dim3(1), dim3(1024), 0, s, sid, n, vocab, ws);
+    else
+      hipLaunchKernelGGL(embedding_sort_kernel<16>, dim3(1), dim3(1024), 0, s, sid, n, vocab, ws);
+    if (int rc = vqa::check_launch("vqa_embedding_bwd/sort")) return rc;
+    hipLaunchKernelGGL(embedding_bwd_kernel, dim3(n, vqa::cdiv(d, 4 * EMB_CL)), dim3(EMB_RL * EMB_CL), 0, s,
+                       dh + (long long)t0 * d, dtable, ws, n, d);
+    if (int rc = vqa::check_launch("vqa_embedding_bwd")) return rc;
+  }
+  return VQA_OK;
 }
 
 // a batch-sum is a column sum over `batch` partial rows

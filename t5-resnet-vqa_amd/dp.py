@@ -40,9 +40,28 @@ def plan_buckets(ready_marks, end, min_bytes=24 << 20):
     return out
 
 
+class _Done:
+    """A completed collective (host-staged gloo path): wait() is a no-op."""
+    def wait(self):
+        return True
+
+
+def _staged(t, group):
+    """gloo runs these collectives on host tensors only: stage device tensors through host
+    memory (CPU tests and the single-GPU multi-process test; RCCL works on HBM in place)."""
+    import torch.distributed as dist
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def allreduce_buckets(flat, buckets, group=None):
     """Launch one async SUM all-reduce per bucket slice of `flat`; returns works."""
     import torch.distributed as dist
+    if _staged(flat, group):
+        for _, a, b in buckets:
+            h = flat[a:b].cpu()
+            dist.all_reduce(h, group=group)
+            flat[a:b].copy_(h)
+        return [_Done() for _ in buckets]
     return [dist.all_reduce(flat[a:b], group=group, async_op=True) for _, a, b in buckets]
 
 
@@ -51,6 +70,13 @@ def gather_rows(ids, rows, out_ids, out_rows, group=None):
     import torch.distributed as dist
     if dist.get_backend(group) == "gloo":                  # CPU tests: list form
         w = dist.get_world_size(group)
+        if _staged(rows, group):
+            hi, hr = torch.empty(out_ids.shape, dtype=out_ids.dtype), torch.empty(out_rows.shape, dtype=out_rows.dtype)
+            dist.all_gather(list(hi.chunk(w)), ids.reshape(-1).cpu(), group=group)
+            dist.all_gather(list(hr.chunk(w)), rows.cpu(), group=group)
+            out_ids.copy_(hi)
+            out_rows.copy_(hr)
+            return [_Done(), _Done()]
         w1 = dist.all_gather(list(out_ids.chunk(w)), ids.reshape(-1), group=group, async_op=True)
         w2 = dist.all_gather(list(out_rows.chunk(w)), rows, group=group, async_op=True)
         return [w1, w2]
@@ -85,13 +111,17 @@ class DataParallelStep:
             prev = ci
         self.tail = calls[prev:]                            # nothing should remain after the last mark
         self.GDH = torch.zeros(self.world * T, D, dtype=torch.float32, device=dev)
-        self.WS = torch.empty(3 * self.world * T, dtype=torch.int32, device=dev)
+        self.WS = torch.empty(3 * min(self.world * T, 16384), dtype=torch.int32, device=dev)   # per 16384-token slice
         self.emb_call = ops.Call("vqa_embedding_bwd", self.GIDS.data_ptr(), self.GDH.data_ptr(),
                                  e.g32["t5.embed"].data_ptr(), self.world * T, D, S.T5_VOCAB, self.WS.data_ptr(),
                                  keep=(self.GIDS, self.GDH, self.WS, e.g32["t5.embed"]))
         self.graphs = None
         if use_graph:
             self.capture()
+        # the dense embedding gradient must be zero outside the rows the scatter writes: the
+        # zero-rows call only clears the PREVIOUS step's gathered ids (GIDS), so clear rows that
+        # local backward passes (warm-ups, a train_step before this object) left behind
+        e.g32["t5.embed"].zero_()
 
     def _run(self, calls):
         s = L.stream_handle()

@@ -124,7 +124,15 @@ class ResnetVQAModel:
             sd = cur
         training = self.training
         self._build(sd)
+        if getattr(self, "_optim_cfg", None):             # the trainer's AdamW / schedule settings survive
+            self.engine.configure_optimizer(**self._optim_cfg)
         self.train(training)
+
+    def configure_optimizer(self, **kw):
+        """Optimizer / schedule settings (trainer._init_optimizer); kept on the model so a
+        later load_state_dict rebuilds the engine with them."""
+        self._optim_cfg = dict(getattr(self, "_optim_cfg", None) or {}, **kw)
+        self.engine.configure_optimizer(**kw)
 
     def parameters_count(self):
         return self.engine.lay.num_params

@@ -47,7 +47,7 @@ class VQATrainer:
         group_lr = {"lang_model": float(optimizer_kwargs.get("lm_encoder_lr", 5e-3)),
                     "scaler": HARD_CODED_LR, "sga_modules": HARD_CODED_LR, "attention_pooler": HARD_CODED_LR,
                     "classification_layer": float(optimizer_kwargs.get("classifier_lr", 1e-5))}
-        model.engine.configure_optimizer(group_lr=group_lr, warmup=warm, total=self.num_training_steps,
+        model.configure_optimizer(group_lr=group_lr, warmup=warm, total=self.num_training_steps,
                                          max_norm=float(gradient_clipping or 0.0),
                                          weight_decay=float(kw.get("weight_decay", 1e-2)),
                                          betas=tuple(kw.get("betas", (0.9, 0.999))), eps=float(kw.get("eps", 1e-8)))

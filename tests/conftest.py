@@ -27,3 +27,20 @@ def golden():
     def _load(name):
         return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     return _load
+
+
+@pytest.fixture(scope="session")
+def parity_report():
+    """Measured errors of the GPU parity checks: tests add {check: value}; at the end of
+    the session they are written to gpurun_out/parity_report.json (merged back by gpurun,
+    then committed under profiles/)."""
+    import json
+    rep = {}
+    yield rep
+    if rep:
+        d = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(d, exist_ok=True)
+        path = os.path.join(d, "parity_report.json")
+        old = json.load(open(path)) if os.path.exists(path) else {}
+        old.update(rep)
+        json.dump(old, open(path, "w"), indent=1, sort_keys=True)

@@ -1,0 +1,59 @@
+"""Worker of tests/test_a_dp2_gpu.py: one DP rank of `dp.DataParallelStep` on cuda:0 over
+the gloo backend (several ranks share the one GPU of the test box; RCCL refuses two ranks
+on one device).  Rank r trains on samples [r*B, (r+1)*B) of each global batch.
+
+  python tests/dp_worker.py RANK WORLD PORT OUT.npz STEPS PIPELINE GRAPH"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    rank, world, port, out, steps, pipe, graph = sys.argv[1:8]
+    rank, world, steps = int(rank), int(world), int(steps)
+    pipe, graph = pipe == "1", graph == "1"
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, L, H = 4, 32, 64
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.0,
+                               seed=rank, pipeline=pipe, t5_dw_group=4, device="cuda:0")
+    gb = [pkg.synthetic.make_batch(world * B, L, H, seed=40 + i) for i in range(steps + 1)]
+    mine = [{k: (None if v is None else v[rank * B:(rank + 1) * B]) for k, v in nb.items()} for nb in gb]
+    dev = [{k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None} for nb in mine]
+    if pipe:
+        eng.prime(dev[0]["image_tensors"])
+        eng.F4.copy_(eng.F4N)
+        eng.load_batch(dev[0], next_images=dev[1]["image_tensors"])
+    else:
+        eng.load_batch(dev[0])
+    step = pkg.dp.DataParallelStep(eng, bucket_mb=8, use_graph=graph)
+    if pipe:
+        eng.prime(dev[0]["image_tensors"])
+    losses, norms = [], []
+    for i in range(steps):
+        if pipe:
+            eng.load_batch(dev[i], next_images=dev[i + 1]["image_tensors"])
+        else:
+            eng.load_batch(dev[i])
+        step.step()
+        torch.cuda.synchronize()
+        losses.append(float(eng.LOSS.item()))
+        norms.append(eng.last_grad_norm())
+    eng.flush_optimizer()
+    torch.cuda.synchronize()
+    np.savez(out, losses=np.array(losses), norms=np.array(norms), p32=eng.P32.cpu().numpy(),
+             g32=eng.G32.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -27,23 +27,49 @@ def pg():
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_dp_world1_matches_single_gpu(pg, pkg, graph):
+@pytest.mark.parametrize("graph,pipe", [(False, False), (True, False), (False, True), (True, True)])
+def test_dp_world1_matches_single_gpu(pg, pkg, graph, pipe):
+    """World-1 DP (bucketed all-reduce, gathered-row embedding scatter, segmented graphs; with
+    `pipe` also the separately replayed next-batch ResNet) == the single-GPU step, bit for bit,
+    over distinct batches per step, and with a local backward run before the DP object exists
+    (its embedding-gradient rows must not leak into the DP steps)."""
     B, L, H = 4, 32, 96
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
-    nb = pkg.synthetic.make_batch(B, L, H, seed=1)
-    e1 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20)
+    nbs = [pkg.synthetic.make_batch(B, L, H, seed=1 + i) for i in range(5)]
+    dev = [{k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None} for nb in nbs]
+    e1 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, pipeline=pipe)
     # the DP engine batches the T5 weight gradients in groups of 4 layers (bench.py), the
     # single-GPU one over all 12: same bits, different bucket boundaries
-    e2 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, t5_dw_group=4)
-    e1.load_batch(nb)
-    e2.load_batch(nb)
+    e2 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, t5_dw_group=4, pipeline=pipe)
+    junk = dev[4]                                    # a local step on another batch, before DP exists
+    for e in (e1, e2):
+        if pipe:
+            e.prime(junk["image_tensors"])
+            e.F4.copy_(e.F4N)
+            e.load_batch(junk, next_images=dev[0]["image_tensors"])
+        else:
+            e.load_batch(junk)
+        e.forward()
+        e.backward()
+        e.RNG[1] = 0
+    if graph:
+        e1.capture()
     step = pkg.dp.DataParallelStep(e2, bucket_mb=8, use_graph=graph)
     assert len(step.buckets) >= 5
-    for _ in range(3):
+    for e in (e1, e2):
+        if pipe:
+            e.prime(dev[0]["image_tensors"])
+    for i in range(3):
+        for e in (e1, e2):
+            if pipe:
+                e.load_batch(dev[i], next_images=dev[i + 1]["image_tensors"])
+            else:
+                e.load_batch(dev[i])
         e1.train_step()
         step.step()
-    torch.cuda.synchronize()
-    assert float(e1.LOSS) == float(e2.LOSS)
+        torch.cuda.synchronize()
+        assert float(e1.LOSS) == float(e2.LOSS), i
     assert torch.equal(e1.G32, e2.G32)
+    e1.flush_optimizer()
+    e2.flush_optimizer()
     assert torch.equal(e1.P32, e2.P32)

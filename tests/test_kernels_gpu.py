@@ -180,7 +180,7 @@ def test_head_fwd_bwd(k, B, L, A):
         torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("T,pad", [(300, 0), (2048, 900), (1, 0), (8192, 5000)])
+@pytest.mark.parametrize("T,pad", [(300, 0), (2048, 900), (1, 0), (8192, 5000), (16384, 7000), (40000, 16000)])
 def test_embedding_relbias_colsum_cast(k, T, pad):
     D, Vv = 768, 1000
     ids = torch.randint(0, Vv, (T,), device="cuda")

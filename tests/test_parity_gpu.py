@@ -2,11 +2,15 @@
 against the reference's own outputs (golden fixtures made by importing the
 reference modules) and the CPU fp32 oracle.
 
-Tolerances (calibrated on the reference's own bf16-autocast
-drift, App. C): log-probs max-abs <= 5e-2, loss rel <= 5e-3, total grad-norm
-rel <= 1e-2, per-group grad-norm rel <= 2e-2.  The grad-norm bounds are looser
-than the autocast drift because this path also runs the frozen ResNet and the
-ConvTranspose2d with bf16 activations (autocast keeps some in fp32)."""
+Tolerances are SURVEY.md §8c's bf16-vs-fp32 bounds (log-probs 5e-2, loss 5e-3,
+total grad-norm 1e-3, per-group grad-norm 5e-3), tightened where the measured
+errors allow (profiles/r02_parity_report.json has every measured value):
+log-probs max-abs <= 2e-2 (measured <= 1.3e-2), loss rel <= 1e-3 (<= 2.3e-4),
+total grad-norm rel <= 1e-3 (<= 2.6e-4), per-group grad-norm rel <= 5e-3
+(<= 3.3e-4) -- except the 769-parameter attention pooler at the B = 4 golden
+batch, <= 1e-2 (measured 6.0e-3 on R50: its gradient is one 768-vector summed
+over only B*L = 128 pooled tokens, so the bf16 rounding of the SGA output does
+not average out; at the benched B = 64 it is 2.0e-4, test_parity_full_gpu.py)."""
 import numpy as np
 import pytest
 import torch
@@ -14,7 +18,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 GROUPS = ("lang_model", "scaler", "sga_modules", "attention_pooler", "classification_layer")
-LP_TOL, LOSS_RTOL, GN_RTOL, GROUP_RTOL = 5e-2, 5e-3, 1e-2, 2e-2
+LP_TOL, LOSS_RTOL, GN_RTOL, GROUP_RTOL = 2e-2, 1e-3, 1e-3, 5e-3
+POOLER_RTOL_B4 = 1e-2
 
 
 @pytest.fixture(scope="module")
@@ -24,7 +29,10 @@ def cuda():
 
 
 @pytest.mark.parametrize("case,vision", [("model_r50_224_l32", "resnet50"), ("model_r34_256_l16", "resnet34")])
-def test_engine_matches_reference_golden(cuda, pkg, golden, case, vision):
+def test_engine_matches_reference_golden(cuda, pkg, golden, parity_report, case, vision):
+    """Three eval-mode steps against the reference's own outputs: log-probs, loss, grad
+    norms (total and per group) per step, then the parameters after the three updates
+    (slices and per-group sum |p - p0|, make_golden.py:147-162)."""
     g = golden(case)
     B, L, H = int(g["B"]), int(g["L"]), int(g["H"])
     sd = pkg.synthetic.make_state_dict(vision, seed=0)
@@ -32,31 +40,69 @@ def test_engine_matches_reference_golden(cuda, pkg, golden, case, vision):
     # the fixtures are eval-mode (dropout off): the reference's train-mode masks come from torch's RNG
     eng = pkg.engine.VQAEngine(sd, vision=vision, batch=B, seq_len=L, image_size=H, warmup=int(g["warmup"]),
                                total=int(g["total"]), dropout=0.0)
-    losses, norms = [], []
+    losses, norms, gnorms = [], [], []
+    lp_err = None
     for s in range(len(g["losses"])):
         lp, loss = eng.forward_backward(nb)
         if s == 0:
-            err = np.abs(lp - g["log_probs"]).max()
-            assert err <= LP_TOL, f"log-prob max-abs {err}"
-            gn = eng.group_grad_norms()
-            got = np.array([gn[k] for k in GROUPS])
-            rel = np.abs(got - g["group_grad_norms"][0]) / g["group_grad_norms"][0]
-            assert (rel <= GROUP_RTOL).all(), dict(zip(GROUPS, rel))
+            lp_err = float(np.abs(lp - g["log_probs"]).max())
+        gn = eng.group_grad_norms()
+        gnorms.append([gn[k] for k in GROUPS])
         eng.optimizer_step()
         torch.cuda.synchronize()
         losses.append(loss)
         norms.append(eng.last_grad_norm())
     lrel = np.abs(np.array(losses) - g["losses"]) / np.abs(g["losses"])
     nrel = np.abs(np.array(norms) - g["grad_norms"]) / g["grad_norms"]
+    grel = np.abs(np.array(gnorms) - g["group_grad_norms"]) / g["group_grad_norms"]
+    post = eng.state_dict()
+    scaler = "downscale_layer" if vision == "resnet50" else "upscale_layer"
+    slices = {"post_t5_q0": post["lang_model.block.0.layer.0.SelfAttention.q.weight"][:4, :16],
+              "post_cls_w": post["classification_layer.weight"][:4, :16],
+              "post_sga_fc1": post["sga_modules.2.ffn.mlp.fc1.weight"][:4, :16],
+              "post_scaler_w": post[scaler + ".weight"][:4, :4]}
+    init = pkg.synthetic.make_state_dict(vision, seed=0)
+    delta = {k: 0.0 for k in GROUPS}
+    for k, v in post.items():
+        if k.startswith("vision_model"):
+            continue
+        top = k.split(".", 1)[0]
+        grp = "scaler" if top in ("upscale_layer", "downscale_layer") else top
+        delta[grp] += float(np.abs(v.astype(np.float64) - init[k]).sum())
+    drel = np.abs(np.array([delta[k] for k in GROUPS]) - g["group_abs_delta"]) / g["group_abs_delta"]
+    # post-update slices: error relative to the size of the update the reference applied there
+    serr = {}
+    for name, v in slices.items():
+        ref = g[name]
+        p0 = {"post_t5_q0": init["lang_model.block.0.layer.0.SelfAttention.q.weight"][:4, :16],
+              "post_cls_w": init["classification_layer.weight"][:4, :16],
+              "post_sga_fc1": init["sga_modules.2.ffn.mlp.fc1.weight"][:4, :16],
+              "post_scaler_w": init[scaler + ".weight"][:4, :4]}[name]
+        # relative L2 error of the slice's update vector (p - p0): AdamW's m / sqrt(v) turns
+        # the bf16 rounding of near-zero gradients into O(lr) update differences elementwise
+        du, dr = v.astype(np.float64) - p0, ref.astype(np.float64) - p0
+        serr[name] = float(np.linalg.norm(du - dr) / max(np.linalg.norm(dr), 1e-30))
+    parity_report[f"golden_{case}"] = {
+        "log_prob_max_abs": lp_err, "loss_rel": lrel.tolist(), "grad_norm_rel": nrel.tolist(),
+        "group_grad_norm_rel_per_step": [dict(zip(GROUPS, r)) for r in grel.tolist()],
+        "group_abs_delta_rel": dict(zip(GROUPS, drel.tolist())), "post_slice_err_over_update": serr}
+    assert lp_err <= LP_TOL, f"log-prob max-abs {lp_err}"
+    tol = np.array([POOLER_RTOL_B4 if k == "attention_pooler" else GROUP_RTOL for k in GROUPS])
+    assert (grel[0] <= tol).all(), dict(zip(GROUPS, grel[0]))
     assert lrel[0] <= LOSS_RTOL, lrel
     assert nrel[0] <= GN_RTOL, nrel
-    # after updates the trajectories may drift a little further (lr up to 5e-3 on T5)
-    assert (lrel <= 3e-2).all(), lrel
-    assert (nrel <= 5e-2).all(), nrel
+    # after updates the trajectories drift a little further (lr up to 5e-3 on T5; measured
+    # loss 2.6e-3, grad-norm 1.2e-2 at step 3)
+    assert (lrel <= 1e-2).all(), lrel
+    assert (nrel <= 3e-2).all(), nrel
+    # the updates themselves: per-group sum |p - p0| (measured <= 5.5e-3) and the relative L2
+    # error of the reference's post-update slices' update vectors (measured <= 0.11)
+    assert (drel <= 2e-2).all(), dict(zip(GROUPS, drel))
+    assert max(serr.values()) <= 0.25, serr
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_engine_vs_oracle_multistep(cuda, pkg, p):
+def test_engine_vs_oracle_multistep(cuda, pkg, parity_report, p):
     """Train-mode steps (p=0.1: the reference's dropout, masks from the shared
     counter hash, restated in the oracle) and eval-mode steps (p=0)."""
     from oracle import vqa_oracle as orc
@@ -64,15 +110,21 @@ def test_engine_vs_oracle_multistep(cuda, pkg, p):
     sd = pkg.synthetic.make_state_dict("resnet50", seed=5)
     eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=50, dropout=p, seed=7)
     ot = orc.OracleTrainer(sd, "resnet50", warmup=1, total=50, dropout=p, seed=7)
+    rec = []
     for step in range(3):
         nb = pkg.synthetic.make_batch(B, L, H, seed=10 + step)
         lp, loss = eng.forward_backward(nb)
         olp, oloss, ogn = ot.train_one_step(orc.to_torch_batch(nb))
         eng.optimizer_step()
         torch.cuda.synchronize()
-        assert np.abs(lp - olp.numpy()).max() <= LP_TOL * (1 + step)
-        assert abs(loss - float(oloss)) <= LOSS_RTOL * (1 + 2 * step) * abs(float(oloss))
-        assert abs(eng.last_grad_norm() - float(ogn)) <= GN_RTOL * (1 + 2 * step) * float(ogn)
+        rec.append({"log_prob_max_abs": float(np.abs(lp - olp.numpy()).max()),
+                    "loss_rel": abs(loss - float(oloss)) / abs(float(oloss)),
+                    "grad_norm_rel": abs(eng.last_grad_norm() - float(ogn)) / float(ogn)})
+    parity_report[f"oracle_multistep_p{p}"] = rec
+    for step, r in enumerate(rec):
+        assert r["log_prob_max_abs"] <= LP_TOL * (1 + step), (step, r)
+        assert r["loss_rel"] <= LOSS_RTOL * (1 + 2 * step), (step, r)
+        assert r["grad_norm_rel"] <= GN_RTOL * (1 + 2 * step), (step, r)
 
 
 def test_state_dict_roundtrip_and_graph_replay(cuda, pkg):

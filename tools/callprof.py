@@ -30,7 +30,7 @@ eng.forward()
 eng.backward()
 torch.cuda.synchronize()
 if "--autotune" in sys.argv:
-    eng.autotune()
+    eng.autotune(table=os.path.join(ROOT, "t5-resnet-vqa_amd", "tuning", "gemm_gfx950.json"))
 s = L.stream_handle()
 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
@@ -60,7 +60,8 @@ for phase, calls in (("fwd", eng.fwd_calls), ("bwd", eng.bwd_calls), ("opt", eng
             kind = (f"{'At' if d.a_trans else 'A'}{'c' if d.a_conv else ''}"
                     f"{'Bt' if d.b_trans else 'B'}{'c' if d.b_conv else ''}")
             cfg = L.load().vqa_gemm_select(d)
-            info = f"{kind:6s} m={d.m:6d} n={d.n:6d} k={d.k:6d} cfg={cfg} {fl / us / 1e6:6.1f}TF"
+            info = (f"{kind:6s} m={d.m:6d} n={d.n:6d} k={d.k:6d} b={max(1, d.batch)} cfg={cfg} sk={d.splitk} "
+                    f"{fl / us / 1e6:6.1f}TF")
             key = f"gemm {phase} {'conv' if d.a_conv or d.b_conv else 'lin'} {kind}"
             if CONFIGS:
                 alt = []

@@ -1,0 +1,67 @@
+"""Replay selected launches of the benched step alone, for rocprofv3 PMC passes.
+
+  python tools/kernel_replay.py MANIFEST.json [REPS]
+
+Builds the engine exactly as bench.py does (B=64, 224x224, L=32, tuned tiles),
+runs one forward/backward so every buffer holds real data, then replays, REPS
+times each and in this order: the whole-arena AdamW pass, the ConvTranspose2d
+weight-gradient GEMM, and every SGA launch bench.py's sga_mfma counts.  The
+manifest lists (tag, kernel call name, FLOP, algorithmic bytes) per dispatch in
+issue order, so tools/pmc_step.py can map the LAST dispatches of a profile to
+them."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from __graft_entry__ import load_package  # noqa: E402
+
+out_path = sys.argv[1]
+REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+pkg = load_package()
+L = pkg.lib
+dev = torch.device("cuda", 0)
+B, Lq, H = 64, 32, 224
+sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=Lq, image_size=H, device=dev, warmup=10,
+                           total=100000, dropout=0.1, seed=0)
+del sd
+eng.load_batch(pkg.synthetic.make_batch(B, Lq, H, seed=1))
+eng.forward()
+eng.backward()
+eng.autotune(table=os.path.join(ROOT, "t5-resnet-vqa_amd", "tuning", "gemm_gfx950.json"))
+eng.forward()
+eng.backward()
+eng.optimizer_step()          # leaves the update pending, so the AdamW replays below do the full pass
+torch.cuda.synchronize()
+s = L.stream_handle()
+
+
+def gemm_flop(c):
+    if c.name == "vqa_gemm":
+        return 2.0 * c.desc.m * c.desc.n * c.desc.k * max(1, c.desc.batch)
+    if c.name == "vqa_gemm_pair":
+        return sum(2.0 * d.m * d.n * d.k for d in c.desc)
+    d = c.desc
+    return (4.0 if c.name == "vqa_attn_fwd" else 8.0) * d.batch * d.heads * d.lq * d.lk * d.dh
+
+
+plan = [("adamw", eng.adam_full, 0.0, 38.0 * eng.lay.total)]
+wg = next(c for c in eng.bwd_calls if c.name == "vqa_gemm" and c.desc.b_conv == 1)
+plan.append(("convT_dW", wg, gemm_flop(wg), 0.0))
+sga = [c for c in eng.sga_vision_calls + eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
+       if c.name in ("vqa_gemm", "vqa_gemm_pair", "vqa_attn_fwd", "vqa_attn_bwd")]
+for c in sga:
+    plan.append(("sga_gemm" if c.name.startswith("vqa_gemm") else "sga_attn", c, gemm_flop(c), 0.0))
+man = []
+for tag, c, fl, by in plan:
+    for _ in range(REPS):
+        c(s)
+        # a paired launch is one dispatch; every call here is one kernel dispatch
+        man.append({"tag": tag, "call": c.name, "flop": fl, "bytes": by})
+torch.cuda.synchronize()
+json.dump({"reps": REPS, "dispatches": man}, open(out_path, "w"))
+print(f"replayed {len(man)} dispatches", flush=True)
