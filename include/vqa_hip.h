@@ -119,7 +119,7 @@ typedef struct vqa_gemm_desc {
 
 /* tile configs: 1 128x128/3 stages, 2 128x64/4, 3 64x64/4, 4 64x64/2, 5 64x64/3, 6 128x64/2,
  * 7 64x128/2, 8 128x128/2 (4 waves); 9 256x128/2, 10 128x256/2, 11 256x256/2, 12 256x128/3 (8 waves) */
-#define VQA_GEMM_CONFIGS 12
+#define VQA_GEMM_CONFIGS 16
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
 /* tile configuration (1..VQA_GEMM_CONFIGS) that vqa_gemm would run for this descriptor */
 int vqa_gemm_select(const vqa_gemm_desc* d);

@@ -523,6 +523,7 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
       for (int r0 = 0; r0 < HALF; r0 += RPP) {
         const int r = r0 + tid / TPR, row = m0 + pw * WM + pg * HALF + r;
         if (HALF % RPP != 0 && r >= HALF) continue;
+        if (NT % TPR != 0 && tid >= RPP * TPR) continue;   // BN = 192: 24 threads per row, 10 rows per sweep
         if (row >= P.m || col >= P.n) continue;
         const float4 x0 = *reinterpret_cast<const float4*>(img + r * LDR + c);
         const float4 x1 = *reinterpret_cast<const float4*>(img + r * LDR + c + 4);
@@ -667,7 +668,8 @@ int launch(GemmParams& P, int batch, hipStream_t s) {
 // config: 0 = auto; 1 = 128x128 (3 stages); 2 = 128x64 (4); 3 = 64x64 (4); 4 = 64x64 (2);
 //         5 = 64x64 (3); 6 = 128x64 (2); 7 = 64x128 (2); 8 = 128x128 (2)  -- 4 waves (2x2);
 //         9 = 256x128 (2, 8 waves 4x2); 10 = 128x256 (2, 8 waves 2x4); 11 = 256x256 (2, 8 waves 2x4);
-//         12 = 256x128 (3, 8 waves 4x2).
+//         12 = 256x128 (3, 8 waves 4x2); 13 = 64x192 (2); 14 = 128x192 (2); 15 = 64x192 (3);
+//         16 = 128x192 (3) -- 4 waves, k-contiguous B only.
 // Every config accumulates each output element in the same K order (BK = 64
 // k-tiles, 16-deep MFMA steps), so the choice changes speed, never the bits.
 // Auto (measured on MI355X, tools/callprof.py): fewer stages = less LDS = more
@@ -697,6 +699,17 @@ int dispatch_tile(GemmParams& P, int batch, int config, hipStream_t s) {
     case 10: return launch<128, 256, 2, 2, 4, AKC, BKC, GA, GB>(P, batch, s);
     case 11: return launch<256, 256, 2, 2, 4, AKC, BKC, GA, GB>(P, batch, s);
     case 12: return launch<256, 128, 3, 4, 2, AKC, BKC, GA, GB>(P, batch, s);
+    case 13: case 14: case 15: case 16:
+      // 192-column tiles: one tile per CU for the transformer shapes (2048 x 3072 = 16 x 16 tiles
+      // of 128 x 192); the n-contig (transposed-B) LDS image has no 192-row form
+      if constexpr (BKC) {
+        if (config == 13) return launch<64, 192, 2, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+        if (config == 14) return launch<128, 192, 2, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+        if (config == 15) return launch<64, 192, 3, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+        return launch<128, 192, 3, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
+      } else {
+        return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: tile config %d needs a k-contiguous B operand (b_trans=0)", config);
+      }
     default: return launch<64, 64, 4, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
   }
 }
@@ -707,7 +720,8 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 void tile_of(int config, int& bm, int& bn) {
   static const int T[VQA_GEMM_CONFIGS + 1][2] = {{64, 64},   {128, 128}, {128, 64}, {64, 64},  {64, 64},
                                                  {64, 64},   {128, 64},  {64, 128}, {128, 128}, {256, 128},
-                                                 {128, 256}, {256, 256}, {256, 128}};
+                                                 {128, 256}, {256, 256}, {256, 128}, {64, 192}, {128, 192},
+                                                 {64, 192},  {128, 192}};
   bm = T[config][0];
   bn = T[config][1];
 }

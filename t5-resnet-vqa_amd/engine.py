@@ -117,6 +117,11 @@ class VQAEngine:
         # all-reduced, while the rest of the backward runs.  VQA_T5_DW_GROUP overrides (A/B).
         g = os.environ.get("VQA_T5_DW_GROUP")
         self.t5_dw_group = int(g) if g else (int(t5_dw_group) if t5_dw_group else S.T5_LAYERS)
+        # uneven groups, top layer first (e.g. "8,4": layers 11..4, then 3..0); overrides the size
+        gs = os.environ.get("VQA_T5_DW_GROUPS")
+        self.t5_dw_groups = [int(x) for x in gs.split(",")] if gs else None
+        if self.t5_dw_groups:
+            assert sum(self.t5_dw_groups) == S.T5_LAYERS and min(self.t5_dw_groups) >= 1
         # SGA blocks' q2 / m2 / fc1 / fc2 weight gradients batched over the blocks
         self.sga_dw_batch = os.environ.get("VQA_SGA_DW_BATCH", "1") != "0"
         # AdamW of step k applied inside step k+1's forward (see _plan_optimizer)
@@ -760,7 +765,8 @@ class VQAEngine:
         # G > 1: the layers' input gradients chain alone and every G layers ONE batched launch
         # per weight (wo, wi, o, qkv) computes the group's weight gradients (4 x G GEMMs of
         # K = 2048 as 4 launches); G == 1: each layer's dX + dW as paired launches
-        dxdw = self._dxdw if G == 1 else (lambda lst, dy, x, w, rows, **kw: self._dx(lst, dy, w, rows, **kw))
+        dxdw = self._dxdw if (G == 1 and not self.t5_dw_groups) else \
+            (lambda lst, dy, x, w, rows, **kw: self._dx(lst, dy, w, rows, **kw))
         for i in reversed(range(nl)):
             dF, dHM, dQKV = self.dFS[nl - 1 - i], self.dHMS[nl - 1 - i], self.dQKVS[nl - 1 - i]
             dxdw(b, dH16[i], self.FF[i], f"t5.{i}.wo", T, out16=dF, mask16=self.FF[i], alpha=ks)
@@ -791,9 +797,14 @@ class VQAEngine:
                        None, d32, d16, extra=kp + [self.RNG])
             self._defer(ws, nparts, D, D, self.g32[f"t5.{i}.ln0"])
             done = nl - i                                   # layers finished so far (11 .. i)
-            if G == 1:
+            ends = (np.cumsum(self.t5_dw_groups) if self.t5_dw_groups else None)
+            if G == 1 and ends is None:
                 mark(f"t5.{i}.ln1")
-            elif done % G == 0 or i == 0:
+            elif ends is not None and done in ends:
+                k = int(np.searchsorted(ends, done))
+                self._t5_group_dw(b, i + self.t5_dw_groups[k] - 1, i)
+                mark(f"t5.{i}.ln1")
+            elif ends is None and (done % G == 0 or i == 0):
                 self._t5_group_dw(b, i + (done - 1) % G, i)
                 mark(f"t5.{i}.ln1")
         # the relative-position bias is shared by all 12 layers: dPB = sum over (layer, sample) of dS,
@@ -1282,6 +1293,8 @@ class VQAEngine:
                 best = None
                 nk = -(-d.k // 64)
                 for cfg in range(1, lib_gemm_configs() + 1):
+                    if cfg in L.GEMM_KC_B_ONLY and d.b_trans:
+                        continue
                     bm, bn, _ = L.GEMM_TILES[cfg]
                     tiles = -(-d.m // bm) * -(-d.n // bn) * max(1, d.batch)
                     for sk in SPLITS:
@@ -1351,3 +1364,36 @@ class VQAEngine:
 
     def segment_grad(self, name):
         return self.g32[name]
+
+    def param_view(self, key):
+        """(parameter, gradient) device views of reference state-dict entry `key` inside the
+        flat fp32 arenas (no copy: they alias the engine's live weights / gradients).  The
+        q|k|v and k|v stacks are row blocks, so their parts are exact reference-shaped views;
+        the ConvTranspose2d scaler is stored as the flipped conv weight, so its view has the
+        kernel layout [768, 3, 3, Cin] (layout.py).  None if `key` is not trainable here."""
+        specs = S.model_specs(self.vision, self.A, self.NB)
+        for sg in self.lay.segments.values():
+            if key not in sg.parts:
+                continue
+            p32, g32 = self.p32[sg.name], self.g32[sg.name]
+            if sg.kind == "convT":
+                return p32, g32
+            if sg.kind == "flat":
+                return p32.view(specs[key]), g32.view(specs[key])
+            row = 0
+            for part in sg.parts:
+                n = specs[part][0]
+                if part == key:
+                    return p32[row:row + n].view(specs[key]), g32[row:row + n].view(specs[key])
+                row += n
+        return None
+
+    def refresh_shadow(self):
+        """Re-derive the bf16 GEMM shadow from the fp32 masters (after writing weights through
+        param_view / ParameterGroup views)."""
+        self.P16.copy_(self.P32)
+
+    def layer4_features(self):
+        """The frozen ResNet's layer4 map of the current batch as NCHW fp32 (the kernels keep
+        it NHWC bf16): the `features` generate_answers returns (resnet_vqa_model.py:186-203)."""
+        return self.F4.permute(0, 3, 1, 2).float()

@@ -24,7 +24,61 @@ import torch
 from . import synthetic as S
 from .engine import VQAEngine
 
-SUPPORTED_VISION = ("resnet50", "resnet34")
+SUPPORTED_VISION = ("resnet50", "resnet34", "resnet18")
+
+
+class ParameterGroup:
+    """The reference sub-module attribute a trainer reads (`model.lang_model`,
+    `model.sga_modules`, ...; faster_rcnn_vqa_trainer.py:231-263): its `parameters()` /
+    `named_parameters()` are live device views into the engine's flat fp32 arena (each with
+    `.grad` = the matching gradient view), `state_dict()` gives the reference entries.
+    The frozen ResNet (`vision_model`) and the unused scaler are plain fp32 tensors: the
+    reference never gives them a gradient.  Writes through the views reach
+    the fp32 masters; call `model.engine.refresh_shadow()` before the next step so the bf16
+    GEMM operands follow."""
+
+    def __init__(self, model, prefix, trainable=True):
+        self._model, self.prefix, self.trainable = model, prefix, trainable
+
+    def _keys(self):
+        m = self._model
+        return [k for k in S.model_specs(m.vision_model_name, m.answer_spaces, m.num_attention_blocks)
+                if k.startswith(self.prefix + ".")]
+
+    def named_parameters(self):
+        e = self._model.engine
+        for k in self._keys():
+            if k.endswith(("running_mean", "running_var", "num_batches_tracked")):
+                continue
+            v = e.param_view(k) if self.trainable else None
+            if v is None:
+                t = torch.as_tensor(np.asarray(e._frozen[k]))
+                yield k[len(self.prefix) + 1:], t
+            else:
+                p, g = v
+                p.grad = g
+                yield k[len(self.prefix) + 1:], p
+
+    def parameters(self):
+        for _, p in self.named_parameters():
+            yield p
+
+    def state_dict(self):
+        sd = self._model.engine.state_dict()
+        return {k[len(self.prefix) + 1:]: torch.from_numpy(np.ascontiguousarray(np.asarray(sd[k])))
+                for k in self._keys() if k in sd}
+
+    def __getitem__(self, i):                          # sga_modules[n]
+        return ParameterGroup(self._model, f"{self.prefix}.{int(i)}", self.trainable)
+
+    def __len__(self):
+        return self._model.num_attention_blocks if self.prefix == "sga_modules" else len(self._keys())
+
+    def eval(self):
+        return self
+
+    def train(self, mode=True):
+        return self
 
 
 class ResnetVQAModel:
@@ -53,6 +107,15 @@ class ResnetVQAModel:
                                            num_attention_blocks=self.num_attention_blocks)
         self._build(state_dict)
         self.training = True
+        # the sub-module attributes the reference trainer reads (faster_rcnn_vqa_trainer.py:231-263)
+        scaler = "downscale_layer" if vision_model_name == "resnet50" else "upscale_layer"
+        self.vision_model = ParameterGroup(self, "vision_model", trainable=False)
+        self.lang_model = ParameterGroup(self, "lang_model")
+        self.downscale_layer = ParameterGroup(self, "downscale_layer", trainable=scaler == "downscale_layer")
+        self.upscale_layer = ParameterGroup(self, "upscale_layer", trainable=scaler == "upscale_layer")
+        self.sga_modules = ParameterGroup(self, "sga_modules")
+        self.attention_pooler = ParameterGroup(self, "attention_pooler")
+        self.classification_layer = ParameterGroup(self, "classification_layer")
 
     # ------------------------------------------------------------------ engine
     def _build(self, state_dict, **kw):
@@ -108,6 +171,22 @@ class ResnetVQAModel:
         return log_probs, loss
 
     __call__ = forward
+
+    def generate_answers(self, question_input_ids, decoder_question_input_ids=None, question_attention_masks=None,
+                         decoder_question_attention_masks=None, image_tensors=None, annotation_ids=None,
+                         answer_input_ids=None, pixel_values=None, answer_attention_masks=None,
+                         question_type_ids=None):
+        """resnet_vqa_model.py:167-231: the forward plus the frozen ResNet's layer4 map,
+        returned as (log_probs, loss or None, {"features": [B, C, h, w] fp32}) (the kernels
+        hold the map in bf16, so the features carry bf16 rounding)."""
+        log_probs, loss = self.forward(question_input_ids, decoder_question_input_ids, question_attention_masks,
+                                       decoder_question_attention_masks, annotation_ids, image_tensors)
+        return log_probs, loss, {"features": self.engine.layer4_features()}
+
+    @staticmethod
+    def convert_logits_to_predictions(lm_logits):
+        """faster_rcnn_vqa_trainer.py:484-488: argmax of exp(log-probs) over the answers."""
+        return torch.argmax(torch.exp(lm_logits), dim=1)
 
     # ------------------------------------------------------------------ weights
     def state_dict(self):

@@ -15,6 +15,10 @@ Mirrors:
   train_one_epoch   the batch loop with the "secs/batch" timing log, averaged
                     every 10% of the epoch                        :314-360
   valid_one_step    eval-mode forward (dropout off), no update    :408-430
+  valid_one_epoch   the validation loop: average loss and exp/argmax
+                    predictions vs targets (WUPS needs nltk's WordNet, not
+                    on this path: accuracy is reported instead)   :408-480
+  convert_logits_to_predictions  argmax(exp(log-probs))            :484-488
 The whole train step is one replayed hipGraph; the only host sync per step is
 the `loss.item()` the reference API returns (pass sync=False to skip it).
 """
@@ -81,15 +85,20 @@ class VQATrainer:
         return (float(loss) if loss is not None else None), lp
 
     def train_one_epoch(self, batches, epoch=0):
-        """The reference's epoch loop without the WUPS/wandb tail: returns
-        {avg_loss, secs_per_batch, steps}."""
+        """The reference's epoch loop without the WUPS/wandb tail: returns {avg_loss,
+        secs_per_batch, steps, predictions, targets}; predictions are the exp/argmax
+        answers of every step (:336-343), kept on the device until the epoch ends (one
+        host copy per epoch instead of a .tolist() sync per step)."""
         total, n, t_epoch = 0.0, 0, 0.0
         window = max(1, len(batches) // 10) if hasattr(batches, "__len__") else 10
         win_loss, win_time = 0.0, 0.0
+        preds, targets = [], []
         for i, data_items in enumerate(batches):
             t0 = time.time()
-            loss, _ = self.train_one_step(data_items)
+            loss, lp = self.train_one_step(data_items)
             dt = time.time() - t0
+            preds.append(self.convert_logits_to_predictions(lp))
+            targets.append(torch.as_tensor(data_items["annotation_ids"]).reshape(-1))
             total += loss
             n += 1
             t_epoch += dt
@@ -100,7 +109,30 @@ class VQATrainer:
                             f" - secs/batch {win_time / window:.4f}")
                 win_loss, win_time = 0.0, 0.0
         self.total_training_time += t_epoch
-        return {"avg_loss": total / max(1, n), "secs_per_batch": t_epoch / max(1, n), "steps": n}
+        return {"avg_loss": total / max(1, n), "secs_per_batch": t_epoch / max(1, n), "steps": n,
+                "predictions": torch.cat(preds).tolist() if preds else [],
+                "targets": torch.cat([t.cpu() for t in targets]).tolist() if targets else []}
+
+    def valid_one_epoch(self, batches):
+        """faster_rcnn_vqa_trainer.py:408-480 without WUPS / checkpoint callbacks: eval mode,
+        no update; returns {avg_loss, predictions, targets, accuracy}."""
+        total, n = 0.0, 0
+        preds, targets = [], []
+        for data_items in batches:
+            loss, lp = self.valid_one_step(data_items)
+            total += loss if loss is not None else 0.0
+            n += 1
+            preds.append(self.convert_logits_to_predictions(lp))
+            targets.append(torch.as_tensor(data_items["annotation_ids"]).reshape(-1))
+        p = torch.cat(preds).cpu() if preds else torch.zeros(0, dtype=torch.long)
+        t = torch.cat([x.cpu() for x in targets]) if targets else torch.zeros(0, dtype=torch.long)
+        acc = float((p == t).float().mean()) if len(t) else 0.0
+        return {"avg_loss": total / max(1, n), "predictions": p.tolist(), "targets": t.tolist(), "accuracy": acc}
+
+    @staticmethod
+    def convert_logits_to_predictions(lm_logits):
+        """:484-488 -- argmax over exp(log-probs)."""
+        return torch.argmax(torch.exp(lm_logits), dim=1)
 
     def grad_norm(self):
         """clip_grad_norm_'s returned total norm of the last step."""

@@ -206,6 +206,8 @@ def main():
     print("r50 done", flush=True)
     np.savez_compressed(os.path.join(HERE, "model_r34_256_l16.npz"), **full_model_case("resnet34", 4, 16, 256))
     print("r34 done", flush=True)
+    np.savez_compressed(os.path.join(HERE, "model_r18_256_l16.npz"), **full_model_case("resnet18", 4, 16, 256))
+    print("r18 done", flush=True)
 
 
 if __name__ == "__main__":

@@ -79,3 +79,79 @@ def test_trainer_matches_oracle_train_mode(cuda, pkg):
         assert abs(tr.grad_norm() - float(ogn)) <= 1e-2 * (1 + 2 * step) * float(ogn)
     vloss, vlp = tr.valid_one_step(batch(pkg, 20))
     assert vloss is not None and m.training            # valid_one_step restores train mode
+
+
+def test_reference_trainer_attribute_surface(cuda, pkg):
+    """The sub-modules faster_rcnn_vqa_trainer._init_optimizer reads (:231-263) exist, and
+    their parameters() are live views of the engine's weights (and gradients): building the
+    reference's six AdamW param groups from them covers every trainable parameter once."""
+    from oracle import vqa_oracle as orc
+    m = pkg.model.ResnetVQAModel("resnet50", "t5-base", 170, batch_size=B, seq_len=L, image_size=H, seed=0)
+    groups = [m.vision_model, m.lang_model, m.downscale_layer, m.sga_modules, m.attention_pooler,
+              m.classification_layer]
+    opt = torch.optim.AdamW([{"params": list(g.parameters())} for g in groups], weight_decay=0.1, amsgrad=True)
+    trainable = orc.trainable_keys(dict.fromkeys(pkg.synthetic.model_specs("resnet50")))
+    n_trainable = sum(p.numel() for g in groups[1:] for p in g.parameters())
+    assert n_trainable == m.parameters_count() == 141_648_171
+    assert all(not p.is_cuda for p in m.vision_model.parameters())          # frozen, never updated
+    assert len(opt.param_groups) == 6 and len(trainable) > 0
+    # views alias the live weights: the engine's state_dict sees a write through them
+    w = dict(m.classification_layer.named_parameters())["weight"]
+    assert w.shape == (170, 768) and w.is_cuda and w.grad is not None and w.grad.shape == w.shape
+    q = dict(m.lang_model.named_parameters())["block.0.layer.0.SelfAttention.q.weight"]
+    q.add_(1.0)
+    sd = m.state_dict()
+    ref = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    np.testing.assert_array_equal(sd["lang_model.block.0.layer.0.SelfAttention.q.weight"].numpy(),
+                                  ref["lang_model.block.0.layer.0.SelfAttention.q.weight"] + np.float32(1.0))
+    assert len(m.sga_modules) == 3 and set(m.sga_modules[1].state_dict()) == {
+        k[len("sga_modules.1."):] for k in ref if k.startswith("sga_modules.1.")}
+
+
+def test_generate_answers_and_checkpoint_file(cuda, pkg, tmp_path, golden):
+    """generate_answers (resnet_vqa_model.py:167-231) returns (log_probs, loss|None,
+    {"features": layer4}) with the same log-probs as forward; a reference-format
+    best-model.pt (torch.save of the state dict, callbacks.py:34-46) loads with
+    torch.load(weights_only=True) into the mirror and reproduces the golden log-probs."""
+    g = golden("model_r50_224_l32")
+    Bg, Lg, Hg = int(g["B"]), int(g["L"]), int(g["H"])
+    sd = {k: torch.from_numpy(v) for k, v in pkg.synthetic.make_state_dict("resnet50", seed=0).items()}
+    path = tmp_path / "best-model.pt"
+    torch.save(sd, path)
+    loaded = torch.load(path, weights_only=True)
+    m = pkg.model.ResnetVQAModel("resnet50", "t5-base", 170, batch_size=Bg, seq_len=Lg, image_size=Hg)
+    m.load_state_dict(loaded)
+    m.eval()
+    nb = pkg.synthetic.make_batch(Bg, Lg, Hg, seed=1)
+    d = {k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None}
+    lp, loss = m(**d)
+    lp2, loss2, feats = m.generate_answers(**d)
+    assert torch.equal(lp, lp2) and float(loss) == float(loss2)
+    assert np.abs(lp.cpu().numpy() - g["log_probs"]).max() <= 2e-2
+    f = feats["features"]
+    assert f.shape == (Bg, 2048, 7, 7) and f.dtype == torch.float32
+    # the frozen ResNet's layer4 map vs the reference's (bf16 activations: 1e-2 of the range)
+    err = (f[:, :8].cpu().numpy() - g["feat_slice"])
+    assert np.abs(err).max() <= 1e-2 * np.abs(g["feat_slice"]).max() + 1e-3
+    d.pop("annotation_ids")
+    _, none, _ = m.generate_answers(**d)
+    assert none is None
+    pred = m.convert_logits_to_predictions(lp)
+    assert torch.equal(pred, lp.argmax(1))
+
+
+def test_trainer_epochs_and_resnet18(cuda, pkg):
+    """train_one_epoch / valid_one_epoch (faster_rcnn_vqa_trainer.py:314-480) on a
+    ResNet-18 model (resnet_vqa_model.py:57-58): predictions and targets per sample,
+    validation leaves the weights untouched."""
+    m = pkg.model.ResnetVQAModel("resnet18", "t5-base", 170, batch_size=B, seq_len=L, image_size=H, seed=2)
+    tr = pkg.trainer.VQATrainer(m, {"type": "AdamW", "kwargs": {"weight_decay": 0.1, "amsgrad": True}},
+                                {"num_warmup_steps": 1, "max_warmup_steps": 10}, num_training_steps=10, logger=None)
+    batches = [batch(pkg, 30 + i) for i in range(3)]
+    out = tr.train_one_epoch(batches)
+    assert out["steps"] == 3 and len(out["predictions"]) == 3 * B == len(out["targets"])
+    assert all(0 <= p < 170 for p in out["predictions"])
+    before = m.state_dict()["classification_layer.weight"].clone()
+    v = tr.valid_one_epoch(batches)
+    assert len(v["predictions"]) == 3 * B and 0.0 <= v["accuracy"] <= 1.0 and np.isfinite(v["avg_loss"])
+    assert torch.equal(m.state_dict()["classification_layer.weight"], before)

@@ -28,7 +28,7 @@ def close(got, ref, scale, rtol=2e-5):
     assert err <= rtol * scale + 1e-6, f"max err {err} vs scale {scale}"
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 9, 10, 11, 12])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 9, 10, 11, 12, 13, 14, 15, 16])
 @pytest.mark.parametrize("M,N,K", [(2048, 2304, 768), (100, 200, 136), (64, 170, 768), (3136, 768, 1024),
                                    (37, 24, 8)])
 def test_linear_forward_epilogue(ops, M, N, K, cfg):
@@ -200,7 +200,10 @@ def test_all_tile_configs_bitwise_identical(ops, pkg, layout):
             d.drop = pkg.lib.Dropout(0.1, 3, rng.data_ptr())
             return d
     outs = []
+    b_kc = layout in ("AB", "AtB", "conv")
     for cfg in range(1, n_cfg + 1):
+        if cfg in pkg.lib.GEMM_KC_B_ONLY and not b_kc:
+            continue
         out = torch.empty(M, N, device="cuda")
         d = mk(out)
         d.config = cfg
@@ -279,7 +282,7 @@ def test_splitk_matches_reference_and_is_config_invariant(ops, pkg, layout, spli
         ref = 0.5 * (A @ Bm) + res
         scale = 0.5 * (A.abs() @ Bm.abs()).max().item()
     outs = []
-    cfgs = sorted(pkg.lib.GEMM_TILES)
+    cfgs = [c for c in sorted(pkg.lib.GEMM_TILES) if layout in ("AB", "conv") or c not in pkg.lib.GEMM_KC_B_ONLY]
     for cfg in cfgs:
         out = torch.full((M, N), float("nan"), device="cuda")
         d = mk(out)
@@ -296,3 +299,16 @@ def test_splitk_matches_reference_and_is_config_invariant(ops, pkg, layout, spli
     close(outs[0], ref, scale)
     for cfg, o in zip(cfgs[1:], outs[1:]):
         assert torch.equal(o, outs[0]), f"config {cfg} differs at splitk={splitk}"
+
+
+def test_kc_b_only_configs_refuse_transposed_b(ops, pkg):
+    """The 192-column tiles have no transposed-B (n-contig) LDS image: asking for one
+    returns an error instead of running another config silently."""
+    M, N, K = 128, 192, 64
+    dy, w = bf((M, K), seed=3), bf((K, N), 0.05, seed=4)
+    out = torch.empty(M, N, device="cuda")
+    for cfg in pkg.lib.GEMM_KC_B_ONLY:
+        d = ops.gemm_desc(dy, w, M, N, K, lda=K, ldb=N, b_trans=True, c32=out, ldc32=N)
+        d.config = cfg
+        with pytest.raises(RuntimeError):
+            ops.run(d)

@@ -6,7 +6,8 @@ import torch
 import torch.nn.functional as F
 
 
-@pytest.mark.parametrize("vision,count", [("resnet50", 141_648_171), ("resnet34", 141_648_171 - 14_156_544 + 3_539_712)])
+@pytest.mark.parametrize("vision,count", [("resnet50", 141_648_171), ("resnet34", 141_648_171 - 14_156_544 + 3_539_712),
+                                          ("resnet18", 141_648_171 - 14_156_544 + 3_539_712)])
 def test_trainable_count_and_roundtrip(pkg, vision, count):
     lay = pkg.layout.ParamLayout(vision)
     assert lay.num_params == count

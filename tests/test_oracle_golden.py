@@ -47,7 +47,8 @@ def test_sga_block_matches_reference(golden, pkg):
     np.testing.assert_allclose(got, g["param_grad_norms"], rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("case,vision", [("model_r50_224_l32", "resnet50"), ("model_r34_256_l16", "resnet34")])
+@pytest.mark.parametrize("case,vision", [("model_r50_224_l32", "resnet50"), ("model_r34_256_l16", "resnet34"),
+                                          ("model_r18_256_l16", "resnet18")])
 def test_full_step_matches_reference(golden, pkg, case, vision):
     g = golden(case)
     B, L, H = int(g["B"]), int(g["L"]), int(g["H"])

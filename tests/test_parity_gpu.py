@@ -28,7 +28,8 @@ def cuda():
         pytest.skip("needs a GPU")
 
 
-@pytest.mark.parametrize("case,vision", [("model_r50_224_l32", "resnet50"), ("model_r34_256_l16", "resnet34")])
+@pytest.mark.parametrize("case,vision", [("model_r50_224_l32", "resnet50"), ("model_r34_256_l16", "resnet34"),
+                                          ("model_r18_256_l16", "resnet18")])
 def test_engine_matches_reference_golden(cuda, pkg, golden, parity_report, case, vision):
     """Three eval-mode steps against the reference's own outputs: log-probs, loss, grad
     norms (total and per group) per step, then the parameters after the three updates
