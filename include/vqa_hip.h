@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 7
+#define VQA_ABI_VERSION 8
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -239,6 +239,18 @@ int vqa_colsum_workspace_floats(int rows, int cols);
 /* drop: T5 embedding dropout (TF :725) on out (element token*d + col); NULL = none */
 int vqa_embedding_fwd(const long long* ids, const float* table, float* out, int tokens, int d, int vocab,
                       const vqa_dropout* drop, hipStream_t stream);
+/* ---------------------------------------------------------- input pipeline ---
+ * The collate's image path (dataset_utils/resnet_vqa_daquar_dataset.py:145-163:
+ * cv2.resize(INTER_LINEAR) to oh x ow, then ToTensor) for a whole batch: `src`
+ * holds the decoded uint8 RGB images (HWC, row-major) back to back, desc[b] (device
+ * memory) says where image b starts and its size; out = [batch, 3, oh, ow] fp32 in
+ * [0, 1].  OpenCV's 8-bit fixed-point bilinear arithmetic (image.hip). */
+typedef struct {
+  long long offset;        /* byte offset of the image in src */
+  int h, w;                /* source size (>= 1) */
+} vqa_image_desc;
+int vqa_resize_linear_u8(const void* src, const vqa_image_desc* desc, int batch, int oh, int ow, float* out,
+                         hipStream_t stream);
 /* deterministic, no atomics: each touched row gets its tokens' dh rows summed in token order
  * and ADDED to it (the rows must be zero, or hold an earlier partial sum); any number of
  * tokens (slices of 16384, in order); ws = 3*min(tokens, 16384) ints */

@@ -7,15 +7,19 @@ Layout:
   lib.py         ctypes binding of that ABI (fails loudly when the .so is absent)
   engine.py      flat parameter/gradient/optimizer arenas, the explicit
                  forward/backward schedule, fused clip+AdamW, hipGraph capture
-  model/         mirror of the reference module API (ResnetVQAModel, SGA)
-  trainer/       train_one_step mirror and the data-parallel (RCCL) step
+  layout.py      the flat arena <-> reference state_dict mapping
+  ops.py         prepared C-ABI calls (descriptors built once, replayed)
+  model.py       mirror of the reference module API (ResnetVQAModel)
+  trainer.py     train_one_step / epoch loops of the reference trainer
+  dp.py          the data-parallel (RCCL over xGMI) step
+  data.py        the collate's image path on the GPU (resize + ToTensor)
   synthetic.py   deterministic weights / batches (no network)
 """
 import importlib
 
 from . import synthetic  # noqa: F401  (numpy only)
 
-_LAZY = ("lib", "ops", "engine", "layout", "model", "trainer", "dp")
+_LAZY = ("lib", "ops", "engine", "layout", "model", "trainer", "dp", "data")
 
 
 def __getattr__(name):

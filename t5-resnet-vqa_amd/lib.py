@@ -51,6 +51,11 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class ImageDesc(ctypes.Structure):
+    """vqa_image_desc: byte offset of an image in the packed uint8 buffer, its height, width."""
+    _fields_ = [("offset", c_ll), ("h", c_int), ("w", c_int)]
+
+
 class ColsumJob(ctypes.Structure):
     _fields_ = [("ws", c_void_p), ("out", c_void_p), ("stride", c_ll), ("parts", c_int), ("cols", c_int),
                 ("beta", c_float), ("first_block", c_int)]
@@ -155,6 +160,7 @@ register("vqa_dropout_mask", P, P, c_ll)
 register("vqa_colsum_partials", P, c_int, c_ll, c_int, P, c_float)
 register("vqa_image_to_nhwc8", P, P, c_int, c_int, c_int)
 register("vqa_image_to_s2d16", P, P, c_int, c_int, c_int)
+register("vqa_resize_linear_u8", P, P, c_int, c_int, c_int, P)
 register("vqa_maxpool3x3s2_nhwc", P, P, c_int, c_int, c_int, c_int, c_int, c_int)
 register("vqa_colsum", P, c_int, c_int, c_int, c_ll, P, c_float, P)
 register("vqa_embedding_fwd", P, P, P, c_int, c_int, c_int, P)

@@ -1,7 +1,7 @@
 #!/bin/bash
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gemm_gpu.py tests/test_api_gpu.py -m gpu -q --timeout 150 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 400 python -u -m pytest tests/test_gemm_gpu.py tests/test_api_gpu.py tests/test_input_pipeline_gpu.py -m gpu -q --timeout 150 --timeout-method thread -p no:cacheprovider \
    > gpurun_out/r02_gemmtest.log 2>&1 || { echo GEMMTESTFAIL; grep -E "FAIL|Error|error" gpurun_out/r02_gemmtest.log | head -20; tail -5 gpurun_out/r02_gemmtest.log; exit 1; }
 tail -2 gpurun_out/r02_gemmtest.log
 timeout -k 10 300 python tools/gemm_lab.py > gpurun_out/gemm_lab2.log 2>&1 || { echo LABFAIL; tail gpurun_out/gemm_lab2.log; exit 1; }
