@@ -116,10 +116,12 @@ class VQAEngine:
         # DP passes a smaller group so the T5 gradient buckets still become final, and get
         # all-reduced, while the rest of the backward runs.  VQA_T5_DW_GROUP overrides (A/B).
         g = os.environ.get("VQA_T5_DW_GROUP")
-        self.t5_dw_group = int(g) if g else (int(t5_dw_group) if t5_dw_group else S.T5_LAYERS)
-        # uneven groups, top layer first (e.g. "8,4": layers 11..4, then 3..0); overrides the size
+        # a sequence = uneven groups, top layer first (e.g. (4, 4, 3, 1): layers 11..8, 7..4, 3..1,
+        # then 0 -- DP keeps the last, un-overlappable gradient bucket small)
+        seq = t5_dw_group if isinstance(t5_dw_group, (list, tuple)) else None
+        self.t5_dw_group = int(g) if g else (int(t5_dw_group) if t5_dw_group and seq is None else S.T5_LAYERS)
         gs = os.environ.get("VQA_T5_DW_GROUPS")
-        self.t5_dw_groups = [int(x) for x in gs.split(",")] if gs else None
+        self.t5_dw_groups = [int(x) for x in gs.split(",")] if gs else (list(seq) if seq else None)
         if self.t5_dw_groups:
             assert sum(self.t5_dw_groups) == S.T5_LAYERS and min(self.t5_dw_groups) >= 1
         # SGA blocks' q2 / m2 / fc1 / fc2 weight gradients batched over the blocks

@@ -24,7 +24,7 @@ def main():
     B, L, H = 4, 32, 64
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
     eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.0,
-                               seed=rank, pipeline=pipe, t5_dw_group=4, device="cuda:0")
+                               seed=rank, pipeline=pipe, t5_dw_group=(4, 4, 3, 1), device="cuda:0")
     gb = [pkg.synthetic.make_batch(world * B, L, H, seed=40 + i) for i in range(steps + 1)]
     mine = [{k: (None if v is None else v[rank * B:(rank + 1) * B]) for k, v in nb.items()} for nb in gb]
     dev = [{k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None} for nb in mine]

@@ -40,7 +40,7 @@ def test_dp_world1_matches_single_gpu(pg, pkg, graph, pipe):
     e1 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, pipeline=pipe)
     # the DP engine batches the T5 weight gradients in groups of 4 layers (bench.py), the
     # single-GPU one over all 12: same bits, different bucket boundaries
-    e2 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, t5_dw_group=4, pipeline=pipe)
+    e2 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, t5_dw_group=(4, 4, 3, 1), pipeline=pipe)
     junk = dev[4]                                    # a local step on another batch, before DP exists
     for e in (e1, e2):
         if pipe:

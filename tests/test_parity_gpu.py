@@ -213,13 +213,13 @@ def test_t5_weight_gradient_grouping_is_bit_identical(cuda, pkg, monkeypatch):
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
     nb = pkg.synthetic.make_batch(B, L, H, seed=3)
     grads = []
-    for g, sga in ((1, "0"), (4, "1"), (12, "1")):
+    for g, sga in ((1, "0"), (4, "1"), (12, "1"), ((4, 4, 3, 1), "1")):
         monkeypatch.setenv("VQA_SGA_DW_BATCH", sga)
         eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=20, dropout=0.1, seed=1,
                                    t5_dw_group=g)
         eng.forward_backward(nb)
         grads.append(eng.G32.clone())
-    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
+    assert all(torch.equal(grads[0], x) for x in grads[1:])
 
 
 def test_deferred_optimizer_update_is_bit_identical(cuda, pkg, monkeypatch):

@@ -21,6 +21,7 @@ from __graft_entry__ import load_package  # noqa: E402
 
 out_path = sys.argv[1]
 REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+MODE = sys.argv[3] if len(sys.argv) > 3 else "default"     # "res": every frozen-ResNet launch instead
 pkg = load_package()
 L = pkg.lib
 dev = torch.device("cuda", 0)
@@ -50,18 +51,26 @@ def gemm_flop(c):
 
 
 plan = [("adamw", eng.adam_full, 0.0, 38.0 * eng.lay.total)]
-wg = next(c for c in eng.bwd_calls if c.name == "vqa_gemm" and c.desc.b_conv == 1)
-plan.append(("convT_dW", wg, gemm_flop(wg), 0.0))
-sga = [c for c in eng.sga_vision_calls + eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
-       if c.name in ("vqa_gemm", "vqa_gemm_pair", "vqa_attn_fwd", "vqa_attn_bwd")]
-for c in sga:
-    plan.append(("sga_gemm" if c.name.startswith("vqa_gemm") else "sga_attn", c, gemm_flop(c), 0.0))
+if MODE == "res":
+    plan = [(f"res{i:02d}", c, gemm_flop(c) if c.name == "vqa_gemm" else 0.0, 0.0) for i, c in enumerate(eng.res_calls)]
+    # the T5 layer-0 forward GEMMs for comparison
+    t5 = [c for c in eng.fwd_calls[eng._t5_layer_start[0]:eng._t5_layer_start[1]] if c.name == "vqa_gemm"]
+    plan += [(f"t5_{i}", c, gemm_flop(c), 0.0) for i, c in enumerate(t5)]
+if MODE != "res":
+    wg = next(c for c in eng.bwd_calls if c.name == "vqa_gemm" and c.desc.b_conv == 1)
+    plan.append(("convT_dW", wg, gemm_flop(wg), 0.0))
+    sga = [c for c in eng.sga_vision_calls + eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
+           if c.name in ("vqa_gemm", "vqa_gemm_pair", "vqa_attn_fwd", "vqa_attn_bwd")]
+    for c in sga:
+        plan.append(("sga_gemm" if c.name.startswith("vqa_gemm") else "sga_attn", c, gemm_flop(c), 0.0))
 man = []
 for tag, c, fl, by in plan:
     for _ in range(REPS):
         c(s)
         # a paired launch is one dispatch; every call here is one kernel dispatch
-        man.append({"tag": tag, "call": c.name, "flop": fl, "bytes": by})
+        d = c.desc if c.name == "vqa_gemm" else None
+        man.append({"tag": tag, "call": c.name, "flop": fl, "bytes": by,
+                    "shape": [d.m, d.n, d.k, d.config, d.splitk] if d is not None else None})
 torch.cuda.synchronize()
 json.dump({"reps": REPS, "dispatches": man}, open(out_path, "w"))
 print(f"replayed {len(man)} dispatches", flush=True)
