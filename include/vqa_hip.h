@@ -67,8 +67,12 @@ int vqa_dropout_mask(const vqa_dropout* d, float* out, long long n, hipStream_t 
  * resnet_vqa_model.py:72-78).
  *   a_trans = 0: A(m,k) = a[m*lda + k]   a_trans = 1: A(m,k) = a[k*lda + m]
  *   b_trans = 0: B(k,n) = b[n*ldb + k]   b_trans = 1: B(k,n) = b[k*ldb + n]
- * a_conv: A(m,k) is the implicit im2col of an NHWC bf16 activation
+ * a_conv = 1: A(m,k) is the implicit im2col of an NHWC bf16 activation
  *   (m = output pixel (img,oh,ow), k = (kh,kw,c)); requires a_trans = 0.
+ * a_conv = 2: the same 3x3 / stride-1 / pad-1 convolution read from input patches staged
+ *   once per 64-channel chunk in LDS (each input pixel crosses L2 -> LDS once, not 9x):
+ *   k = (c / 64, kh, kw, c % 64), i.e. weights stored [Cout][C/64][3][3][64]; C % 64 == 0,
+ *   b_trans = 0, batch 1, no split-K; tile configs VQA_GEMM_PATCH_FIRST..VQA_GEMM_CONFIGS.
  * b_conv: B(k,n) is the implicit im2col with k = output pixel, n = (kh,kw,c);
  *   requires b_trans = 1 (weight-gradient of a convolution).
  * Epilogue: k = [mask(m,n) > 0] * dropout multiplier of element (z*m+row)*n+col
@@ -119,7 +123,8 @@ typedef struct vqa_gemm_desc {
 
 /* tile configs: 1 128x128/3 stages, 2 128x64/4, 3 64x64/4, 4 64x64/2, 5 64x64/3, 6 128x64/2,
  * 7 64x128/2, 8 128x128/2 (4 waves); 9 256x128/2, 10 128x256/2, 11 256x256/2, 12 256x128/3 (8 waves) */
-#define VQA_GEMM_CONFIGS 16
+#define VQA_GEMM_CONFIGS 20
+#define VQA_GEMM_PATCH_FIRST 17    /* configs 17..20: a_conv = 2 only */
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
 /* tile configuration (1..VQA_GEMM_CONFIGS) that vqa_gemm would run for this descriptor */
 int vqa_gemm_select(const vqa_gemm_desc* d);

@@ -127,9 +127,9 @@ class DaquarCollate:
         B = len(data_points)
         dec = np.zeros((B, 20), np.int64)                 # decoder_* / answer_* (ignored by the model)
         batch = {
-            "question_input_ids": torch.from_numpy(ids).to(self.dev, non_blocking=True),
+            "question_input_ids": torch.from_numpy(ids).to(self.dev),
             "decoder_question_input_ids": torch.from_numpy(dec).to(self.dev),
-            "question_attention_masks": torch.from_numpy(mask).to(self.dev, non_blocking=True),
+            "question_attention_masks": torch.from_numpy(mask).to(self.dev),
             "decoder_question_attention_masks": torch.from_numpy(dec).to(self.dev),
             "annotation_ids": torch.as_tensor([int(dp["annotation_id"]) for dp in data_points],
                                               dtype=torch.int64).to(self.dev),

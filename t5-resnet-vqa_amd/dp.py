@@ -25,6 +25,7 @@ import torch
 from . import lib as L
 from . import ops
 from . import synthetic as S
+from .engine import no_gc_capture
 
 
 def plan_buckets(ready_marks, end, min_bytes=24 << 20):
@@ -139,6 +140,11 @@ class DataParallelStep:
         torch.cuda.current_stream(e.dev).wait_stream(s)
         torch.cuda.synchronize(e.dev)
         e.RNG.copy_(saved_rng)                              # the warm-up must not consume a dropout draw
+        with no_gc_capture():
+            self.graphs = self._capture_all(s)
+
+    def _capture_all(self, s):
+        e = self.eng
         gs = {}
 
         def cap(name, calls):
@@ -156,7 +162,7 @@ class DataParallelStep:
             cap("seg", seg)
         cap("tail", self.tail + [self.emb_call])
         cap("opt", e.opt_calls)
-        self.graphs = gs
+        return gs
 
     def _res_begin(self):
         """Pipelined engines: F4 <- F4N, then the next batch's frozen ResNet on its own

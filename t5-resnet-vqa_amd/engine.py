@@ -27,7 +27,9 @@ Design (MI355X-first, not a translation of eager PyTorch):
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import gc
 import os
 import math
 
@@ -85,6 +87,31 @@ def _gemm_key(d):
             d.beta != 0.0, d.drop.p > 0.0)
 
 
+@contextlib.contextmanager
+def no_gc_capture():
+    """Stream capture with the cyclic garbage collector held off.  Engines (and the graphs /
+    tensors they own) are reclaimed through reference cycles; a collection that lands inside
+    a capture destroys another engine's graph execs and frees its blocks while the capture
+    is being recorded (measured: the later replay of the captured graph crashed in the
+    runtime).  Collect first, then keep the collector off until the capture has ended."""
+    was = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+
+
+def _h2d(dst, src):
+    """dst <- src (numpy / torch, host or device).  Asynchronous only from device or pinned
+    memory: an async copy out of a pageable temporary (freed when this returns) may be read
+    by the runtime after the free."""
+    src = torch.as_tensor(src).to(dst.dtype).reshape(dst.shape)
+    dst.copy_(src, non_blocking=src.is_cuda or src.is_pinned())
+
+
 class VQAEngine:
     def __init__(self, state_dict, vision="resnet50", batch=64, seq_len=32, image_size=224, device="cuda:0",
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
@@ -111,19 +138,30 @@ class VQAEngine:
         self.group_lr = {}                # per-group LR overrides (trainer optimizer_kwargs)
         # dX + dW of a layer as one paired GEMM launch (VQA_PAIR_BWD=0: separate launches, A/B only)
         self.pair_bwd = os.environ.get("VQA_PAIR_BWD", "1") != "0"
-        # T5 weight gradients batched over groups of this many layers (1: paired per layer).
-        # Single GPU: all 12 in one batch per weight (measured 6.88 vs 7.13 ms per step paired);
-        # DP passes a smaller group so the T5 gradient buckets still become final, and get
-        # all-reduced, while the rest of the backward runs.  VQA_T5_DW_GROUP overrides (A/B).
-        g = os.environ.get("VQA_T5_DW_GROUP")
-        # a sequence = uneven groups, top layer first (e.g. (4, 4, 3, 1): layers 11..8, 7..4, 3..1,
-        # then 0 -- DP keeps the last, un-overlappable gradient bucket small)
-        seq = t5_dw_group if isinstance(t5_dw_group, (list, tuple)) else None
-        self.t5_dw_group = int(g) if g else (int(t5_dw_group) if t5_dw_group and seq is None else S.T5_LAYERS)
-        gs = os.environ.get("VQA_T5_DW_GROUPS")
-        self.t5_dw_groups = [int(x) for x in gs.split(",")] if gs else (list(seq) if seq else None)
-        if self.t5_dw_groups:
+        # T5 weight gradients: per weight ONE launch batched over a group of layers (the
+        # layers' activations / gradients stacked at constant strides).  `t5_dw_group` is a
+        # group size (1: dX + dW paired per layer; 12: one group) or a sequence of group sizes,
+        # top layer first.  Default (single GPU): groups of 9 and 3 layers, the batched weight
+        # gradients on a side stream beside the remaining input-gradient chain (measured 6.66 vs
+        # 6.78-6.84 ms per step against one group of 12 on the chain; tools/gpu/ab_env.sh).
+        # DP passes (4, 4, 3, 1): the buckets become final, and are all-reduced, while the
+        # backward runs, and the last, exposed bucket is one layer.
+        # VQA_T5_DW_GROUP / VQA_T5_DW_GROUPS override (A/B).
+        self._default_dw = t5_dw_group is None
+        if t5_dw_group is None:
+            t5_dw_group = (9, 3)
+        env_g, env_gs = os.environ.get("VQA_T5_DW_GROUP"), os.environ.get("VQA_T5_DW_GROUPS")
+        if env_gs:
+            t5_dw_group = tuple(int(x) for x in env_gs.split(","))
+        elif env_g:
+            t5_dw_group = int(env_g)
+        if isinstance(t5_dw_group, (list, tuple)):
+            self.t5_dw_groups = [int(x) for x in t5_dw_group]
+            self.t5_dw_group = S.T5_LAYERS
             assert sum(self.t5_dw_groups) == S.T5_LAYERS and min(self.t5_dw_groups) >= 1
+        else:
+            self.t5_dw_groups = None
+            self.t5_dw_group = int(t5_dw_group)
         # SGA blocks' q2 / m2 / fc1 / fc2 weight gradients batched over the blocks
         self.sga_dw_batch = os.environ.get("VQA_SGA_DW_BATCH", "1") != "0"
         # AdamW of step k applied inside step k+1's forward (see _plan_optimizer)
@@ -150,7 +188,7 @@ class VQAEngine:
         self._wside = torch.cuda.Stream(self.dev)
         self._rstream = torch.cuda.Stream(self.dev)
         self._ostream = torch.cuda.Stream(self.dev)      # deferred AdamW ranges (run_forward_streams)
-        self.dw_stream = os.environ.get("VQA_DW_STREAM", "0") == "1"
+        self.dw_stream = os.environ.get("VQA_DW_STREAM", "1" if self._default_dw else "0") == "1"
         self._scratch = None             # split-K workspace used while autotuning
 
     @classmethod
@@ -278,8 +316,15 @@ class VQAEngine:
         g = ops.conv_geom(n, h, w, c, oh, oh, kh, kw, stride, pad)
         if kh == 1 and kw == 1 and stride == 1 and pad == 0:
             g = None                                   # a 1x1/1 conv is a plain GEMM over the NHWC rows
+        # 3x3 / stride 1: the LDS-patch convolution (a_conv = 2), weights reordered to
+        # [Cout][C/64][9][64] (VQA_CONV_PATCH=0: the implicit-im2col path, A/B)
+        patch = (kh == 3 and kw == 3 and stride == 1 and pad == 1 and c % 64 == 0 and 14 <= w <= 64
+                 and os.environ.get("VQA_CONV_PATCH", "1") != "0")
+        if patch:
+            w16 = w16.reshape(cout, 9, c // 64, 64).permute(0, 2, 1, 3).contiguous().reshape(cout, kh, kw, c)
+            self._res_keep.append(w16)
         self._gemm(self.res_calls, x, w16, n * oh * oh, cout, kh * kw * c, lda=kh * kw * c, ldb=kh * kw * c, ga=g,
-                   c16=out, ldc16=cout, bias=b32, relu=relu, res16=res16, ldres=cout)
+                   c16=out, ldc16=cout, bias=b32, relu=relu, res16=res16, ldres=cout, a_patch=patch)
 
     def _alloc_activations(self):
         B, Lq, T, NB, V = self.B, self.L, self.T, self.NB, self.V_TOK
@@ -955,10 +1000,8 @@ class VQAEngine:
         tensors of the batch that the FOLLOWING step trains on (this batch's images went
         in one step earlier, or through prime())."""
         def cp(dst, src):
-            if src is None:
-                return
-            src = torch.as_tensor(src)
-            dst.copy_(src.to(dst.dtype).reshape(dst.shape), non_blocking=True)
+            if src is not None:
+                _h2d(dst, src)
         cp(self.IMG, next_images if self.pipeline else batch["image_tensors"])
         cp(self.IDS, batch["question_input_ids"])
         cp(self.MASK, batch["question_attention_masks"])
@@ -968,7 +1011,7 @@ class VQAEngine:
         """Pipelined engines: compute the layer4 features of the first batch's images, so
         that the first train_step has them (later steps produce their successor's)."""
         assert self.pipeline, "prime() is for pipelined engines"
-        self.IMG.copy_(torch.as_tensor(images).to(self.IMG.dtype).reshape(self.IMG.shape), non_blocking=True)
+        _h2d(self.IMG, images)
         self._run(self.res_calls)
 
     def forward(self):
@@ -1198,7 +1241,13 @@ class VQAEngine:
                 self.backward()
         torch.cuda.current_stream(self.dev).wait_stream(s)
         torch.cuda.synchronize(self.dev)
-        parts = []
+        with no_gc_capture():
+            parts = self._capture_parts(s)
+        self.opt_state.copy_(saved)
+        self.RNG.copy_(saved_rng)                       # the warm-up launch must not consume a dropout draw
+        self.graph = parts
+
+    def _capture_parts(self, s):
         if self.allreduce is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
@@ -1216,9 +1265,7 @@ class VQAEngine:
                 self.optimizer_step()
             ar = self.allreduce
             parts = [g1, lambda: ar(self.G32), g2]
-        self.opt_state.copy_(saved)
-        self.RNG.copy_(saved_rng)                       # the warm-up launch must not consume a dropout draw
-        self.graph = parts
+        return parts
 
     # ------------------------------------------------------------------ GEMM autotuning
     def _tune_scratch(self, d):
@@ -1295,13 +1342,13 @@ class VQAEngine:
                 best = None
                 nk = -(-d.k // 64)
                 for cfg in range(1, lib_gemm_configs() + 1):
-                    if cfg in L.GEMM_KC_B_ONLY and d.b_trans:
+                    if (cfg in L.GEMM_KC_B_ONLY and d.b_trans) or ((cfg in L.GEMM_PATCH_ONLY) != (d.a_conv == 2)):
                         continue
                     bm, bn, _ = L.GEMM_TILES[cfg]
                     tiles = -(-d.m // bm) * -(-d.n // bn) * max(1, d.batch)
                     for sk in SPLITS:
                         # split only grids that leave CUs idle, with >= 2 k-tiles per slice
-                        if sk > 1 and (tiles >= 512 or nk < 2 * sk or tiles > 16384):
+                        if sk > 1 and (tiles >= 512 or nk < 2 * sk or tiles > 16384 or d.a_conv == 2):
                             continue
                         d.config = cfg
                         ops.set_splitk(d, sk)

@@ -29,7 +29,7 @@ def conv_geom(n, h, w, c, oh, ow, kh, kw, stride, pad):
 def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None, ldc32=0, c16=None, ldc16=0,
               bias=None, res32=None, res16=None, ldres=0, mask16=None, ldmask=0, alpha=1.0, beta=0.0,
               relu=False, ga=None, gb=None, batch=1, stride_a=0, stride_b=0, stride_c32=0, stride_c16=0,
-              stride_res=0, splitk=0, workspace=None, stride_bias=0, drop_site_stride=0):
+              stride_res=0, splitk=0, workspace=None, stride_bias=0, drop_site_stride=0, a_patch=False):
     for t in (a, b, c16, res16, mask16):
         assert not isinstance(t, torch.Tensor) or t.dtype == torch.bfloat16, "bf16 operand expected"
     for t in (c32, bias, res32):
@@ -47,7 +47,7 @@ def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None
     d.mask16 = addr(mask16)
     d.ldmask = ldmask
     d.alpha, d.beta, d.relu = alpha, beta, int(relu)
-    d.a_conv = int(ga is not None)
+    d.a_conv = (2 if a_patch else 1) if ga is not None else 0
     if ga is not None:
         d.ga = ga
     d.b_conv = int(gb is not None)

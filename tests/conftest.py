@@ -44,3 +44,29 @@ def parity_report():
         old = json.load(open(path)) if os.path.exists(path) else {}
         old.update(rep)
         json.dump(old, open(path, "w"), indent=1, sort_keys=True)
+
+
+@pytest.fixture(autouse=True)
+def _release_gpu_memory(request):
+    """After each GPU test: drop the engines / graphs it left (reference cycles through the
+    prepared calls keep them alive until a collection) and return the cached blocks, so one
+    process can run the whole GPU suite.  The device's free memory before the release is
+    appended to gpurun_out/gpu_mem.log."""
+    yield
+    if request.node.get_closest_marker("gpu") is None or "torch" not in sys.modules:
+        return
+    import gc
+    import torch
+    if not torch.cuda.is_available():
+        return
+    torch.cuda.synchronize()
+    free, total = torch.cuda.mem_get_info()
+    reserved = torch.cuda.memory_reserved()
+    if os.environ.get("VQA_TEST_NO_GC") != "1":           # (A/B of the capture-time collector guard)
+        gc.collect()
+        torch.cuda.empty_cache()
+    d = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "gpu_mem.log"), "a") as f:
+        f.write(f"{request.node.nodeid} free_gib={free / 2**30:.1f} total_gib={total / 2**30:.1f} "
+                f"reserved_gib={reserved / 2**30:.2f} after_gc_free_gib={torch.cuda.mem_get_info()[0] / 2**30:.1f}\n")

@@ -202,7 +202,7 @@ def test_all_tile_configs_bitwise_identical(ops, pkg, layout):
     outs = []
     b_kc = layout in ("AB", "AtB", "conv")
     for cfg in range(1, n_cfg + 1):
-        if cfg in pkg.lib.GEMM_KC_B_ONLY and not b_kc:
+        if (cfg in pkg.lib.GEMM_KC_B_ONLY and not b_kc) or cfg in pkg.lib.GEMM_PATCH_ONLY:
             continue
         out = torch.empty(M, N, device="cuda")
         d = mk(out)
@@ -282,7 +282,8 @@ def test_splitk_matches_reference_and_is_config_invariant(ops, pkg, layout, spli
         ref = 0.5 * (A @ Bm) + res
         scale = 0.5 * (A.abs() @ Bm.abs()).max().item()
     outs = []
-    cfgs = [c for c in sorted(pkg.lib.GEMM_TILES) if layout in ("AB", "conv") or c not in pkg.lib.GEMM_KC_B_ONLY]
+    cfgs = [c for c in sorted(pkg.lib.GEMM_TILES) if (layout in ("AB", "conv") or c not in pkg.lib.GEMM_KC_B_ONLY)
+            and c not in pkg.lib.GEMM_PATCH_ONLY]
     for cfg in cfgs:
         out = torch.full((M, N), float("nan"), device="cuda")
         d = mk(out)
@@ -312,3 +313,57 @@ def test_kc_b_only_configs_refuse_transposed_b(ops, pkg):
         d.config = cfg
         with pytest.raises(RuntimeError):
             ops.run(d)
+
+
+@pytest.mark.parametrize("nb,h,c,co", [(2, 14, 64, 96), (3, 7, 128, 64), (2, 28, 256, 128), (2, 56, 64, 64),
+                                       (1, 10, 192, 136), (2, 8, 512, 128)])
+def test_patch_conv_matches_reference(ops, pkg, nb, h, c, co):
+    """a_conv = 2 (3x3 / stride 1 / pad 1 read from LDS input patches, k = (c/64, kh, kw, c%64))
+    == F.conv2d in fp32 (bias, ReLU, bf16 residual epilogue), for every patch tile config
+    bit for bit, and close to the a_conv = 1 implicit-im2col path (same products, another
+    k-tile order)."""
+    x = bf((nb, h, h, c), seed=61)
+    wt = bf((co, 3, 3, c), 0.05, seed=62)                       # [Cout][kh][kw][C]
+    bias = torch.randn(co, device="cuda")
+    res = bf((nb * h * h, co), seed=63)
+    g = ops.conv_geom(nb, h, h, c, h, h, 3, 3, 1, 1)
+    M, N, K = nb * h * h, co, 9 * c
+    wp = wt.reshape(co, 9, c // 64, 64).permute(0, 2, 1, 3).contiguous()   # [Cout][C/64][9][64]
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), wt.float().permute(0, 3, 1, 2), bias, padding=1)
+    ref = torch.relu(ref.permute(0, 2, 3, 1).reshape(M, N) + res.float())
+    scale = F.conv2d(x.float().abs().permute(0, 3, 1, 2), wt.float().abs().permute(0, 3, 1, 2), padding=1).max().item()
+    outs = []
+    for cfg in [0] + list(pkg.lib.GEMM_PATCH_ONLY):
+        out = torch.full((M, N), float("nan"), device="cuda")
+        d = ops.gemm_desc(x, wp, M, N, K, lda=K, ldb=K, c32=out, ldc32=N, bias=bias, relu=True, res16=res, ldres=N,
+                          ga=g, a_patch=True)
+        d.config = cfg
+        ops.run(d)
+        outs.append(out)
+    torch.cuda.synchronize()
+    close(outs[0], ref, scale)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), "patch tile configs must give the same bits"
+    o1 = torch.empty(M, N, device="cuda")
+    d1 = ops.gemm_desc(x, wt, M, N, K, lda=K, ldb=K, c32=o1, ldc32=N, bias=bias, relu=True, res16=res, ldres=N, ga=g)
+    ops.run(d1)
+    torch.cuda.synchronize()
+    close(outs[0], o1, scale)
+
+
+def test_patch_configs_refused_elsewhere(ops, pkg):
+    """Patch tile configs only run a_conv = 2, and a_conv = 2 only runs patch configs."""
+    M, N, K = 128, 64, 64
+    a, b = bf((M, K), seed=1), bf((N, K), seed=2)
+    out = torch.empty(M, N, device="cuda")
+    d = ops.gemm_desc(a, b, M, N, K, lda=K, ldb=K, c32=out, ldc32=N)
+    d.config = pkg.lib.GEMM_PATCH_ONLY[0]
+    with pytest.raises(RuntimeError):
+        ops.run(d)
+    x = bf((1, 8, 8, 64), seed=3)
+    w = bf((64, 3, 3, 64), seed=4)
+    d = ops.gemm_desc(x, w, 64, 64, 576, lda=576, ldb=576, c32=out, ldc32=64,
+                      ga=ops.conv_geom(1, 8, 8, 64, 8, 8, 3, 3, 1, 1), a_patch=True)
+    d.config = 4
+    with pytest.raises(RuntimeError):
+        ops.run(d)
