@@ -33,9 +33,6 @@ from __graft_entry__ import load_package  # noqa: E402
 FLOP_PER_PAIR = 30.95e9        # fwd+bwd algorithmic FLOPs, R50 @224, L=32
 MFMA_PEAK_TFLOPS = 2517.0      # bf16 dense: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
-# DP: T5 weight gradients in groups of 4, 4, 3 and 1 layers, so their gradient buckets are
-# all-reduced while the backward still runs and the last (exposed) bucket is one layer
-DP_T5_DW_GROUPS = (4, 4, 3, 1)
 PMC_FILE = "r02_pmc.json"               # rocprofv3 PMC summary this bench quotes (tools/pmc_step.py)
 
 
@@ -133,7 +130,7 @@ def main():
     pipe = not args.no_pipeline
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev,
                                warmup=10, total=100000, dropout=0.1, seed=rank, pipeline=pipe,
-                               t5_dw_group=None if world == 1 else DP_T5_DW_GROUPS)
+                               t5_dw_group=None if world == 1 else pkg.dp.DP_T5_DW_GROUPS)
     del sd
     pool = []
     for i in range(4):

@@ -28,6 +28,12 @@ from . import synthetic as S
 from .engine import no_gc_capture
 
 
+# T5 weight-gradient groups of a DP engine (VQAEngine t5_dw_group), top layer first: the
+# buckets of layers 11..8, 7..4 and 3..1 are all-reduced while the backward continues, and
+# the last, exposed bucket holds one layer
+DP_T5_DW_GROUPS = (4, 4, 3, 1)
+
+
 def plan_buckets(ready_marks, end, min_bytes=24 << 20):
     """Group the engine's ready marks (call index, prefix end) into buckets of
     at least `min_bytes` of fp32 gradient.  Returns [(call_index, start, stop)]."""

@@ -21,6 +21,14 @@ Mirrors:
   convert_logits_to_predictions  argmax(exp(log-probs))            :484-488
 The whole train step is one replayed hipGraph; the only host sync per step is
 the `loss.item()` the reference API returns (pass sync=False to skip it).
+
+Data parallel (the reference trains on one device,
+faster_rcnn_vqa_trainer.py:61-62): with torch.distributed initialised and more
+than one rank in `process_group` (or data_parallel=True), each rank trains on its
+own batch and `train_one_step` runs `dp.DataParallelStep` -- the gradient buckets
+all-reduced over RCCL while the backward runs, the embedding rows all-gathered --
+so every rank applies the same update.  The returned loss / log-probs are the
+rank's own (its batch), the clip norm is the global one.
 """
 from __future__ import annotations
 
@@ -28,6 +36,7 @@ import time
 
 import torch
 
+from . import dp
 from .model import ResnetVQAModel
 
 HARD_CODED_LR = 5e-4          # faster_rcnn_vqa_trainer.py:244-261
@@ -35,7 +44,8 @@ HARD_CODED_LR = 5e-4          # faster_rcnn_vqa_trainer.py:244-261
 
 class VQATrainer:
     def __init__(self, model: ResnetVQAModel, optimizer_kwargs: dict, lr_scheduler_kwargs: dict,
-                 num_training_steps: int, gradient_clipping=1.0, use_graph=True, logger=print):
+                 num_training_steps: int, gradient_clipping=1.0, use_graph=True, logger=print,
+                 data_parallel=None, process_group=None, bucket_mb=24):
         if optimizer_kwargs.get("type", "AdamW") != "AdamW":
             raise ValueError("only AdamW is on this path (vit_daquar_config.json:41)")
         kw = dict(optimizer_kwargs.get("kwargs", {}))
@@ -43,6 +53,16 @@ class VQATrainer:
             raise ValueError("the reference trains with amsgrad=True; plain AdamW is not planned here")
         self.model = model
         self.logger = logger
+        if data_parallel is None:
+            data_parallel = (torch.distributed.is_available() and torch.distributed.is_initialized()
+                             and torch.distributed.get_world_size(process_group) > 1)
+        self.data_parallel = bool(data_parallel)
+        self.process_group, self.bucket_mb = process_group, int(bucket_mb)
+        self._dp = None
+        if self.data_parallel and model.engine.t5_dw_groups != list(dp.DP_T5_DW_GROUPS):
+            # DP layout: T5 weight gradients in groups that let the buckets become final (and be
+            # all-reduced) while the backward runs; rebuilt before the optimizer is configured
+            model._build(model.state_dict(), t5_dw_group=dp.DP_T5_DW_GROUPS)
         self.num_training_steps = int(num_training_steps)
         warm = lr_scheduler_kwargs.get("num_warmup_steps", -1)
         warm = self.num_training_steps // 10 if warm == -1 else int(warm)
@@ -67,9 +87,15 @@ class VQATrainer:
         m.load_batch(data_items["question_input_ids"], data_items["question_attention_masks"],
                      data_items["image_tensors"], data_items["annotation_ids"])
         e = m.engine
-        if self.use_graph and e.graph is None:
-            e.capture()
-        e.train_step()
+        if self.data_parallel:
+            if self._dp is None:
+                self._dp = dp.DataParallelStep(e, group=self.process_group, bucket_mb=self.bucket_mb,
+                                               use_graph=self.use_graph)
+            self._dp.step()
+        else:
+            if self.use_graph and e.graph is None:
+                e.capture()
+            e.train_step()
         loss = float(e.LOSS.item()) if sync else e.LOSS[0]
         return loss, e.LOGP
 

@@ -2,7 +2,10 @@
 the gloo backend (several ranks share the one GPU of the test box; RCCL refuses two ranks
 on one device).  Rank r trains on samples [r*B, (r+1)*B) of each global batch.
 
-  python tests/dp_worker.py RANK WORLD PORT OUT.npz STEPS PIPELINE GRAPH"""
+  python tests/dp_worker.py RANK WORLD PORT OUT.npz STEPS PIPELINE GRAPH [trainer]
+
+`trainer`: drive the step through model.ResnetVQAModel + trainer.VQATrainer (data_parallel
+picked up from the initialised process group) instead of the engine directly."""
 import os
 import sys
 
@@ -23,11 +26,17 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     B, L, H = 4, 32, 64
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
-    eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.0,
-                               seed=rank, pipeline=pipe, t5_dw_group=(4, 4, 3, 1), device="cuda:0")
     gb = [pkg.synthetic.make_batch(world * B, L, H, seed=40 + i) for i in range(steps + 1)]
     mine = [{k: (None if v is None else v[rank * B:(rank + 1) * B]) for k, v in nb.items()} for nb in gb]
     dev = [{k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None} for nb in mine]
+    if len(sys.argv) > 8 and sys.argv[8] == "trainer":
+        tr = trainer_run(pkg, sd, B, L, H, dev, steps, graph)
+        np.savez(out, **tr)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.0,
+                               seed=rank, pipeline=pipe, t5_dw_group=(4, 4, 3, 1), device="cuda:0")
     if pipe:
         eng.prime(dev[0]["image_tensors"])
         eng.F4.copy_(eng.F4N)
@@ -53,6 +62,29 @@ def main():
              g32=eng.G32.cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()
+
+
+TRAINER_KW = dict(optimizer_kwargs={"type": "AdamW", "lm_encoder_lr": 1e-4, "classifier_lr": 1e-4,
+                                    "kwargs": {"weight_decay": 0.1, "amsgrad": True}},
+                  lr_scheduler_kwargs={"num_warmup_steps": 1}, num_training_steps=20, gradient_clipping=1.0)
+
+
+def trainer_run(pkg, sd, B, L, H, batches, steps, graph, **kw):
+    """VQATrainer steps over `batches`; returns losses, clip norms and the final fp32 params."""
+    import numpy as np
+    import torch
+    model = pkg.model.ResnetVQAModel("resnet50", "t5-base", 170, batch_size=B, seq_len=L, image_size=H,
+                                     state_dict=sd, dropout=0.0, device="cuda:0")
+    tr = pkg.trainer.VQATrainer(model, use_graph=graph, logger=None, bucket_mb=8, **TRAINER_KW, **kw)
+    losses, norms = [], []
+    for i in range(steps):
+        loss, _ = tr.train_one_step(batches[i])
+        losses.append(loss)
+        norms.append(tr.grad_norm())
+    model.engine.flush_optimizer()
+    torch.cuda.synchronize()
+    return dict(losses=np.array(losses), norms=np.array(norms), p32=model.engine.P32.cpu().numpy(),
+                dp=np.array(tr.data_parallel))
 
 
 if __name__ == "__main__":

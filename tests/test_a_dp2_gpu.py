@@ -27,11 +27,11 @@ def _port():
     return str(p)
 
 
-def _ranks(tmp_path, world, steps, pipe, graph):
-    outs = [str(tmp_path / f"r{r}_{pipe}{graph}.npz") for r in range(world)]
+def _ranks(tmp_path, world, steps, pipe, graph, mode="engine"):
+    outs = [str(tmp_path / f"r{r}_{pipe}{graph}{mode}.npz") for r in range(world)]
     port = _port()
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), str(r), str(world), port, outs[r],
-                               str(steps), str(int(pipe)), str(int(graph))]) for r in range(world)]
+                               str(steps), str(int(pipe)), str(int(graph)), mode]) for r in range(world)]
     rcs = [p.wait(timeout=110) for p in procs]
     assert rcs == [0] * world, rcs
     return [np.load(o) for o in outs]
@@ -81,3 +81,33 @@ def test_dp_two_ranks_match_global_batch(gpu, pkg, tmp_path, parity_report, pipe
     # (m / sqrt(v) amplifies its rounding): a loose bound on the trajectory
     assert (dloss <= 2e-3).all() and (dnorm <= 2e-2).all(), (dloss, dnorm)
     assert upd_err <= 5e-2, upd_err
+
+
+def test_trainer_data_parallel_two_ranks(gpu, pkg, tmp_path, parity_report):
+    """`VQATrainer` picks up the initialised process group (world 2) and drives
+    dp.DataParallelStep: ranks stay bit-identical and train like one trainer on the
+    global batch (the reference's train_one_step, faster_rcnn_vqa_trainer.py:391-406)."""
+    sys.path.insert(0, HERE)
+    import dp_worker
+    world, steps = 2, 3
+    res = _ranks(tmp_path, world, steps, False, True, mode="trainer")
+    assert all(bool(r["dp"]) for r in res), "the trainer did not switch to data parallel"
+    for r in res[1:]:
+        assert np.array_equal(r["p32"], res[0]["p32"]), "DP ranks diverged"
+        assert np.array_equal(r["norms"], res[0]["norms"])
+    B, L, H = 4, 32, 64
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    import torch
+    gb = [{k: torch.as_tensor(v).cuda() for k, v in pkg.synthetic.make_batch(world * B, L, H, seed=40 + i).items()
+           if v is not None} for i in range(steps)]
+    ref = dp_worker.trainer_run(pkg, sd, world * B, L, H, gb, steps, True, data_parallel=False)
+    dloss = np.abs(np.mean([r["losses"] for r in res], axis=0) - ref["losses"]) / np.abs(ref["losses"])
+    dnorm = np.abs(res[0]["norms"] - ref["norms"]) / ref["norms"]
+    p0 = pkg.layout.ParamLayout("resnet50").pack(sd)
+    parity_report["dp2_trainer"] = {"loss_rel": dloss.tolist(), "grad_norm_rel": dnorm.tolist()}
+    assert dloss[0] <= 1e-5 and dnorm[0] <= 1e-4, (dloss, dnorm)
+    assert (dloss <= 2e-3).all() and (dnorm <= 2e-2).all(), (dloss, dnorm)
+    upd = float(np.linalg.norm(res[0]["p32"].astype(np.float64) - ref["p32"]) /
+                np.linalg.norm(ref["p32"].astype(np.float64) - p0))
+    parity_report["dp2_trainer"]["update_rel_l2"] = upd
+    assert upd <= 5e-2, upd
