@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 8
+#define VQA_ABI_VERSION 9
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -79,6 +79,8 @@ int vqa_dropout_mask(const vqa_dropout* d, float* out, long long n, hipStream_t 
  *   (1 when neither is given); v = k*(alpha*acc + bias[n]) + res(m,n); relu;
  *   c32 = v + beta*c32 (c32 may be NULL); c16 = bf16(v) (may be NULL).
  *   With res, relu acts after the residual (ResNet); relu with dropout needs no res.
+ *   `relu` is the epilogue activation: 0 none, 1 ReLU, 2 GELU (erf form), 3 tanh;
+ *   GELU / tanh take no dropout and no mask16 (ViT intermediate / pooler, config 4).
  * batch > 1 offsets a, b, c32, c16 by their strides and res/mask by stride_res. */
 typedef struct vqa_conv_geom {
   int n, h, w, c;          /* NHWC input */
@@ -149,7 +151,12 @@ int vqa_gemm_pair(const vqa_gemm_desc* dx, const vqa_gemm_desc* dw, hipStream_t 
  * dV = P^T dO; when dbias != NULL the per-sample dS is written to
  * dbias[b, h, i, j] (reduce with vqa_batch_sum; no atomics -> deterministic).
  * drop: dropout on P (element index ((b*H + h)*Lq + i)*Lk + j): O = drop(P) V;
- * p keeps the pre-dropout P and the backward regenerates the mask. */
+ * p keeps the pre-dropout P and the backward regenerates the mask.
+ * Long forward (lq > 32 or lk > 64, up to lk = 1024; dh 64 / 96; no p, bias, mask or
+ * dropout): ViTSelfAttention of BASELINE config 4 (vit_vqa_model.py:183-186, frozen,
+ * no_grad), an online-softmax MFMA kernel; there is no long backward.
+ * Causal T5 decoder self-attention (vit_vqa_model.py:199-205): the bias rows carry
+ * finfo.min where j > i (vqa_t5_relbias_fwd with bucket < 0). */
 typedef struct vqa_attn_desc {
   const void* q; long long ldq;
   const void* k; long long ldk;
@@ -234,7 +241,8 @@ int vqa_colsum_batched(const vqa_colsum_job* jobs, int njobs, int nblocks, hipSt
  *   its dense scatter-add gradient (dtable must be zeroed by the caller).
  * vqa_t5_relbias_fwd/bwd: compute_bias gather of the [buckets, H] table by a
  *   precomputed bucket map [Lq*Lk] (TF modeling_t5.py:217-279) and its
- *   scatter-add gradient (dtable zeroed by the caller). */
+ *   scatter-add gradient (dtable zeroed by the caller).  bucket < 0 writes
+ *   finfo(f32).min (a causally masked pair of the T5 decoder) and takes no gradient. */
 int vqa_image_to_nhwc8(const float* img, void* out, int n, int h, int w, hipStream_t stream);
 int vqa_image_to_s2d16(const float* img, void* out, int n, int h, int w, hipStream_t stream);
 int vqa_maxpool3x3s2_nhwc(const void* x, void* y, int n, int h, int w, int c, int oh, int ow, hipStream_t stream);
@@ -275,6 +283,31 @@ int vqa_t5_relbias_bwd(const float* dbias, const int* bucket, float* dtable, int
 int vqa_batch_sum(const float* x, int batch, long long n, float* out, float beta, hipStream_t stream);
 int vqa_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t stream);
 int vqa_zero(void* p, long long bytes, hipStream_t stream);
+
+/* ------------------------------------------------ config 4: ViT + T5 enc-dec ---
+ * VitVQAModel (model/vit_vqa_model.py:127-227) data movement (vit.hip):
+ * vqa_vit_patchify: ViTPatchEmbeddings' Conv2d(3, 768, 16, stride 16) as an im2col:
+ *   out[(b*np + p)][c*P*P + ky*P + kx] bf16 from NCHW fp32 pixel_values.
+ * vqa_gather_rows / vqa_scatter_rows: dst[r] = src[row(r)] / dst[row(r)] = src[r],
+ *   row(r) = idx ? idx[r] : offset + r*stride (stride 0 broadcasts one row); esz 2 or 4
+ *   bytes, 16-byte rows: the CLS token rows, encoder_outputs[:, 0, :] into the fusing
+ *   layer's concat (:189-195), the answer-token gather (:208-212) and its gradient.
+ * vqa_last_index: out[b] = b*len + max{j : mask[b, j] == 1} (0 if none), (:208).
+ * vqa_xattn1_fwd/bwd: the T5 decoder's EncDecAttention over its ONE encoder token
+ *   (encoder_hidden_states = fused.unsqueeze(1), :199-205): context[b*len + i, h*dh + e]
+ *   = drop(1)[b, h, i] * v[b, h*dh + e] (softmax over one key is 1; weight-dropout
+ *   element ((b*H + h)*len + i)); backward dv[b] = sum_i drop * dctx[b*len + i]
+ *   (query order); q and k get no gradient. */
+int vqa_vit_patchify(const float* img, void* out, int n, int h, int w, int patch, hipStream_t stream);
+int vqa_gather_rows(const void* src, long long lds, const long long* idx, long long stride, long long offset,
+                    void* dst, long long ldd, int rows, int cols, int esz, hipStream_t stream);
+int vqa_scatter_rows(const void* src, long long lds, const long long* idx, long long stride, long long offset,
+                     void* dst, long long ldd, int rows, int cols, int esz, hipStream_t stream);
+int vqa_last_index(const long long* mask, int batch, int len, long long* out, hipStream_t stream);
+int vqa_xattn1_fwd(const void* v, long long ldv, void* out, long long ldo, int batch, int len, int heads, int dh,
+                   const vqa_dropout* drop, hipStream_t stream);
+int vqa_xattn1_bwd(const void* dctx, long long ldd, float* dv32, void* dv16, int batch, int len, int heads, int dh,
+                   const vqa_dropout* drop, hipStream_t stream);
 
 /* ------------------------------------------------------------------ head ---
  * AttentionPooler (resnet_vqa_model.py:14-26) + classification_layer +

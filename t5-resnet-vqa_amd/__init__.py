@@ -19,7 +19,7 @@ import importlib
 
 from . import synthetic  # noqa: F401  (numpy only)
 
-_LAZY = ("lib", "ops", "engine", "layout", "model", "trainer", "dp", "data")
+_LAZY = ("lib", "ops", "engine", "layout", "model", "trainer", "dp", "data", "vit_model", "vit_engine")
 
 
 def __getattr__(name):

@@ -206,7 +206,12 @@ bool vqa_attn_mfma_ok(const vqa_attn_desc* d);           // attention_mfma.hip
 int vqa_attn_fwd_mfma(const vqa_attn_desc* d, hipStream_t s);
 int vqa_attn_bwd_mfma(const vqa_attn_desc* d, hipStream_t s);
 
+bool vqa_attn_long_ok(const vqa_attn_desc* d);
+int vqa_attn_fwd_long(const vqa_attn_desc* d, hipStream_t s);
+
 extern "C" int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t s) {
+  VQA_REQUIRE(d && d->q && d->k && d->v, "attention: null q/k/v");
+  if ((d->lq > 32 || d->lk > 64) && vqa_attn_long_ok(d)) return vqa_attn_fwd_long(d, s);   // ViT (config 4)
   AttnP P;
   if (int rc = fill(P, d)) return rc;
   VQA_REQUIRE(d->o, "vqa_attn_fwd: null output");

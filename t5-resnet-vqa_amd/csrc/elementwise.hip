@@ -332,7 +332,10 @@ __global__ __launch_bounds__(256) void relbias_fwd_kernel(const float* __restric
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= heads * lqk) return;
   const int h = i / lqk, p = i - h * lqk;
-  out[i] = table[bucket[p] * heads + h];
+  const int bk = bucket[p];
+  // bucket < 0: a causally masked (query, key) pair of the T5 decoder (the extended
+  // attention mask's finfo.min, TF modeling_t5 get_extended_attention_mask)
+  out[i] = bk < 0 ? -3.4028234663852886e38f : table[bk * heads + h];
 }
 
 // dtable[b, h] = sum over (i, j) with bucket(i, j) == b of dbias[h, i, j]:

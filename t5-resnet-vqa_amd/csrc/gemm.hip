@@ -26,7 +26,7 @@
 
 namespace {
 
-template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB>
+template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, bool EXT = false>
 __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, char* smem) {
   constexpr int NW = NWM * NWN, NT = 64 * NW;
   constexpr int WM = BM / NWM, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
@@ -186,13 +186,21 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
       }
   }
 
-  tile_epilogue<BM, BN, STAGES, NWM, NWN>(P, acc, z, m0, n0, P.m, smem);
+  tile_epilogue<BM, BN, STAGES, NWM, NWN, EXT>(P, acc, z, m0, n0, P.m, smem);
 }
 
 template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB>
 __global__ __launch_bounds__(64 * NWM * NWN) void gemm_kernel(GemmParams P) {
   __shared__ __attribute__((aligned(1024))) char smem[TileCfg<BM, BN, STAGES>::LDS];
   gemm_body<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB>(P, blockIdx.x, smem);
+}
+
+// GELU / tanh epilogues (vqa_gemm_desc.relu 2 / 3: the ViT intermediate and pooler of
+// config 4) in ONE tile config (64x128, 2 stages, k-contiguous A and B = X W^T), so the
+// extra epilogue code is not instantiated into every config
+__global__ __launch_bounds__(256) void gemm_ext_kernel(GemmParams P) {
+  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<64, 128, 2>::LDS];
+  gemm_body<64, 128, 2, 2, 2, true, true, false, false, true>(P, blockIdx.x, smem);
 }
 
 // Two independent problems in one launch (the backward's dX and dW of one
@@ -363,6 +371,9 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
   P.c16 = (bf16_t*)d->c16; P.ldc16 = d->ldc16;
   P.bias = d->bias; P.res32 = d->res32; P.res16 = (const bf16_t*)d->res16; P.ldres = d->ldres;
   P.mask16 = (const bf16_t*)d->mask16; P.ldmask = d->ldmask;
+  VQA_REQUIRE(d->relu >= 0 && d->relu <= 3, "vqa_gemm: activation must be 0..3");
+  VQA_REQUIRE(d->relu <= 1 || (!(d->drop.p > 0.f && d->drop.rng) && !d->mask16),
+              "vqa_gemm: GELU / tanh epilogues take no dropout or mask (act(k*t) != k*act(t))");
   P.alpha = d->alpha; P.beta = d->beta; P.relu = d->relu;
   P.ga = d->ga; P.gb = d->gb;
   P.sa = d->stride_a; P.sb = d->stride_b; P.sc32 = d->stride_c32; P.sc16 = d->stride_c16; P.sres = d->stride_res;
@@ -410,6 +421,14 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
     return conv_patch_dispatch(P, vqa_gemm_select(d), stream);
   }
   VQA_REQUIRE(!patch_cfg, "vqa_gemm: tile config %d is for a_conv = 2 only", cfg);
+  if (d->relu >= 2) {                                     // GELU / tanh: gemm_ext_kernel only
+    VQA_REQUIRE(akc && bkc && !d->a_conv && !d->b_conv && P.splitk <= 1,
+                "vqa_gemm: GELU / tanh epilogues need k-contiguous A and B, no conv operand, no split-K");
+    P.tiles_m = vqa::cdiv(P.m, 64);
+    P.tiles_n = vqa::cdiv(P.n, 128);
+    hipLaunchKernelGGL(gemm_ext_kernel, dim3(P.tiles_m * P.tiles_n, 1, batch), dim3(256), 0, stream, P);
+    return vqa::check_launch("vqa_gemm (ext epilogue)");
+  }
   if (akc && bkc && !d->a_conv) return dispatch_tile<true, true, false, false>(P, batch, cfg, stream);
   if (akc && bkc && d->a_conv) return dispatch_tile<true, true, true, false>(P, batch, cfg, stream);
   if (akc && !bkc && !d->a_conv && !d->b_conv) return dispatch_tile<true, false, false, false>(P, batch, cfg, stream);

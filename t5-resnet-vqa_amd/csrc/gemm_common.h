@@ -291,7 +291,25 @@ struct TileCfg {
 // acc[i][j][4g+t] -> row m0+wm*WM+i*32+(l&31), col n0+wn*WN+j*32+8g+4(l>>5)+t; rows at or
 // beyond `mlim` are not stored (the GEMMs pass P.m; the patch convolution the end of its
 // tile's valid output rows).
-template <int BM, int BN, int STAGES, int NWM, int NWN>
+// epilogue activation (vqa_gemm_desc.relu): 1 ReLU, 2 GELU (erf form, torch's default
+// nn.functional.gelu: ViT intermediate), 3 tanh (ViT pooler)
+// (EXT epilogues only -- one kernel instantiation, gemm_ext_kernel; compact branch-free
+// forms: erf by Abramowitz-Stegun 7.1.26, |error| < 1.5e-7, far below the bf16 rounding
+// of the output)
+__device__ __forceinline__ float epi_act(float v, int a) {
+  if (a == 1) return fmaxf(v, 0.f);
+  if (a == 2) {
+    const float x = v * 0.7071067811865476f, ax = fabsf(x);
+    const float t = 1.f / (1.f + 0.3275911f * ax);
+    const float y = 1.f - ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t +
+                           0.254829592f) * t * __expf(-ax * ax);
+    return 0.5f * v * (1.f + copysignf(y, x));
+  }
+  const float e = __expf(-2.f * fabsf(v));
+  return copysignf((1.f - e) / (1.f + e), v);
+}
+
+template <int BM, int BN, int STAGES, int NWM, int NWN, bool EXT = false>
 __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&acc)[BM / NWM / 32][BN / NWN / 32],
                                               const int z, const int m0, const int n0, const int mlim, char* smem) {
   constexpr int NW = NWM * NWN, NT = 64 * NW;
@@ -400,7 +418,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
         }
         if (P.relu) {
 #pragma unroll
-          for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+          for (int t = 0; t < 8; ++t) v[t] = EXT ? epi_act(v[t], P.relu) : fmaxf(v[t], 0.f);
         }
         if (C32) {
           float4* cp = reinterpret_cast<float4*>(C32 + (long)row * P.ldc32 + col);
@@ -441,7 +459,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
           float v = kf * (acc[i][j][e] * P.alpha + (BIAS ? BIAS[col] : 0.f));
           if (R32) v += R32[(long)row * P.ldres + col];
           if (R16) v += bf2f(R16[(long)row * P.ldres + col]);
-          if (P.relu) v = fmaxf(v, 0.f);
+          if (P.relu) v = EXT ? epi_act(v, P.relu) : fmaxf(v, 0.f);
           if (C32) {
             float* cp = C32 + (long)row * P.ldc32 + col;
             *cp = beta ? v + P.beta * *cp : v;

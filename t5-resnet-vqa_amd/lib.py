@@ -177,6 +177,12 @@ register("vqa_zero", P, c_ll)
 register("vqa_head_fwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_head_bwd", P, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_grad_sqnorm", P, c_ll, P, c_int)
+register("vqa_vit_patchify", P, P, c_int, c_int, c_int, c_int)
+register("vqa_gather_rows", P, c_ll, P, c_ll, c_ll, P, c_ll, c_int, c_int, c_int)
+register("vqa_scatter_rows", P, c_ll, P, c_ll, c_ll, P, c_ll, c_int, c_int, c_int)
+register("vqa_last_index", P, c_int, c_int, P)
+register("vqa_xattn1_fwd", P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, P)
+register("vqa_xattn1_bwd", P, c_ll, P, P, c_int, c_int, c_int, c_int, P)
 register("vqa_optim_finalize", P, c_int, c_float, c_float, c_int, c_int, c_float, c_float, P)
 
 
