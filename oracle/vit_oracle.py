@@ -144,10 +144,12 @@ def t5_decoder(sd, ids, mask, enc, drop=_nodrop, prefix="lang_model.decoder."):
     return drop(SITE_DEC_FINAL, t5_rmsnorm(h, g("final_layer_norm.weight")))
 
 
-def model_forward(sd, batch, drop=_nodrop):
-    """VitVQAModel.forward (:166-225) -> (log_probs, loss)."""
-    with torch.no_grad():
-        pooled = vit_pooled(sd, batch["pixel_values"])
+def model_forward(sd, batch, drop=_nodrop, pooled=None):
+    """VitVQAModel.forward (:166-225) -> (log_probs, loss).  `pooled` overrides the ViT's
+    pooled output (tests: isolating the frozen ViT's bf16 error from the trained part)."""
+    if pooled is None:
+        with torch.no_grad():
+            pooled = vit_pooled(sd, batch["pixel_values"])
     enc = t5_encoder(sd, batch["question_input_ids"], batch["question_attention_masks"], drop)
     cat = torch.cat([pooled, enc[:, 0, :]], dim=1)
     fused = drop(SITE_FUSE, F.relu(cat @ sd["fusing_layer.0.weight"].T + sd["fusing_layer.0.bias"]), FUSE_P)
@@ -189,14 +191,14 @@ class VitOracleTrainer:
         self.vmax = {k: torch.zeros_like(self.sd[k]) for k in self.keys}
         self.step_count = 0
 
-    def forward_backward(self, batch):
+    def forward_backward(self, batch, pooled=None):
         for k in self.keys:
             self.sd[k].grad = None
         drop = _nodrop
         if self.dropout > 0.0:
             self.rng_counter += 1
             drop = HashDropout(self.dropout, self.seed, self.rng_counter)
-        lp, loss = model_forward(self.sd, batch, drop=drop)
+        lp, loss = model_forward(self.sd, batch, drop=drop, pooled=pooled)
         loss.backward()
         for k in self.keys:                                       # parameters on the graph that got none
             if self.sd[k].grad is None:

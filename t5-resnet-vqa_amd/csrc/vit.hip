@@ -87,7 +87,8 @@ __global__ __launch_bounds__(256) void xattn1_fwd_kernel(const bf16_t* __restric
 // dv[b][c] = sum_i drop(b, h(c), i) * dctx[b*len + i][c], in query order (deterministic)
 __global__ __launch_bounds__(256) void xattn1_bwd_kernel(const bf16_t* __restrict__ dctx, long ldd,
                                                          float* __restrict__ dv32, bf16_t* __restrict__ dv16,
-                                                         int batch, int len, int heads, int dh, vqa_dropout drop) {
+                                                         long lddv, int batch, int len, int heads, int dh,
+                                                         vqa_dropout drop) {
   const int D = heads * dh;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)batch * D) return;
@@ -98,8 +99,8 @@ __global__ __launch_bounds__(256) void xattn1_bwd_kernel(const bf16_t* __restric
     const float m = dk.on ? drop_mul(dk, (uint32_t)(((long)b * heads + h) * len + q)) : 1.f;
     s += m * bf2f(dctx[((long)b * len + q) * ldd + c]);
   }
-  if (dv32) dv32[(long)b * D + c] = s;
-  if (dv16) dv16[(long)b * D + c] = f2bf(s);
+  if (dv32) dv32[(long)b * lddv + c] = s;
+  if (dv16) dv16[(long)b * lddv + c] = f2bf(s);
 }
 
 }  // namespace
@@ -158,13 +159,13 @@ extern "C" int vqa_xattn1_fwd(const void* v, long long ldv, void* out, long long
   return vqa::check_launch("vqa_xattn1_fwd");
 }
 
-extern "C" int vqa_xattn1_bwd(const void* dctx, long long ldd, float* dv32, void* dv16, int batch, int len,
-                              int heads, int dh, const vqa_dropout* drop, hipStream_t s) {
-  VQA_REQUIRE(dctx && (dv32 || dv16) && batch > 0 && len > 0 && heads > 0 && dh > 0,
+extern "C" int vqa_xattn1_bwd(const void* dctx, long long ldd, float* dv32, void* dv16, long long lddv, int batch,
+                              int len, int heads, int dh, const vqa_dropout* drop, hipStream_t s) {
+  VQA_REQUIRE(dctx && (dv32 || dv16) && batch > 0 && len > 0 && heads > 0 && dh > 0 && lddv >= heads * dh,
               "vqa_xattn1_bwd: bad arguments");
   vqa_dropout d = drop ? *drop : vqa_dropout{0.f, 0u, nullptr};
   const long total = (long)batch * heads * dh;
   hipLaunchKernelGGL(xattn1_bwd_kernel, dim3((unsigned)vqa::cdiv(total, 256)), dim3(256), 0, s,
-                     (const bf16_t*)dctx, (long)ldd, dv32, (bf16_t*)dv16, batch, len, heads, dh, d);
+                     (const bf16_t*)dctx, (long)ldd, dv32, (bf16_t*)dv16, (long)lddv, batch, len, heads, dh, d);
   return vqa::check_launch("vqa_xattn1_bwd");
 }

@@ -1333,7 +1333,7 @@ class VQAEngine:
                 d1.config, d2.config = _TUNE_CACHE[key] // 10, _TUNE_CACHE[key] % 10
                 chosen[key] = _TUNE_CACHE[key]
                 continue
-            if c.name != "vqa_gemm":
+            if c.name != "vqa_gemm" or c.desc.relu >= 2:        # GELU / tanh: one fixed kernel
                 continue
             d = c.desc
             key = repr(_gemm_key(d))

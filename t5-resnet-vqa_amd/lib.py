@@ -182,7 +182,7 @@ register("vqa_gather_rows", P, c_ll, P, c_ll, c_ll, P, c_ll, c_int, c_int, c_int
 register("vqa_scatter_rows", P, c_ll, P, c_ll, c_ll, P, c_ll, c_int, c_int, c_int)
 register("vqa_last_index", P, c_int, c_int, P)
 register("vqa_xattn1_fwd", P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, P)
-register("vqa_xattn1_bwd", P, c_ll, P, P, c_int, c_int, c_int, c_int, P)
+register("vqa_xattn1_bwd", P, c_ll, P, P, c_ll, c_int, c_int, c_int, c_int, P)
 register("vqa_optim_finalize", P, c_int, c_float, c_float, c_int, c_int, c_float, c_float, P)
 
 

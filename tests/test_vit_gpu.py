@@ -1,0 +1,214 @@
+"""BASELINE config 4 (VitVQAModel, ViT-base + T5 encoder-decoder) on the GPU: the new
+kernels against torch fp32 references, and the engine's train step against the
+reference's own fixture (eval mode, tests/golden/make_golden_vit.py) and the CPU
+oracle (train mode, hash dropout).  Measured errors go to the parity report."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "vit_model_b4_l16.npz")
+GROUPS = ("lang_model", "fusing_layer", "classification_layer")
+
+
+@pytest.fixture(scope="module")
+def cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+def test_long_attention_matches_torch(cuda, pkg, parity_report):
+    """vqa_attn_fwd at ViT's 197 tokens (online-softmax MFMA kernel) and a ragged length."""
+    L_, ops = pkg.lib, pkg.ops
+    errs = {}
+    for B, Lt, dh in ((2, 197, 64), (3, 70, 64), (1, 33, 96)):
+        H = 12 if dh == 64 else 8
+        g = torch.Generator().manual_seed(Lt)
+        qkv = torch.randn(B * Lt, 3 * H * dh, generator=g).cuda()
+        q16 = _bf(qkv)
+        o = torch.zeros(B * Lt, H * dh, dtype=torch.bfloat16, device="cuda")
+        d = L_.AttnDesc()
+        D = H * dh
+        d.q, d.ldq, d.k, d.ldk, d.v, d.ldv = q16.data_ptr(), 3 * D, q16.data_ptr() + 2 * D, 3 * D, \
+            q16.data_ptr() + 4 * D, 3 * D
+        d.o, d.ldo = o.data_ptr(), D
+        d.batch, d.heads, d.lq, d.lk, d.dh, d.scale = B, H, Lt, Lt, dh, dh ** -0.5
+        L_.check(L_.load().vqa_attn_fwd(__import__("ctypes").byref(d), L_.stream_handle()), "vqa_attn_fwd")
+        torch.cuda.synchronize()
+        x = q16.float().view(B, Lt, 3, H, dh)
+        qq, kk, vv = (x[:, :, j].transpose(1, 2) for j in range(3))
+        ref = (torch.softmax(qq @ kk.transpose(2, 3) * dh ** -0.5, -1) @ vv).transpose(1, 2).reshape(B * Lt, D)
+        err = float((o.float() - ref).abs().max() / ref.abs().max())
+        errs[f"{B}x{Lt}x{dh}"] = err
+        assert err <= 1e-2, (B, Lt, dh, err)
+    parity_report["vit_long_attention_rel"] = errs
+
+
+def test_gelu_tanh_epilogues(cuda, pkg):
+    ops = pkg.ops
+    g = torch.Generator().manual_seed(3)
+    x = _bf(torch.randn(300, 768, generator=g)).cuda()
+    w = _bf(torch.randn(512, 768, generator=g) * 0.05).cuda()
+    b = (torch.randn(512, generator=g) * 0.1).cuda()
+    for act, fn in ((2, torch.nn.functional.gelu), (3, torch.tanh)):
+        out = torch.zeros(300, 512, dtype=torch.float32, device="cuda")
+        d = ops.gemm_desc(x, w, 300, 512, 768, lda=768, ldb=768, c32=out, ldc32=512, bias=b, relu=act)
+        ops.gemm_call(d, [x, w, out, b])(pkg.lib.stream_handle())
+        torch.cuda.synchronize()
+        ref = fn(x.float() @ w.float().T + b)
+        assert float((out - ref).abs().max()) <= 2e-3, act
+
+
+def test_vit_data_movement_kernels(cuda, pkg):
+    L_ = pkg.lib
+    lib = L_.load()
+    s = L_.stream_handle()
+    g = torch.Generator().manual_seed(5)
+    img = torch.rand(2, 3, 64, 48, generator=g).cuda()
+    out = torch.zeros(2 * 4 * 3, 768, dtype=torch.bfloat16, device="cuda")
+    L_.check(lib.vqa_vit_patchify(img.data_ptr(), out.data_ptr(), 2, 64, 48, 16, s), "patchify")
+    ref = torch.nn.functional.unfold(img, 16, stride=16).transpose(1, 2).reshape(-1, 768)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref.to(torch.bfloat16))
+    # gather / scatter rows, last index
+    src = torch.randn(10, 64, generator=g).cuda()
+    idx = torch.tensor([3, 0, 9], dtype=torch.int64, device="cuda")
+    dst = torch.zeros(3, 64, device="cuda")
+    L_.check(lib.vqa_gather_rows(src.data_ptr(), 64, idx.data_ptr(), 0, 0, dst.data_ptr(), 64, 3, 64, 4, s), "g")
+    back = torch.zeros(10, 64, device="cuda")
+    L_.check(lib.vqa_scatter_rows(dst.data_ptr(), 64, None, 4, 1, back.data_ptr(), 64, 3, 64, 4, s), "s")
+    mask = torch.tensor([[1, 1, 0, 0], [1, 1, 1, 1], [0, 0, 0, 0]], dtype=torch.int64, device="cuda")
+    last = torch.zeros(3, dtype=torch.int64, device="cuda")
+    L_.check(lib.vqa_last_index(mask.data_ptr(), 3, 4, last.data_ptr(), s), "last")
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src[idx])
+    assert torch.equal(back[[1, 5, 9]], dst) and float(back[[0, 2, 3, 4, 6, 7, 8]].abs().sum()) == 0.0
+    assert last.tolist() == [1, 7, 8]
+    # single-token cross-attention, dropout off: broadcast and its query-order sum
+    v = _bf(torch.randn(2, 768, generator=g)).cuda()
+    ctx = torch.zeros(2 * 5, 768, dtype=torch.bfloat16, device="cuda")
+    L_.check(lib.vqa_xattn1_fwd(v.data_ptr(), 768, ctx.data_ptr(), 768, 2, 5, 12, 64, None, s), "xf")
+    dctx = _bf(torch.randn(10, 768, generator=g)).cuda()
+    dv = torch.zeros(2, 768, device="cuda")
+    L_.check(lib.vqa_xattn1_bwd(dctx.data_ptr(), 768, dv.data_ptr(), None, 768, 2, 5, 12, 64, None, s), "xb")
+    torch.cuda.synchronize()
+    assert torch.equal(ctx.view(2, 5, 768), v[:, None].expand(2, 5, 768))
+    assert torch.allclose(dv, dctx.float().view(2, 5, 768).sum(1), atol=1e-5)
+
+
+def test_vit_engine_matches_reference_golden(cuda, pkg, parity_report):
+    fix = np.load(GOLDEN, allow_pickle=False)
+    vm = pkg.vit_model
+    B, L = int(fix["B"]), int(fix["L"])
+    nb = vm.make_batch(B, L, seed=1)
+    eng = pkg.vit_engine.VitVQAEngine(vm.make_state_dict(seed=0), batch=B, seq_len=L, warmup=int(fix["warmup"]),
+                                      total=int(fix["total"]), dropout=0.0)
+    losses, norms, gnorms, lp_err, pool_err = [], [], [], None, None
+    for s in range(len(fix["losses"])):
+        lp, loss = eng.forward_backward(nb)
+        if s == 0:
+            lp_err = float(np.abs(lp - fix["log_probs"]).max())
+            pool = eng.vit_pooled().cpu().numpy()
+            pool_err = float(np.abs(pool - fix["vit_pooled"]).max() / np.abs(fix["vit_pooled"]).max())
+        gn = eng.group_grad_norms()
+        gnorms.append([gn[k] for k in GROUPS])
+        eng.optimizer_step()
+        torch.cuda.synchronize()
+        losses.append(loss)
+        norms.append(eng.last_grad_norm())
+    lrel = np.abs(np.array(losses) - fix["losses"]) / np.abs(fix["losses"])
+    nrel = np.abs(np.array(norms) - fix["grad_norms"]) / fix["grad_norms"]
+    grel = np.abs(np.array(gnorms) - fix["group_grad_norms"]) / fix["group_grad_norms"]
+    post = eng.state_dict()
+    init = vm.make_state_dict(seed=0)
+    serr = {}
+    for f, k in (("post_cls_w", "classification_layer.weight"), ("post_fuse_w", "fusing_layer.0.weight"),
+                 ("post_dec_wi0", "lang_model.decoder.block.0.layer.2.DenseReluDense.wi.weight"),
+                 ("post_dec_xv0", "lang_model.decoder.block.0.layer.1.EncDecAttention.v.weight"),
+                 ("post_enc_q0", "lang_model.encoder.block.0.layer.0.SelfAttention.q.weight")):
+        du = post[k][:4, :16].astype(np.float64) - init[k][:4, :16]
+        dr = fix[f].astype(np.float64) - init[k][:4, :16]
+        serr[f] = float(np.linalg.norm(du - dr) / max(np.linalg.norm(dr), 1e-30))
+    # A/B: the CPU oracle fed the engine's own (bf16) ViT pooled output -- what is left is the
+    # trained part's error; the rest is the frozen ViT's bf16 forward (12 pre-LN layers)
+    from oracle import vit_oracle as orc
+    ot = orc.VitOracleTrainer(vm.make_state_dict(seed=0), warmup=int(fix["warmup"]), total=int(fix["total"]))
+    tb = {k: (None if v is None else torch.as_tensor(v)) for k, v in nb.items()}
+    eng0 = pkg.vit_engine.VitVQAEngine(vm.make_state_dict(seed=0), batch=B, seq_len=L, dropout=0.0)
+    lp0, loss0 = eng0.forward_backward(nb)
+    olp, oloss = ot.forward_backward(tb, pooled=eng0.vit_pooled().cpu())
+    og = ot.group_grad_norms()
+    g0 = eng0.group_grad_norms()
+    grads = {k: (ot.sd[k].grad.numpy() if ot.sd[k].grad is not None else np.zeros(tuple(ot.sd[k].shape), np.float32))
+             for k in ot.sd if not k.startswith("vision_model.")}
+    go = eng0.lay.pack(grads)
+    ge = eng0.G32.cpu().numpy()
+    ab = {"log_prob_max_abs": float(np.abs(lp0 - olp.numpy()).max()),
+          "loss_rel": abs(loss0 - float(oloss)) / float(oloss),
+          "group_grad_norm_rel": {k: abs(g0[k] - og[k]) / og[k] for k in GROUPS},
+          "gradient_rel_l2": float(np.linalg.norm(ge - go) / np.linalg.norm(go))}
+    del eng0
+    parity_report["vit_golden_b4_l16"] = {
+        "with_engine_vit_pooled": ab,
+        "vit_pooled_rel": pool_err, "log_prob_max_abs": lp_err, "loss_rel": lrel.tolist(),
+        "grad_norm_rel": nrel.tolist(), "group_grad_norm_rel_per_step": [dict(zip(GROUPS, r)) for r in grel.tolist()],
+        "post_slice_err_over_update": serr}
+    # the frozen ViT in bf16 (pooled max-abs 1.2e-2 of its max, measured) moves the fused token
+    # and with it every downstream gradient: step 0 grad norms 4-6e-3 (measured); with the
+    # engine's own pooled output the oracle agrees to the ResNet path's level (A/B above)
+    assert pool_err <= 2e-2, pool_err
+    assert lp_err <= 2e-2, lp_err
+    assert lrel[0] <= 1e-3 and nrel[0] <= 1e-2, (lrel, nrel)
+    assert (grel[0] <= 1e-2).all(), dict(zip(GROUPS, grel[0]))
+    assert ab["log_prob_max_abs"] <= 2e-2 and ab["loss_rel"] <= 1e-3, ab
+    # at B = 4 the T5 gradient enters through 4 answer rows and 4 CLS rows only, so the bf16
+    # rounding does not average out (group norms 5e-3 at B = 4, 1.5e-3 at B = 32, measured
+    # with tools/vit_grad_diag.py); the whole gradient vector: relative L2 5.3e-2 at both
+    # (cosine 0.9986), the bf16-vs-fp32 floor of the path (ReLU units within rounding of 0)
+    assert max(ab["group_grad_norm_rel"].values()) <= 1e-2, ab
+    assert ab["gradient_rel_l2"] <= 0.1, ab
+    # after two AdamW updates (lr up to 5e-3 on T5): m / sqrt(v) turns near-zero gradients'
+    # rounding into O(lr) update differences
+    assert (lrel <= 1e-2).all() and (nrel <= 5e-2).all(), (lrel, nrel)
+    assert max(serr.values()) <= 0.5, serr
+
+
+def test_vit_engine_vs_oracle_train_mode(cuda, pkg, parity_report):
+    """Dropout on (p = 0.1 at the T5 sites, 0.5 at the fusing layer), masks from the shared
+    counter hash; two steps, the second through a captured graph."""
+    from oracle import vit_oracle as orc
+    vm = pkg.vit_model
+    B, L, Ld = 3, 24, 12
+    sd = vm.make_state_dict(seed=4)
+    eng = pkg.vit_engine.VitVQAEngine(sd, batch=B, seq_len=L, dec_len=Ld, warmup=1, total=40, dropout=0.1, seed=9)
+    ot = orc.VitOracleTrainer(sd, warmup=1, total=40, dropout=0.1, seed=9)
+    rec = []
+    for step in range(2):
+        nb = vm.make_batch(B, L, dec_len=Ld, seed=20 + step)
+        tb = {k: (None if v is None else torch.as_tensor(v)) for k, v in nb.items()}
+        if step == 0:
+            lp, loss = eng.forward_backward(nb)
+            eng.optimizer_step()
+        else:
+            eng.load_batch(nb)
+            eng.capture()
+            eng.train_step()
+            torch.cuda.synchronize()
+            lp, loss = eng.LOGP.cpu().numpy(), float(eng.LOSS.item())
+        olp, oloss, ogn = ot.train_one_step(tb)
+        torch.cuda.synchronize()
+        rec.append({"log_prob_max_abs": float(np.abs(lp - olp.numpy()).max()),
+                    "loss_rel": abs(loss - float(oloss)) / abs(float(oloss)),
+                    "grad_norm_rel": abs(eng.last_grad_norm() - float(ogn)) / float(ogn)})
+    parity_report["vit_oracle_train_mode"] = rec
+    for step, r in enumerate(rec):
+        assert r["log_prob_max_abs"] <= 2e-2 * (1 + step), (step, r)
+        assert r["loss_rel"] <= 1e-3 * (1 + 2 * step), (step, r)
+        # B = 3: the gradient enters through 3 answer rows (see the golden test: measured 4.6e-3)
+        assert r["grad_norm_rel"] <= 1e-2 * (1 + step), (step, r)
