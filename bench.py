@@ -58,6 +58,83 @@ def cpu_baseline(pkg, batch=64, steps=5, warm=2):
                       f"({t:.2f} s/step), torch CPU {threads} threads"}
 
 
+def vit_flop_per_pair(lq, ld, nv=197, d=768, dff=3072, vff=3072, layers=12):
+    """Algorithmic FLOPs of one config-4 pair (VitVQAModel, vit_vqa_model.py:166-225): the frozen
+    ViT forward, the T5 encoder and decoder forward + backward (x3: the input and weight
+    gradients), the fusing layer and classifier (2 FLOP per multiply-add)."""
+    vit = 2 * (nv - 1) * d * d + layers * (2 * nv * d * 3 * d + 4 * nv * nv * d + 2 * nv * d * d
+                                           + 4 * nv * d * vff) + 2 * d * d
+    enc = layers * (2 * lq * d * 3 * d + 4 * lq * lq * d + 2 * lq * d * d + 4 * lq * d * dff)
+    dec = layers * (2 * ld * d * 3 * d + 4 * ld * ld * d + 2 * ld * d * d + 2 * d * d + 2 * ld * d * d
+                    + 4 * ld * d * dff)
+    head = 2 * 2 * d * d + 2 * d * 170
+    return float(vit + 3 * (enc + dec + head))
+
+
+def bench_vit(args, pkg, dev):
+    """BASELINE configs[3]: ViT-base + T5-base encoder-decoder (VitVQAModel) train step, 1 GPU."""
+    B, L, Ld = args.batch, args.seq_len, 20
+    vm = pkg.vit_model
+    eng = pkg.vit_engine.VitVQAEngine(vm.make_state_dict(seed=0), batch=B, seq_len=L, dec_len=Ld, device=dev,
+                                      warmup=10, total=100000, dropout=0.1)
+    pool = [{k: (None if v is None else torch.as_tensor(v).to(dev)) for k, v in
+             vm.make_batch(B, L, dec_len=Ld, seed=1 + i).items()} for i in range(4)]
+    eng.load_batch(pool[0])
+    eng.forward()
+    eng.backward()
+    eng.autotune(table=args.tune_table, save=args.tune_save)
+    if not args.no_graph:
+        eng.capture()
+
+    def step(i):
+        eng.load_batch(pool[i % len(pool)])
+        eng.train_step()
+    for i in range(args.warmup):
+        step(i)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(i)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    gpu_step = ev0.elapsed_time(ev1) * 1e-3 / args.steps
+    fpp = vit_flop_per_pair(L, Ld)
+    tf = fpp * B / gpu_step / 1e12
+    out = {"metric": "question-image pairs/sec, ViT-base+T5-base encoder-decoder train step (BASELINE configs[3])",
+           "value": round(B * args.steps / dt, 2), "unit": "pairs/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+           "config": {"workload": "VitVQAModel train step (vit_vqa_model.py:127-227), BASELINE configs[3]",
+                      "model": "vit-base-patch16-224 (frozen) + t5-base encoder-decoder", "global_batch": B,
+                      "seq_len": L, "dec_len": Ld, "image_size": 224, "answers": 170, "parallelism": "dp1",
+                      "graph": not args.no_graph},
+           "roofline": {"bound": "mfma", "kernel": "whole train step (one hipGraph replay)",
+                        "achieved": round(tf, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(tf / MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                        "flop_per_step": fpp * B, "step_gpu_ms": round(gpu_step * 1e3, 4)},
+           "loss": round(float(eng.LOSS.item()), 5), "grad_norm": round(eng.last_grad_norm(), 4)}
+    if not args.no_cpu_baseline:
+        from oracle import vit_oracle as orc
+        cb, steps, warm = 16, 3, 1
+        tr = orc.VitOracleTrainer(vm.make_state_dict(seed=0), warmup=10, total=1000, dropout=0.1)
+        nb = {k: (None if v is None else torch.as_tensor(v)) for k, v in vm.make_batch(cb, L, dec_len=Ld).items()}
+        times = []
+        for i in range(warm + steps):
+            t1 = time.perf_counter()
+            tr.train_one_step(nb)
+            if i >= warm:
+                times.append(time.perf_counter() - t1)
+        t = float(np.median(times))
+        out["cpu_baseline"] = {"value": round(cb / t, 3), "unit": "pairs/s", "cores": torch.get_num_threads(),
+                               "kind": "port", "sample": f"config-4 oracle fp32 train step, B={cb}, L={L}, Ld={Ld}, "
+                                                         f"224x224, median of {steps} after {warm} ({t:.2f} s/step)"}
+    print(json.dumps(out), flush=True)
+
+
 def spawn_ranks(n):
     """Start n ranks of this script (one per GPU) with a torchrun-style environment;
     called before any GPU call, so no process here ever initialises the GPU."""
@@ -107,6 +184,8 @@ def main():
     ap.add_argument("--tune-table", default=os.path.join(ROOT, "t5-resnet-vqa_amd", "tuning", "gemm_gfx950.json"),
                     help="measured GEMM tile choices (missing shapes are timed at start-up)")
     ap.add_argument("--tune-save", default=None, help="write the tile choices used to this file")
+    ap.add_argument("--model", choices=("resnet", "vit"), default="resnet",
+                    help="vit: BASELINE configs[3], ViT-base + T5 encoder-decoder (1 GPU)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -119,6 +198,11 @@ def main():
         raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.model == "vit":
+        if world != 1:
+            raise SystemExit("bench --model vit: BASELINE configs[3] is a 1-GPU configuration")
+        bench_vit(args, load_package(), dev)
+        return
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -150,6 +150,11 @@ class ResnetVQAModel:
         if tuple(image_tensors.shape) != want_i:
             raise ValueError(f"image_tensors shape {tuple(image_tensors.shape)} != planned {want_i}")
 
+    def load_items(self, items):
+        """The reference collate's batch dict (the keys train_one_step passes on)."""
+        self.load_batch(items["question_input_ids"], items["question_attention_masks"], items["image_tensors"],
+                        items.get("annotation_ids"))
+
     def load_batch(self, question_input_ids, question_attention_masks, image_tensors, annotation_ids=None):
         self._check_batch(question_input_ids, image_tensors)
         self.engine.load_batch({"question_input_ids": question_input_ids,
@@ -210,6 +215,145 @@ class ResnetVQAModel:
     def configure_optimizer(self, **kw):
         """Optimizer / schedule settings (trainer._init_optimizer); kept on the model so a
         later load_state_dict rebuilds the engine with them."""
+        self._optim_cfg = dict(getattr(self, "_optim_cfg", None) or {}, **kw)
+        self.engine.configure_optimizer(**kw)
+
+    def parameters_count(self):
+        return self.engine.lay.num_params
+
+
+VIT_NAMES = ("google/vit-base-patch16-224-in21k",)
+
+
+class _VitGroup(ParameterGroup):
+    """ParameterGroup over the config-4 engine (the ViT trainer's groups, vit_vqa_trainer.py:300-316)."""
+
+    def _keys(self):
+        from . import vit_model as VM
+        return [k for k in VM.model_specs(self._model.answer_spaces, self._model.image_size)
+                if k.startswith(self.prefix + ".")]
+
+    def __len__(self):
+        return len(self._keys())
+
+
+class VitVQAModel:
+    """`VitVQAModel` (model/vit_vqa_model.py:127-351) -- BASELINE config 4 -- over
+    `vit_engine.VitVQAEngine`: the same constructor names, `forward(**batch)` ->
+    (log_probs, loss), `generate_answers`, the reference state-dict keys and the
+    sub-modules the ViT trainer reads (`vision_model`, `lang_model`, `fusing_layer`,
+    `classification_layer`).  Shapes are fixed at construction (batch, question and
+    decoder lengths, image size), as for ResnetVQAModel."""
+
+    def __init__(self, vision_model_name="google/vit-base-patch16-224-in21k", language_model_name="t5-base",
+                 answer_spaces=170, fine_tune_lm_encoder=True, fine_tune_lm_decoder=True, fine_tune_vision=True,
+                 device="cuda", *, batch_size=64, seq_len=32, dec_len=20, image_size=224, state_dict=None, seed=0,
+                 dropout=0.1, dropout_seed=0):
+        from . import vit_model as VM
+        if vision_model_name not in VIT_NAMES:
+            raise ValueError(f"vision_model_name {vision_model_name!r}: this path supports {VIT_NAMES}")
+        if language_model_name != "t5-base":
+            raise ValueError("language_model_name must be 't5-base' (vit_vqa_model.py:146-147)")
+        self.vision_model_name, self.language_model_name = vision_model_name, language_model_name
+        self.answer_spaces, self.device = int(answer_spaces), torch.device(device)
+        self.batch_size, self.seq_len, self.dec_len, self.image_size = int(batch_size), int(seq_len), int(dec_len), \
+            int(image_size)
+        self.num_beams, self.max_answer_length = 2, 5                   # :163-164 (beam search is not wired)
+        self._cfg = dict(dropout=float(dropout), seed=int(dropout_seed))
+        if state_dict is None:
+            state_dict = VM.make_state_dict(seed=seed, answer_spaces=self.answer_spaces, image=self.image_size)
+        self._build(state_dict)
+        self.training = True
+        self.vision_model = _VitGroup(self, "vision_model", trainable=False)
+        self.lang_model = _VitGroup(self, "lang_model")
+        self.fusing_layer = _VitGroup(self, "fusing_layer")
+        self.classification_layer = _VitGroup(self, "classification_layer")
+
+    def _build(self, state_dict):
+        from . import vit_model as VM
+        from .vit_engine import VitVQAEngine
+        sd = {k: (v.detach().cpu().float().numpy() if isinstance(v, torch.Tensor) else np.asarray(v))
+              for k, v in state_dict.items()}
+        if "lang_model.shared.weight" in sd:
+            for k in VM.TIED:
+                sd.setdefault(k, sd["lang_model.shared.weight"])
+        missing = [k for k in VM.model_specs(self.answer_spaces, self.image_size) if k not in sd]
+        if missing:
+            raise KeyError(f"state_dict lacks {len(missing)} reference keys, e.g. {missing[:3]}")
+        self.engine = VitVQAEngine(sd, batch=self.batch_size, seq_len=self.seq_len, dec_len=self.dec_len,
+                                   image_size=self.image_size, device=self.device, answer_spaces=self.answer_spaces,
+                                   **self._cfg)
+
+    def train(self, mode=True):
+        self.training = bool(mode)
+        self.engine.set_training(self.training)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def load_items(self, items):
+        """The ViT collate's batch dict (dataset_utils/vit_vqa_daquar_dataset.py:168-195)."""
+        want = {"pixel_values": (self.batch_size, 3, self.image_size, self.image_size),
+                "question_input_ids": (self.batch_size, self.seq_len),
+                "decoder_question_input_ids": (self.batch_size, self.dec_len)}
+        for k, shape in want.items():
+            if items.get(k) is None or tuple(items[k].shape) != shape:
+                raise ValueError(f"{k}: expected shape {shape}")
+        self.engine.load_batch(items)
+
+    def forward(self, question_input_ids, decoder_question_input_ids=None, question_attention_masks=None,
+                decoder_question_attention_masks=None, annotation_ids=None, pixel_values=None, image_tensors=None,
+                answer_input_ids=None, answer_attention_masks=None, question_type_ids=None):
+        """vit_vqa_model.py:166-225 -> (log_probs, loss); loss is None without annotation_ids."""
+        self.load_items({"question_input_ids": question_input_ids, "question_attention_masks": question_attention_masks,
+                         "decoder_question_input_ids": decoder_question_input_ids,
+                         "decoder_question_attention_masks": decoder_question_attention_masks,
+                         "pixel_values": pixel_values, "annotation_ids": annotation_ids})
+        self.engine.forward()
+        return self.engine.LOGP.clone(), (self.engine.LOSS[0].clone() if annotation_ids is not None else None)
+
+    __call__ = forward
+
+    def generate_answers(self, question_input_ids, decoder_question_input_ids=None, question_attention_masks=None,
+                         decoder_question_attention_masks=None, pixel_values=None, image_tensors=None,
+                         answer_input_ids=None, answer_attention_masks=None, annotation_ids=None,
+                         question_type_ids=None):
+        """:229-290 -> (log_probs, loss or None, attention_tensors).  The ViT's attention
+        probabilities (output_attentions=True, read only by the heat-map script) are never
+        materialised by the online-softmax attention kernel: attention_tensors is None."""
+        lp, loss = self.forward(question_input_ids, decoder_question_input_ids, question_attention_masks,
+                                decoder_question_attention_masks, annotation_ids, pixel_values)
+        return lp, loss, None
+
+    @staticmethod
+    def convert_logits_to_predictions(lm_logits):
+        return torch.argmax(torch.exp(lm_logits), dim=1)
+
+    @staticmethod
+    def trainer_group_lr(optimizer_kwargs):
+        """vit_vqa_trainer.py:300-316: lang_model at lm_encoder_lr, fusing and classifier layers
+        at classifier_lr (the vision group gets no gradient)."""
+        c = float(optimizer_kwargs.get("classifier_lr", 1e-5))
+        return {"lang_model": float(optimizer_kwargs.get("lm_encoder_lr", 5e-3)), "fusing_layer": c,
+                "classification_layer": c}
+
+    def state_dict(self):
+        return {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in self.engine.state_dict().items()}
+
+    def load_state_dict(self, state_dict, strict=True):
+        sd = dict(state_dict)
+        if not strict:
+            cur = self.state_dict()
+            cur.update({k: v for k, v in sd.items() if k in cur})
+            sd = cur
+        training = self.training
+        self._build(sd)
+        if getattr(self, "_optim_cfg", None):
+            self.engine.configure_optimizer(**self._optim_cfg)
+        self.train(training)
+
+    def configure_optimizer(self, **kw):
         self._optim_cfg = dict(getattr(self, "_optim_cfg", None) or {}, **kw)
         self.engine.configure_optimizer(**kw)
 

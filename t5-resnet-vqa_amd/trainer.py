@@ -32,6 +32,7 @@ rank's own (its batch), the clip norm is the global one.
 """
 from __future__ import annotations
 
+import inspect
 import time
 
 import torch
@@ -57,6 +58,9 @@ class VQATrainer:
             data_parallel = (torch.distributed.is_available() and torch.distributed.is_initialized()
                              and torch.distributed.get_world_size(process_group) > 1)
         self.data_parallel = bool(data_parallel)
+        if self.data_parallel and not hasattr(model.engine, "ready_marks"):
+            raise ValueError("data parallel training is planned for ResnetVQAModel (BASELINE configs[2]); "
+                             "the ViT configuration (configs[3]) is a single-GPU one")
         self.process_group, self.bucket_mb = process_group, int(bucket_mb)
         self._dp = None
         if self.data_parallel and model.engine.t5_dw_groups != list(dp.DP_T5_DW_GROUPS):
@@ -68,9 +72,12 @@ class VQATrainer:
         warm = self.num_training_steps // 10 if warm == -1 else int(warm)
         warm = min(warm, int(lr_scheduler_kwargs.get("max_warmup_steps", warm)))
         self.num_warmup_steps = warm
-        group_lr = {"lang_model": float(optimizer_kwargs.get("lm_encoder_lr", 5e-3)),
-                    "scaler": HARD_CODED_LR, "sga_modules": HARD_CODED_LR, "attention_pooler": HARD_CODED_LR,
-                    "classification_layer": float(optimizer_kwargs.get("classifier_lr", 1e-5))}
+        if hasattr(model, "trainer_group_lr"):             # VitVQAModel: the ViT trainer's groups
+            group_lr = model.trainer_group_lr(optimizer_kwargs)
+        else:
+            group_lr = {"lang_model": float(optimizer_kwargs.get("lm_encoder_lr", 5e-3)),
+                        "scaler": HARD_CODED_LR, "sga_modules": HARD_CODED_LR, "attention_pooler": HARD_CODED_LR,
+                        "classification_layer": float(optimizer_kwargs.get("classifier_lr", 1e-5))}
         model.configure_optimizer(group_lr=group_lr, warmup=warm, total=self.num_training_steps,
                                          max_norm=float(gradient_clipping or 0.0),
                                          weight_decay=float(kw.get("weight_decay", 1e-2)),
@@ -84,8 +91,7 @@ class VQATrainer:
         m = self.model
         if not m.training:
             m.train()
-        m.load_batch(data_items["question_input_ids"], data_items["question_attention_masks"],
-                     data_items["image_tensors"], data_items["annotation_ids"])
+        m.load_items(data_items)
         e = m.engine
         if self.data_parallel:
             if self._dp is None:
@@ -105,8 +111,8 @@ class VQATrainer:
         m = self.model
         was = m.training
         m.eval()
-        lp, loss = m(**{k: data_items.get(k) for k in ("question_input_ids", "question_attention_masks",
-                                                      "image_tensors", "annotation_ids")})
+        names = inspect.signature(m.forward).parameters
+        lp, loss = m(**{k: v for k, v in data_items.items() if k in names})
         m.train(was)
         return (float(loss) if loss is not None else None), lp
 

@@ -585,6 +585,27 @@ class VitVQAEngine:
         sd.update(self.lay.unpack(self.P32.cpu().numpy()))
         return {k: sd[k] for k in VM.model_specs(self.A, self.H)}
 
+    def param_view(self, key):
+        """(parameter, gradient) views of reference entry `key` in the flat arenas (the tied
+        embedding keys all alias the `embed` segment); None for frozen / unknown keys."""
+        specs = VM.model_specs(self.A, self.H)
+        if key in VM.TIED:
+            key = "lang_model.shared.weight"
+        for sg in self.lay.segments.values():
+            if key not in sg.parts:
+                continue
+            p32, g32 = self.p32[sg.name], self.g32[sg.name]
+            row = 0
+            for part in sg.parts:
+                n = specs[part][0]
+                if part == key:
+                    return p32[row:row + n].view(specs[key]), g32[row:row + n].view(specs[key])
+                row += n
+        return None
+
+    def refresh_shadow(self):
+        self.P16.copy_(self.P32)
+
     def vit_pooled(self):
         """pooler_output of the frozen ViT for the current batch ([B, 768], from its bf16 copy)."""
         return self.CAT16[:, :D].float()

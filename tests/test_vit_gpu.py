@@ -50,15 +50,16 @@ def test_long_attention_matches_torch(cuda, pkg, parity_report):
     parity_report["vit_long_attention_rel"] = errs
 
 
-def test_gelu_tanh_epilogues(cuda, pkg):
+@pytest.mark.parametrize("m,n,k", [(300, 512, 768), (8192, 4096, 256)])     # 64x128 / 256x256 kernels
+def test_gelu_tanh_epilogues(cuda, pkg, m, n, k):
     ops = pkg.ops
     g = torch.Generator().manual_seed(3)
-    x = _bf(torch.randn(300, 768, generator=g)).cuda()
-    w = _bf(torch.randn(512, 768, generator=g) * 0.05).cuda()
-    b = (torch.randn(512, generator=g) * 0.1).cuda()
+    x = _bf(torch.randn(m, k, generator=g)).cuda()
+    w = _bf(torch.randn(n, k, generator=g) * 0.05).cuda()
+    b = (torch.randn(n, generator=g) * 0.1).cuda()
     for act, fn in ((2, torch.nn.functional.gelu), (3, torch.tanh)):
-        out = torch.zeros(300, 512, dtype=torch.float32, device="cuda")
-        d = ops.gemm_desc(x, w, 300, 512, 768, lda=768, ldb=768, c32=out, ldc32=512, bias=b, relu=act)
+        out = torch.zeros(m, n, dtype=torch.float32, device="cuda")
+        d = ops.gemm_desc(x, w, m, n, k, lda=k, ldb=k, c32=out, ldc32=n, bias=b, relu=act)
         ops.gemm_call(d, [x, w, out, b])(pkg.lib.stream_handle())
         torch.cuda.synchronize()
         ref = fn(x.float() @ w.float().T + b)
@@ -212,3 +213,36 @@ def test_vit_engine_vs_oracle_train_mode(cuda, pkg, parity_report):
         assert r["loss_rel"] <= 1e-3 * (1 + 2 * step), (step, r)
         # B = 3: the gradient enters through 3 answer rows (see the golden test: measured 4.6e-3)
         assert r["grad_norm_rel"] <= 1e-2 * (1 + step), (step, r)
+
+
+def test_vit_model_api_and_trainer(cuda, pkg, tmp_path):
+    """The VitVQAModel mirror: forward(**batch), generate_answers, state_dict round trip through
+    torch.save / torch.load(weights_only=True), and VQATrainer steps with the ViT groups."""
+    vm = pkg.vit_model
+    B, L, Ld = 2, 16, 12
+    model = pkg.model.VitVQAModel(answer_spaces=170, batch_size=B, seq_len=L, dec_len=Ld, dropout=0.1)
+    nb = {k: (None if v is None else torch.as_tensor(v).cuda()) for k, v in
+          vm.make_batch(B, L, dec_len=Ld, seed=3).items()}
+    model.eval()
+    lp, loss = model(**nb)
+    lp2, loss2, att = model.generate_answers(**nb)
+    assert torch.equal(lp, lp2) and float(loss) == float(loss2) and att is None
+    assert model.convert_logits_to_predictions(lp).shape == (B,)
+    names = [n for n, _ in model.lang_model.named_parameters()]
+    assert "shared.weight" in names and "decoder.block.0.layer.1.EncDecAttention.v.weight" in names
+    path = tmp_path / "vit.pt"
+    torch.save(model.state_dict(), path)
+    sd = torch.load(path, weights_only=True)
+    model2 = pkg.model.VitVQAModel(batch_size=B, seq_len=L, dec_len=Ld, state_dict=sd)
+    model2.eval()
+    lp3, _ = model2(**nb)
+    assert torch.equal(lp, lp3)
+    model.train()
+    tr = pkg.trainer.VQATrainer(model, {"type": "AdamW", "lm_encoder_lr": 1e-4, "classifier_lr": 1e-4,
+                                        "kwargs": {"weight_decay": 0.1, "amsgrad": True}},
+                                {"num_warmup_steps": 1}, num_training_steps=10, logger=None)
+    l0, _ = tr.train_one_step(nb)
+    l1, _ = tr.train_one_step(nb)
+    assert np.isfinite(l0) and np.isfinite(l1) and tr.grad_norm() > 0
+    res = tr.valid_one_epoch([nb])
+    assert 0.0 <= res["accuracy"] <= 1.0 and len(res["predictions"]) == B
