@@ -196,9 +196,9 @@ __global__ __launch_bounds__(64 * NWM * NWN) void gemm_kernel(GemmParams P) {
 }
 
 // GELU / tanh epilogues (vqa_gemm_desc.relu 2 / 3: the ViT intermediate and pooler of
-// config 4) in two tile configs (64x128 4 waves; 256x256 8 waves for grids of >= 512 such
-// tiles: the ViT intermediate), k-contiguous A and B = X W^T, so the extra epilogue code
-// is not instantiated into every config
+// config 4) in ONE tile config (64x128, 2 stages, k-contiguous A and B = X W^T), so the
+// extra epilogue code is not instantiated into every config (a 256x256 variant measured
+// 1 ms slower per config-4 step: 600 tiles leave 2.3 rounds per CU)
 template <int BM, int BN, int NWM, int NWN>
 __global__ __launch_bounds__(64 * NWM * NWN) void gemm_ext_kernel(GemmParams P) {
   __shared__ __attribute__((aligned(1024))) char smem[TileCfg<BM, BN, 2>::LDS];
@@ -426,18 +426,10 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   if (d->relu >= 2) {                                     // GELU / tanh: gemm_ext_kernel only
     VQA_REQUIRE(akc && bkc && !d->a_conv && !d->b_conv && P.splitk <= 1,
                 "vqa_gemm: GELU / tanh epilogues need k-contiguous A and B, no conv operand, no split-K");
-    const long big = (long)vqa::cdiv(P.m, 256) * vqa::cdiv(P.n, 256) * batch;
-    if (big >= 512) {
-      P.tiles_m = vqa::cdiv(P.m, 256);
-      P.tiles_n = vqa::cdiv(P.n, 256);
-      hipLaunchKernelGGL((gemm_ext_kernel<256, 256, 2, 4>), dim3(P.tiles_m * P.tiles_n, 1, batch), dim3(512), 0,
-                         stream, P);
-    } else {
-      P.tiles_m = vqa::cdiv(P.m, 64);
-      P.tiles_n = vqa::cdiv(P.n, 128);
-      hipLaunchKernelGGL((gemm_ext_kernel<64, 128, 2, 2>), dim3(P.tiles_m * P.tiles_n, 1, batch), dim3(256), 0,
-                         stream, P);
-    }
+    P.tiles_m = vqa::cdiv(P.m, 64);
+    P.tiles_n = vqa::cdiv(P.n, 128);
+    hipLaunchKernelGGL((gemm_ext_kernel<64, 128, 2, 2>), dim3(P.tiles_m * P.tiles_n, 1, batch), dim3(256), 0, stream,
+                       P);
     return vqa::check_launch("vqa_gemm (ext epilogue)");
   }
   if (akc && bkc && !d->a_conv) return dispatch_tile<true, true, false, false>(P, batch, cfg, stream);

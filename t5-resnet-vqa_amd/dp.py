@@ -137,6 +137,7 @@ class DataParallelStep:
 
     def capture(self):
         e = self.eng
+        e.flush_optimizer()              # the warm-up's backward must not overwrite a pending update's G
         s = torch.cuda.Stream(e.dev)
         s.wait_stream(torch.cuda.current_stream(e.dev))
         saved_rng = e.RNG.clone()

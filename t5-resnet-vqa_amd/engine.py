@@ -1232,6 +1232,7 @@ class VQAEngine:
     def capture(self, warm=True):
         """Capture the step as hipGraph(s): one graph when single-GPU; with a DP
         all-reduce hook, graph(fwd+bwd) -> eager collective -> graph(optimizer)."""
+        self.flush_optimizer()           # the warm-up's backward must not overwrite a pending update's G
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         saved, saved_rng = self.opt_state.clone(), self.RNG.clone()
