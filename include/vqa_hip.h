@@ -297,7 +297,7 @@ int vqa_zero(void* p, long long bytes, hipStream_t stream);
  *   (encoder_hidden_states = fused.unsqueeze(1), :199-205): context[b*len + i, h*dh + e]
  *   = drop(1)[b, h, i] * v[b, h*dh + e] (softmax over one key is 1; weight-dropout
  *   element ((b*H + h)*len + i)); backward dv[b] = sum_i drop * dctx[b*len + i]
- *   (query order); q and k get no gradient. */
+ *   (query order), rows of dv lddv elements apart; q and k get no gradient. */
 int vqa_vit_patchify(const float* img, void* out, int n, int h, int w, int patch, hipStream_t stream);
 int vqa_gather_rows(const void* src, long long lds, const long long* idx, long long stride, long long offset,
                     void* dst, long long ldd, int rows, int cols, int esz, hipStream_t stream);
@@ -306,8 +306,8 @@ int vqa_scatter_rows(const void* src, long long lds, const long long* idx, long 
 int vqa_last_index(const long long* mask, int batch, int len, long long* out, hipStream_t stream);
 int vqa_xattn1_fwd(const void* v, long long ldv, void* out, long long ldo, int batch, int len, int heads, int dh,
                    const vqa_dropout* drop, hipStream_t stream);
-int vqa_xattn1_bwd(const void* dctx, long long ldd, float* dv32, void* dv16, int batch, int len, int heads, int dh,
-                   const vqa_dropout* drop, hipStream_t stream);
+int vqa_xattn1_bwd(const void* dctx, long long ldd, float* dv32, void* dv16, long long lddv, int batch, int len,
+                   int heads, int dh, const vqa_dropout* drop, hipStream_t stream);
 
 /* ------------------------------------------------------------------ head ---
  * AttentionPooler (resnet_vqa_model.py:14-26) + classification_layer +

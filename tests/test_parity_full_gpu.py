@@ -1,12 +1,5 @@
-"""Parity of the benched configuration and of single blocks, on the GPU.
+"""Parity of single blocks on the GPU (the benched step: tests/test_a_bench_step_gpu.py).
 
-* test_bench_step_b64_matches_oracle: the engine built EXACTLY as bench.py
-  builds it (BASELINE configs[1]: R50, B=64, 224x224, L=32, pipelined frozen
-  ResNet, tuned tile / split-K table, captured hipGraph step, deferred AdamW,
-  train-mode dropout 0.1 from the shared counter hash, bench's warm-up and
-  schedule) against the CPU fp32 oracle fed the same batches and dropout
-  masks, step by step: log-probs, loss, total and per-group grad norms, then
-  the parameters after the updates.  (trainer/faster_rcnn_vqa_trainer.py:391-406.)
 * test_sga_block_matches_reference / test_t5_encoder_matches_reference: one
   SGA block (forward + backward from a given output gradient) and the T5
   encoder output, through the HIP kernels, against the fixtures the reference
@@ -24,93 +17,12 @@ import torch
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TABLE = os.path.join(ROOT, "t5-resnet-vqa_amd", "tuning", "gemm_gfx950.json")
-GROUPS = ("lang_model", "scaler", "sga_modules", "attention_pooler", "classification_layer")
-
-# bf16 GEMM operands / fp32 accumulate vs the fp32 oracle (log-probs 5e-2, loss
-# 5e-3, total grad-norm 1e-3, per-group 5e-3), tightened to what is met with margin (measured
-# at B=64: log-probs <= 1.2e-2, loss <= 4.4e-5, grad-norm <= 6.2e-4, per-group <= 9.7e-4).
-# Train-mode steps with identical dropout masks.
-LP_TOL, LOSS_RTOL, GN_RTOL, GROUP_RTOL = 2e-2, 5e-4, 1e-3, 5e-3
-# parameter updates: relative L2 error of the per-group update vectors (delta = post - pre);
-# measured <= 5.5e-2 (T5, where AdamW's m / sqrt(v) amplifies near-zero gradients' rounding)
-DELTA_RTOL = 0.1
 
 
 @pytest.fixture(scope="module")
 def cuda():
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
-
-
-def _dev(nb):
-    return {k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None}
-
-
-def test_bench_step_b64_matches_oracle(cuda, pkg, parity_report):
-    from oracle import vqa_oracle as orc
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
-    B, L, H = 64, 32, 224
-    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
-    # bench.py main(): same constructor arguments, same priming / tuning / capture sequence
-    eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, warmup=10, total=100000,
-                               dropout=0.1, seed=0, pipeline=True, t5_dw_group=None)
-    assert eng.defer_opt and eng.pipeline
-    nsteps = 3
-    nbs = [pkg.synthetic.make_batch(B, L, H, seed=1 + i) for i in range(nsteps + 1)]
-    pool = [_dev(nb) for nb in nbs]
-    eng.prime(pool[0]["image_tensors"])
-    eng.F4.copy_(eng.F4N)
-    eng.load_batch(pool[0], next_images=pool[1]["image_tensors"])
-    eng.forward()
-    eng.backward()
-    eng.autotune(table=TABLE)
-    eng.capture()
-    eng.prime(pool[0]["image_tensors"])
-    splitk = sum(1 for c in eng.res_calls + eng.fwd_calls + eng.bwd_calls if c.name == "vqa_gemm" and c.desc.splitk > 1)
-    assert splitk > 0, "the tuned table should give split-K launches at B=64"
-
-    ot = orc.OracleTrainer(sd, "resnet50", warmup=10, total=100000, dropout=0.1, seed=0)
-    p0 = {k: v.detach().clone() for k, v in ot.sd.items() if k in ot.keys}
-    rep = {"splitk_launches": splitk}
-    fails = []
-    for i in range(nsteps):
-        ot.rng_counter = int(eng.RNG[1].item())             # the same dropout draw (engine bumps, then uses)
-        eng.load_batch(pool[i], next_images=pool[i + 1]["image_tensors"])
-        eng.train_step()
-        torch.cuda.synchronize()
-        lp, loss, gn = eng.LOGP.cpu().numpy(), float(eng.LOSS.item()), eng.last_grad_norm()
-        ggn = eng.group_grad_norms()
-        olp, oloss = ot.forward_backward(orc.to_torch_batch(nbs[i]))
-        ogg = ot.group_grad_norms()
-        ogn = float(ot.clip_and_step())
-        lp_err = float(np.abs(lp - olp.numpy()).max())
-        loss_rel = abs(loss - float(oloss)) / abs(float(oloss))
-        gn_rel = abs(gn - ogn) / ogn
-        grp = {g: abs(ggn[g] - ogg[g]) / ogg[g] for g in GROUPS}
-        rep[f"step{i}"] = {"log_prob_max_abs": lp_err, "loss_rel": loss_rel, "grad_norm_rel": gn_rel,
-                           "group_grad_norm_rel": grp, "loss": loss, "grad_norm": gn}
-        fails += [(i, what) for what, bad in (("log_probs", lp_err > LP_TOL), ("loss", loss_rel > LOSS_RTOL),
-                                              ("grad_norm", gn_rel > GN_RTOL * (1 + i)),
-                                              ("group_grad_norms", max(grp.values()) > GROUP_RTOL * (1 + i))) if bad]
-    # parameters after the updates (deferred update flushed), per group: L2 error of the
-    # update vectors relative to the oracle's update
-    post = eng.state_dict()
-    delta = {}
-    for g in GROUPS:
-        num = den = 0.0
-        for k in ot.keys:
-            if orc.group_of(k) != g:
-                continue
-            do = (ot.sd[k].detach() - p0[k]).double().numpy()
-            de = post[k].astype(np.float64) - p0[k].double().numpy()
-            num += float(((de - do) ** 2).sum())
-            den += float((do ** 2).sum())
-        delta[g] = (num / den) ** 0.5 if den > 0 else 0.0
-    rep["update_rel_l2"] = delta
-    parity_report["bench_b64"] = rep
-    assert not fails, (fails, rep)
-    assert max(delta.values()) <= DELTA_RTOL, delta
 
 
 def _sga_engine(pkg):
