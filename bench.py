@@ -186,6 +186,9 @@ def main():
     ap.add_argument("--tune-save", default=None, help="write the tile choices used to this file")
     ap.add_argument("--model", choices=("resnet", "vit"), default="resnet",
                     help="vit: BASELINE configs[3], ViT-base + T5 encoder-decoder (1 GPU)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="run every rank on cuda:0 over gloo: exercises the N-rank code path (bucketing, "
+                         "gathers, capture, lockstep) on a one-GPU box; the timing is not a measurement")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -196,6 +199,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.rehearse:
+        local = 0                                          # every rank shares the one GPU (gloo, host-staged)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if args.model == "vit":
@@ -206,7 +211,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     pkg = load_package()
     B, L, H = args.batch, args.seq_len, args.image_size
@@ -272,7 +280,7 @@ def main():
     dt = time.perf_counter() - t0
     gpu_step = ev0.elapsed_time(ev1) * 1e-3 / args.steps       # HIP events on the replay stream
     if dist:
-        t = torch.tensor([dt, gpu_step], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt, gpu_step], device="cpu" if args.rehearse else dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, gpu_step = float(t[0].item()), float(t[1].item())
     loss = float(eng.LOSS.item())
@@ -309,10 +317,18 @@ def main():
                    "seq_len": L, "image_size": H, "answers": 170, "parallelism": f"dp{world}",
                    "world_size": (dist.get_world_size() if dist else 1), "graph": not args.no_graph,
                    "resnet_pipelined": pipe},
+        **({"rehearsal": "all ranks on cuda:0 over gloo: a code-path check, not a measurement"}
+           if args.rehearse else {}),
         "roofline": roofline,
         "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
     }
-    if not args.no_kernel_rooflines:
+    if args.rehearse:                               # the N-rank path's results: lockstep across ranks
+        eng.flush_optimizer()
+        p = eng.P32[:: max(1, eng.P32.numel() // 65536)].cpu()
+        ps = [torch.empty_like(p) for _ in range(world)]
+        dist.all_gather(ps, p)
+        out["rehearsal_lockstep"] = all(torch.equal(q, ps[0]) for q in ps)
+    elif not args.no_kernel_rooflines:
         out.update(kernel_rooflines(eng, stream, pmc))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pkg)
