@@ -196,7 +196,9 @@ def test_embedding_relbias_colsum_cast(k, T, pad):
     ws = torch.empty(3 * T, device="cuda", dtype=torch.int32)
     run(k, "vqa_embedding_bwd", ids, dh, dt, T, D, Vv, ws)
     ref = torch.zeros(Vv, D, device="cuda", dtype=torch.float64).index_add_(0, ids, dh.double()).float()
-    torch.testing.assert_close(dt, ref, rtol=1e-5, atol=1e-4)
+    # a row summed over n tokens in fp32 (fixed token order) carries ~sqrt(n) ulps of its partial sums
+    nmax = int(torch.bincount(ids, minlength=Vv).max())
+    torch.testing.assert_close(dt, ref, rtol=1e-5, atol=1e-4 * max(1.0, (nmax / 2000) ** 0.5))
     dt2 = torch.zeros(Vv, D, device="cuda")
     run(k, "vqa_embedding_bwd", ids, dh, dt2, T, D, Vv, ws)
     assert torch.equal(dt, dt2), "embedding backward must be deterministic"
