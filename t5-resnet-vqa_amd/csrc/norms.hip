@@ -124,32 +124,46 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* __restric
   float dwacc[NV][4] = {};
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
-  for (int row = r0 + wv; row < r1; row += ROWS_PER_BLOCK) {
-    float d[NV][4], v[NV][4], o[NV][4];
-    load_row<NV>(dy + (long)row * D, d);
-    load_row<NV>(x + (long)row * D, v);
-    if (dres) load_row<NV>(dres + (long)row * D, o);   // issued with dy and x: one round trip per row
-    drop_row<NV>(kdy, row, d);
-    const float r = rstd[row];
-    float s = 0.f;
+  // a wave's rows two at a time, both rows' loads issued before either is used: one memory
+  // round trip per pair instead of per row (the per-row arithmetic and order are unchanged)
+  for (int row0 = r0 + wv; row0 < r1; row0 += 2 * ROWS_PER_BLOCK) {
+    float d[2][NV][4], v[2][NV][4], o[2][NV][4], r[2];
+    const int nr = row0 + ROWS_PER_BLOCK < r1 ? 2 : 1;
 #pragma unroll
-    for (int i = 0; i < NV; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s += g[i][j] * d[i][j] * v[i][j];
-        dwacc[i][j] += d[i][j] * v[i][j] * r;
+    for (int h = 0; h < 2; ++h) {
+      if (h < nr) {
+        const int row = row0 + h * ROWS_PER_BLOCK;
+        load_row<NV>(dy + (long)row * D, d[h]);
+        load_row<NV>(x + (long)row * D, v[h]);
+        if (dres) load_row<NV>(dres + (long)row * D, o[h]);
+        r[h] = rstd[row];
       }
-    s = wave_sum(s);
-    const float c = r * r * r * s / D;
+    }
 #pragma unroll
-    for (int i = 0; i < NV; ++i)
+    for (int h = 0; h < 2; ++h) {
+      if (h >= nr) break;
+      const int row = row0 + h * ROWS_PER_BLOCK;
+      drop_row<NV>(kdy, row, d[h]);
+      float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float t = r * g[i][j] * d[i][j] - c * v[i][j];
-        o[i][j] = dres ? o[i][j] + t : t;
-      }
-    if (dx32) store_row32_drop<NV>(dx32 + (long)row * D, k32, row, o);
-    if (dx16) store_row16_drop<NV>(dx16 + (long)row * D, k16, row, o);
+      for (int i = 0; i < NV; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s += g[i][j] * d[h][i][j] * v[h][i][j];
+          dwacc[i][j] += d[h][i][j] * v[h][i][j] * r[h];
+        }
+      s = wave_sum(s);
+      const float c = r[h] * r[h] * r[h] * s / D;
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float t = r[h] * g[i][j] * d[h][i][j] - c * v[h][i][j];
+          o[h][i][j] = dres ? o[h][i][j] + t : t;
+        }
+      if (dx32) store_row32_drop<NV>(dx32 + (long)row * D, k32, row, o[h]);
+      if (dx16) store_row16_drop<NV>(dx16 + (long)row * D, k16, row, o[h]);
+    }
   }
   // reduce the 4 waves' dw partials through LDS, write one row per block
   __shared__ float red[ROWS_PER_BLOCK][NV * 256];
@@ -215,43 +229,58 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
   float dga[NV][4] = {}, dba[NV][4] = {}, dsa[NV][4] = {};
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
-  for (int row = r0 + wv; row < r1; row += ROWS_PER_BLOCK) {
-    float d[NV][4], v[NV][4], o[NV][4], rr[NV][4];
-    load_row<NV>(dy + (long)row * D, d);
-    load_row<NV>(x + (long)row * D, v);
-    if (dres) load_row<NV>(dres + (long)row * D, rr);  // issued with dy and x: one round trip per row
-    const float mu = mean[row], r = rstd[row];
-    float s1 = 0.f, s2 = 0.f;
+  // two rows per iteration, both rows' loads issued first (as in rmsnorm_bwd_kernel)
+  for (int row0 = r0 + wv; row0 < r1; row0 += 2 * ROWS_PER_BLOCK) {
+    float d[2][NV][4], v[2][NV][4], rr[2][NV][4], mu[2], r[2];
+    const int nr = row0 + ROWS_PER_BLOCK < r1 ? 2 : 1;
 #pragma unroll
-    for (int i = 0; i < NV; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[i][j] = (v[i][j] - mu) * r;                    // xhat
-        const float gd = g[i][j] * d[i][j];
-        s1 += gd;
-        s2 += gd * v[i][j];
-        dga[i][j] += d[i][j] * v[i][j];
-        dba[i][j] += d[i][j];
+    for (int h = 0; h < 2; ++h) {
+      if (h < nr) {
+        const int row = row0 + h * ROWS_PER_BLOCK;
+        load_row<NV>(dy + (long)row * D, d[h]);
+        load_row<NV>(x + (long)row * D, v[h]);
+        if (dres) load_row<NV>(dres + (long)row * D, rr[h]);
+        mu[h] = mean[row];
+        r[h] = rstd[row];
       }
-    s1 = wave_sum(s1) / D;
-    s2 = wave_sum(s2) / D;
+    }
 #pragma unroll
-    for (int i = 0; i < NV; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        o[i][j] = r * (g[i][j] * d[i][j] - s1 - v[i][j] * s2);
-        if (dres) rr[i][j] += o[i][j];
-      }
-    // post-LN: dres is an accumulator that only the fp32 output carries; the branch
-    // gradient (dx16, dsum) is the LayerNorm input gradient alone
-    if (dx32) store_row32<NV>(dx32 + (long)row * D, dres ? rr : o);
-    if (dx16 || with_dsum) {
-      drop_row<NV>(k16, row, o);                           // the branch gradient (masked)
-      if (dx16) store_row16<NV>(dx16 + (long)row * D, o);
+    for (int h = 0; h < 2; ++h) {
+      if (h >= nr) break;
+      const int row = row0 + h * ROWS_PER_BLOCK;
+      float o[NV][4];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int i = 0; i < NV; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) dsa[i][j] += o[i][j];
+        for (int j = 0; j < 4; ++j) {
+          v[h][i][j] = (v[h][i][j] - mu[h]) * r[h];        // xhat
+          const float gd = g[i][j] * d[h][i][j];
+          s1 += gd;
+          s2 += gd * v[h][i][j];
+          dga[i][j] += d[h][i][j] * v[h][i][j];
+          dba[i][j] += d[h][i][j];
+        }
+      s1 = wave_sum(s1) / D;
+      s2 = wave_sum(s2) / D;
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[i][j] = r[h] * (g[i][j] * d[h][i][j] - s1 - v[h][i][j] * s2);
+          if (dres) rr[h][i][j] += o[i][j];
+        }
+      // post-LN: dres is an accumulator that only the fp32 output carries; the branch
+      // gradient (dx16, dsum) is the LayerNorm input gradient alone
+      if (dx32) store_row32<NV>(dx32 + (long)row * D, dres ? rr[h] : o);
+      if (dx16 || with_dsum) {
+        drop_row<NV>(k16, row, o);                         // the branch gradient (masked)
+        if (dx16) store_row16<NV>(dx16 + (long)row * D, o);
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dsa[i][j] += o[i][j];
+      }
     }
   }
   __shared__ float red[ROWS_PER_BLOCK][NV * 256];
