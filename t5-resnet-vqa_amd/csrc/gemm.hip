@@ -24,6 +24,11 @@
 // contiguous range of tiles (bijective form, cdna_hip_programming.md §5).
 #include "gemm_common.h"
 
+// diagnostic phase stamps (tools/micro/gemm_stamps.hip defines it; a no-op in the library)
+#ifndef VQA_GEMM_STAMP
+#define VQA_GEMM_STAMP(i)
+#endif
+
 namespace {
 
 template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, bool EXT = false>
@@ -44,7 +49,20 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int tile = wg / S, slice = wg - tile * S;
-  const int tm = tile / P.tiles_n, tn = tile - tm * P.tiles_n;
+  int tm = tile / P.tiles_n, tn = tile - tm * P.tiles_n;
+  if constexpr (GB) {
+    // implicit-im2col B (ConvTranspose2d dW: column = tap * C + c): order the tiles channel
+    // block first, so the consecutive tiles an XCD gets are every tap and row tile of ONE
+    // channel block -- the 9 taps re-read that slice of the layer4 map from this XCD's L2
+    // instead of fetching the whole map 9 times from the Infinity Cache / HBM
+    const int cb = P.gb.c / BN;
+    if (cb > 0 && P.gb.c % BN == 0 && P.tiles_n % cb == 0) {
+      const int taps = P.tiles_n / cb, per = P.tiles_m * taps;
+      const int cblk = tile / per, r = tile - cblk * per;
+      tm = r / taps;
+      tn = (r - tm * taps) * cb + cblk;
+    }
+  }
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int z = blockIdx.z;
@@ -54,6 +72,7 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int wm = w / NWN, wn = w % NWN;
 
+  VQA_GEMM_STAMP(0);
   LA la;
   LB lb;
   la.init(m0, P.m, P.lda, P.ga);
@@ -84,10 +103,12 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
       lb.issue(B, P.ldb, smem + s * ST_BYTES + A_BYTES, (kb + s) * BK, P.k, P.gb);
     }
   }
+  VQA_GEMM_STAMP(1);
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = min(nk - 1, kt + STAGES - 2) - kt;
     wait_tiles<NL, STAGES>(ahead);
     barrier();
+    if (kt == 0) VQA_GEMM_STAMP(2);
     const int nt = kt + STAGES - 1;
     if (nt < nk) {
       char* st = smem + (nt % STAGES) * ST_BYTES;
@@ -186,7 +207,9 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
       }
   }
 
+  VQA_GEMM_STAMP(3);
   tile_epilogue<BM, BN, STAGES, NWM, NWN, EXT>(P, acc, z, m0, n0, P.m, smem);
+  VQA_GEMM_STAMP(4);
 }
 
 template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB>
@@ -322,7 +345,9 @@ int effective_splitk(int k, int splitk, int* kper) {
 
 }  // namespace
 
+#ifndef VQA_GEMM_MICRO
 #include "conv_patch.inl"
+#endif
 
 namespace {
 // auto tile for the patch convolution: 64-column tiles for 64 output channels, 64-row tiles
@@ -410,6 +435,7 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
   return VQA_OK;
 }
 
+#ifndef VQA_GEMM_MICRO
 extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   GemmParams P;
   if (int rc = prepare(d, P)) return rc;
@@ -494,3 +520,4 @@ extern "C" int vqa_gemm_pair(const vqa_gemm_desc* dx, const vqa_gemm_desc* dw, h
     default: return pair_second<4>(c2, P1, P2, stream);
   }
 }
+#endif  // VQA_GEMM_MICRO

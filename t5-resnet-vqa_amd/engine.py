@@ -1113,7 +1113,10 @@ class VQAEngine:
             side.wait_event(ev["embed"])
         for t in range(bounds[0]):                         # embedding + rel-bias
             txt[t](hs)
+        hook = getattr(self, "_res_hook", None)
         for i in range(nl):
+            if hook is not None and hook[0] == i:
+                hook[1]()
             if i + 2 < nl:
                 issue(f"t5.{i + 2}")
             side.wait_event(ev[f"t5.{i}"])
@@ -1202,9 +1205,20 @@ class VQAEngine:
         fork = torch.cuda.Event()
         fork.record(main)
         self._rstream.wait_event(fork)
-        with torch.cuda.stream(self._rstream):
-            self._run(self.res_calls)
+
+        def issue_res():
+            with torch.cuda.stream(self._rstream):
+                self._run(self.res_calls)
+        # capture position of the ResNet branch (a replayed graph submits nodes in capture
+        # order): VQA_RES_AT = T5 layer index before whose calls it is issued (-1: first)
+        at = int(os.environ.get("VQA_RES_AT", "-1"))
+        if at < 0 or not self.defer_opt:
+            issue_res()
+            self._res_hook = None
+        else:
+            self._res_hook = (at, issue_res)
         self.run_forward_streams()                         # ConvTranspose2d || T5 encoder, then SGA
+        self._res_hook = None
         self.run_backward_streams(sq_overlap=self.sq_overlap)
         self._run(self.opt_calls[1:] if self.sq_overlap else self.opt_calls)
         join = torch.cuda.Event()

@@ -1,0 +1,119 @@
+// Where a 2048-row projection GEMM's time goes, phase by phase: every workgroup stamps the
+// 100 MHz wall clock at entry, after its prologue DMAs are issued, when its first k-tile has
+// landed, after the k-loop and after the epilogue (gemm.hip VQA_GEMM_STAMP hooks).  Prints,
+// per shape x tile config: the event-timed launch, the span from the first entry to the
+// last exit, the entry skew, and the median phase durations.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include gemm_stamps.hip ../../t5-resnet-vqa_amd/csrc/api.hip \
+//     -o gemm_stamps
+#include <hip/hip_runtime.h>
+__device__ unsigned long long g_st[16384 * 8];
+#define VQA_GEMM_STAMP(i)                                                                       \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.z == 0) g_st[blockIdx.x * 8 + (i)] = wall_clock64();      \
+  } while (0)
+#define VQA_GEMM_MICRO 1
+#include "../../t5-resnet-vqa_amd/csrc/gemm.hip"
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+template <int BM, int BN, int S, int NWM = 2, int NWN = 2>
+void run(const char* tag, int M, int N, int K, bool res, int splitk = 0) {
+  bf16_t *a, *b;
+  float *c32, *r32;
+  CK(hipMalloc(&a, (size_t)M * K * 2));
+  CK(hipMalloc(&b, (size_t)N * K * 2));
+  CK(hipMalloc(&c32, (size_t)M * N * 4));
+  CK(hipMalloc(&r32, (size_t)M * N * 4));
+  CK(hipMemset(a, 0x3c, (size_t)M * K * 2));
+  CK(hipMemset(b, 0x3c, (size_t)N * K * 2));
+  CK(hipMemset(r32, 0, (size_t)M * N * 4));
+  vqa_gemm_desc d{};
+  d.a = a; d.lda = K; d.b = b; d.ldb = K; d.m = M; d.n = N; d.k = K;
+  d.c32 = c32; d.ldc32 = N; d.alpha = 1.f; d.batch = 1;
+  if (res) { d.res32 = r32; d.ldres = N; }
+  void* ws = nullptr;
+  if (splitk > 1) {
+    int kper;
+    const int S_ = effective_splitk(K, splitk, &kper);
+    const long long need = 2 * splitk_bytes(64, 64, M, N, 1, S_) + splitk_bytes(BM, BN, M, N, 1, S_);
+    CK(hipMalloc(&ws, need));
+    CK(hipMemset(ws, 0, need));
+    d.splitk = splitk; d.workspace = ws; d.workspace_bytes = need;
+    d.config = 0;
+  }
+  GemmParams P;
+  // prepare() sizes the split-K workspace by the config's tile; check it against this tile
+  if (prepare(&d, P)) { printf("prepare failed: %s\n", vqa_last_error()); exit(1); }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> ev;
+  for (int r = 0; r < 25; ++r) {
+    CK(hipEventRecord(e0, 0));
+    GemmParams Q = P;
+    launch<BM, BN, S, NWM, NWN, true, true, false, false>(Q, 1, 0);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (r >= 5) ev.push_back(ms * 1e3f);
+  }
+  std::sort(ev.begin(), ev.end());
+  const int nwg = vqa::cdiv(M, BM) * vqa::cdiv(N, BN) * (P.splitk > 1 ? P.splitk : 1);
+  std::vector<unsigned long long> st((size_t)nwg * 8);
+  CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_st), st.size() * 8));
+  int rate_khz = 0;
+  CK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
+  const double us = 1e3 / rate_khz;                     // microseconds per tick
+  unsigned long long t0 = ~0ull, t0max = 0, t4 = 0;
+  std::vector<double> ph[4];
+  for (int w = 0; w < nwg; ++w) {
+    const unsigned long long* s = &st[(size_t)w * 8];
+    t0 = std::min(t0, s[0]);
+    t0max = std::max(t0max, s[0]);
+    t4 = std::max(t4, s[4]);
+    for (int p = 0; p < 4; ++p) ph[p].push_back((double)(s[p + 1] - s[p]) * us);
+  }
+  for (auto& v : ph) std::sort(v.begin(), v.end());
+  auto med = [](std::vector<double>& v) { return v[v.size() / 2]; };
+  auto mx = [](std::vector<double>& v) { return v.back(); };
+  printf("%-6s %4dx%4dx%4d %3dx%3d s%d k%d wg %4d | event %6.2f us | span %6.2f  entry-skew %5.2f | "
+         "init %5.2f  first-tile %5.2f  k-loop %6.2f (max %6.2f)  epilogue %5.2f (max %5.2f)\n",
+         tag, M, N, K, BM, BN, S, P.splitk, nwg, ev[ev.size() / 2], (t4 - t0) * us, (t0max - t0) * us, med(ph[0]), med(ph[1]),
+         med(ph[2]), mx(ph[2]), med(ph[3]), mx(ph[3]));
+  CK(hipFree(a)); CK(hipFree(b)); CK(hipFree(c32)); CK(hipFree(r32));
+  if (ws) CK(hipFree(ws));
+}
+
+int main() {
+  run<64, 64, 4>("o", 2048, 768, 768, true, 2);
+  run<64, 64, 4>("o", 2048, 768, 768, true, 3);
+  run<64, 64, 2>("o", 2048, 768, 768, true, 2);
+  run<128, 96, 3, 4, 1>("o", 2048, 768, 768, true);
+  run<128, 96, 3, 4, 1>("o", 2048, 768, 768, true, 2);
+  run<128, 96, 2, 4, 1>("o", 2048, 768, 768, true, 2);
+  run<64, 96, 3, 2, 1>("o", 2048, 768, 768, true);
+  run<64, 96, 4, 2, 1>("o", 2048, 768, 768, true);
+  run<64, 192, 3>("o", 2048, 768, 768, true, 2);
+  run<128, 128, 3>("o", 2048, 768, 768, true, 2);
+  run<64, 64, 4>("wo", 2048, 768, 3072, true);
+  run<64, 64, 4>("wo", 2048, 768, 3072, true, 2);
+  run<128, 96, 3, 4, 1>("wo", 2048, 768, 3072, true, 2);
+  run<64, 96, 4, 2, 1>("wo", 2048, 768, 3072, true);
+  run<64, 128, 3>("qkv", 2048, 2304, 768, false);
+  run<128, 96, 3, 4, 1>("qkv", 2048, 2304, 768, false);
+  run<64, 96, 4, 2, 1>("qkv", 2048, 2304, 768, false);
+  run<64, 64, 2>("o", 2048, 768, 768, true);
+  run<64, 64, 3>("o", 2048, 768, 768, true);
+  run<64, 64, 4>("o", 2048, 768, 768, true);
+  run<128, 64, 2>("o", 2048, 768, 768, true);
+  run<64, 128, 2>("qkv", 2048, 2304, 768, false);
+  run<64, 64, 3>("wo", 2048, 768, 3072, true);
+  run<64, 64, 2>("wo", 2048, 768, 3072, true);
+  run<64, 64, 2>("k64", 2048, 768, 64, true);
+  run<64, 64, 2>("k256", 2048, 768, 256, true);
+  return 0;
+}
