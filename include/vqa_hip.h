@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 9
+#define VQA_ABI_VERSION 10
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -72,7 +72,7 @@ int vqa_dropout_mask(const vqa_dropout* d, float* out, long long n, hipStream_t 
  * a_conv = 2: the same 3x3 / stride-1 / pad-1 convolution read from input patches staged
  *   once per 64-channel chunk in LDS (each input pixel crosses L2 -> LDS once, not 9x):
  *   k = (c / 64, kh, kw, c % 64), i.e. weights stored [Cout][C/64][3][3][64]; C % 64 == 0,
- *   b_trans = 0, batch 1, no split-K; tile configs VQA_GEMM_PATCH_FIRST..VQA_GEMM_CONFIGS.
+ *   b_trans = 0, batch 1, no split-K; tile configs VQA_GEMM_PATCH_FIRST..VQA_GEMM_PATCH_LAST.
  * b_conv: B(k,n) is the implicit im2col with k = output pixel, n = (kh,kw,c);
  *   requires b_trans = 1 (weight-gradient of a convolution).
  * Epilogue: k = [mask(m,n) > 0] * dropout multiplier of element (z*m+row)*n+col
@@ -124,9 +124,12 @@ typedef struct vqa_gemm_desc {
 } vqa_gemm_desc;
 
 /* tile configs: 1 128x128/3 stages, 2 128x64/4, 3 64x64/4, 4 64x64/2, 5 64x64/3, 6 128x64/2,
- * 7 64x128/2, 8 128x128/2 (4 waves); 9 256x128/2, 10 128x256/2, 11 256x256/2, 12 256x128/3 (8 waves) */
-#define VQA_GEMM_CONFIGS 20
+ * 7 64x128/2, 8 128x128/2 (4 waves); 9 256x128/2, 10 128x256/2, 11 256x256/2, 12 256x128/3 (8 waves);
+ * 13..16 64x192 / 128x192 (k-contiguous B only); 17..20 the LDS-patch convolution;
+ * 21 64x64/2, 22 64x128/2, 23 128x64/2 with 128-deep k-tiles (no implicit im2col, no split-K) */
+#define VQA_GEMM_CONFIGS 23
 #define VQA_GEMM_PATCH_FIRST 17    /* configs 17..20: a_conv = 2 only */
+#define VQA_GEMM_PATCH_LAST 20
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
 /* tile configuration (1..VQA_GEMM_CONFIGS) that vqa_gemm would run for this descriptor */
 int vqa_gemm_select(const vqa_gemm_desc* d);

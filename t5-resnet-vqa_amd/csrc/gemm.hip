@@ -31,14 +31,15 @@
 
 namespace {
 
-template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, bool EXT = false>
+template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, bool EXT = false,
+          int BKT = BK>
 __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, char* smem) {
   constexpr int NW = NWM * NWN, NT = 64 * NW;
   constexpr int WM = BM / NWM, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
   static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "wave sub-tile must be whole 32x32 blocks");
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, ST_BYTES = A_BYTES + B_BYTES;
-  using LA = Loader<BM, AKC, GA, NW>;
-  using LB = Loader<BN, BKC, GB, NW>;
+  constexpr int A_BYTES = BM * BKT * 2, B_BYTES = BN * BKT * 2, ST_BYTES = A_BYTES + B_BYTES;
+  using LA = Loader<BM, AKC, GA, NW, BKT>;
+  using LB = Loader<BN, BKC, GB, NW, BKT>;
   constexpr int NL = LA::NI + LB::NI;                 // glds instructions per thread per K-tile
 
   // XCD-aware bijective remap of the linear block id; with split-K the slices of
@@ -77,8 +78,8 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
   LB lb;
   la.init(m0, P.m, P.lda, P.ga);
   lb.init(n0, P.n, P.ldb, P.gb);
-  using FA = FragAddr<BM, AKC, TM>;
-  using FB = FragAddr<BN, BKC, TN>;
+  using FA = FragAddr<BM, AKC, TM, BKT>;
+  using FB = FragAddr<BN, BKC, TN, BKT>;
   FA fra;
   FB frb;
   fra.init(wm * WM);
@@ -93,14 +94,14 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  const int nk_all = (P.k + BK - 1) / BK;
+  const int nk_all = (P.k + BKT - 1) / BKT;
   const int kb = S > 1 ? slice * P.kper : 0;                  // this slice's first k-tile
   const int nk = S > 1 ? min(nk_all - kb, P.kper) : nk_all;   // >= 1 (host checks)
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s) {
     if (s < nk) {
-      la.issue(A, P.lda, smem + s * ST_BYTES, (kb + s) * BK, P.k, P.ga);
-      lb.issue(B, P.ldb, smem + s * ST_BYTES + A_BYTES, (kb + s) * BK, P.k, P.gb);
+      la.issue(A, P.lda, smem + s * ST_BYTES, (kb + s) * BKT, P.k, P.ga);
+      lb.issue(B, P.ldb, smem + s * ST_BYTES + A_BYTES, (kb + s) * BKT, P.k, P.gb);
     }
   }
   VQA_GEMM_STAMP(1);
@@ -112,8 +113,8 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
     const int nt = kt + STAGES - 1;
     if (nt < nk) {
       char* st = smem + (nt % STAGES) * ST_BYTES;
-      la.issue(A, P.lda, st, (kb + nt) * BK, P.k, P.ga);
-      lb.issue(B, P.ldb, st + A_BYTES, (kb + nt) * BK, P.k, P.gb);
+      la.issue(A, P.lda, st, (kb + nt) * BKT, P.k, P.ga);
+      lb.issue(B, P.ldb, st + A_BYTES, (kb + nt) * BKT, P.k, P.gb);
     }
     const uint32_t cur = lds0 + (kt % STAGES) * ST_BYTES;
     constexpr int R = FA::READS + FB::READS;
@@ -121,8 +122,8 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
     fra.read(cur, 0, fa[0]);
     frb.read(cur + A_BYTES, 0, fb[0]);
 #pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      if (s + 1 < BK / 16) {
+    for (int s = 0; s < BKT / 16; ++s) {
+      if (s + 1 < BKT / 16) {
         fra.read(cur, s + 1, fa[(s + 1) & 1]);
         frb.read(cur + A_BYTES, s + 1, fb[(s + 1) & 1]);
         wait_lgkm<R>();
@@ -208,14 +209,14 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
   }
 
   VQA_GEMM_STAMP(3);
-  tile_epilogue<BM, BN, STAGES, NWM, NWN, EXT>(P, acc, z, m0, n0, P.m, smem);
+  tile_epilogue<BM, BN, STAGES, NWM, NWN, EXT, BKT>(P, acc, z, m0, n0, P.m, smem);
   VQA_GEMM_STAMP(4);
 }
 
-template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB>
+template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, int BKT = BK>
 __global__ __launch_bounds__(64 * NWM * NWN) void gemm_kernel(GemmParams P) {
-  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<BM, BN, STAGES>::LDS];
-  gemm_body<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB>(P, blockIdx.x, smem);
+  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<BM, BN, STAGES, BKT>::LDS];
+  gemm_body<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB, false, BKT>(P, blockIdx.x, smem);
 }
 
 // GELU / tanh epilogues (vqa_gemm_desc.relu 2 / 3: the ViT intermediate and pooler of
@@ -255,8 +256,10 @@ long long splitk_bytes(int bm, int bn, int m, int n, int batch, int S) {
   return SPLITK_CNT_BYTES + tiles * S * bm * bn * 4;
 }
 
-template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB>
+template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, int BKT = BK>
 int launch(GemmParams& P, int batch, hipStream_t s) {
+  if (BKT != BK && P.splitk > 1)                        // split-K slices are counted in 64-deep k-tiles
+    return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: 128-deep k-tile configs take no split-K");
   P.tiles_m = vqa::cdiv(P.m, BM);
   P.tiles_n = vqa::cdiv(P.n, BN);
   if (P.splitk > 1) {                                   // workspace = [counters | slabs]
@@ -266,7 +269,7 @@ int launch(GemmParams& P, int batch, hipStream_t s) {
     P.slab = reinterpret_cast<float*>(reinterpret_cast<char*>(P.slab) + SPLITK_CNT_BYTES);
   }
   dim3 grid(P.tiles_m * P.tiles_n * (P.splitk > 1 ? P.splitk : 1), 1, batch);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB>), grid, dim3(64 * NWM * NWN), 0, s, P);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB, BKT>), grid, dim3(64 * NWM * NWN), 0, s, P);
   return vqa::check_launch("vqa_gemm");
 }
 
@@ -317,6 +320,17 @@ int dispatch_tile(GemmParams& P, int batch, int config, hipStream_t s) {
       } else {
         return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: tile config %d needs a k-contiguous B operand (b_trans=0)", config);
       }
+    case 21: case 22: case 23:
+      // 128-deep k-tiles: twice the bytes per ring slot and per barrier (the per-k-tile fixed
+      // cost of the L2 -> LDS fill is amortised over 32-48 KB instead of 16-24 KB); plain
+      // (non-gathered) operands, no split-K
+      if constexpr (!GA && !GB) {
+        if (config == 21) return launch<64, 64, 2, 2, 2, AKC, BKC, GA, GB, 128>(P, batch, s);
+        if (config == 22) return launch<64, 128, 2, 2, 2, AKC, BKC, GA, GB, 128>(P, batch, s);
+        return launch<128, 64, 2, 2, 2, AKC, BKC, GA, GB, 128>(P, batch, s);
+      } else {
+        return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: tile config %d takes no implicit-im2col operand", config);
+      }
     default: return launch<64, 64, 4, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
   }
 }
@@ -329,7 +343,7 @@ void tile_of(int config, int& bm, int& bn) {
                                                  {64, 64},   {128, 64},  {64, 128}, {128, 128}, {256, 128},
                                                  {128, 256}, {256, 256}, {256, 128}, {64, 192}, {128, 192},
                                                  {64, 192},  {128, 192}, {128, 64}, {128, 128}, {64, 64},
-                                                 {64, 128}};
+                                                 {64, 128},  {64, 64},   {64, 128}, {128, 64}};
   bm = T[config][0];
   bn = T[config][1];
 }
@@ -441,11 +455,11 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   if (int rc = prepare(d, P)) return rc;
   const int batch = d->batch, cfg = d->config;
   const bool akc = !d->a_trans, bkc = !d->b_trans;
-  const bool patch_cfg = cfg >= VQA_GEMM_PATCH_FIRST;
+  const bool patch_cfg = cfg >= VQA_GEMM_PATCH_FIRST && cfg <= VQA_GEMM_PATCH_LAST;
   if (d->a_conv == 2) {                                   // LDS-patch 3x3 convolution (conv_patch.inl)
     VQA_REQUIRE(akc && bkc && !d->b_conv && batch == 1, "vqa_gemm(a_conv=2): k-contiguous B, batch 1");
     VQA_REQUIRE(cfg == 0 || patch_cfg, "vqa_gemm(a_conv=2): tile config %d is not a patch config (%d..%d)", cfg,
-                VQA_GEMM_PATCH_FIRST, VQA_GEMM_CONFIGS);
+                VQA_GEMM_PATCH_FIRST, VQA_GEMM_PATCH_LAST);
     return conv_patch_dispatch(P, vqa_gemm_select(d), stream);
   }
   VQA_REQUIRE(!patch_cfg, "vqa_gemm: tile config %d is for a_conv = 2 only", cfg);

@@ -35,9 +35,16 @@ struct GemmParams {
   int dsite;               // != 0: batch z uses dropout site + z*dsite, element indices from 0
 };
 
-// byte offset of 16-B chunk `ch` of row `row` in a k-contig image ([rows][64 bf16])
+// byte offset of 16-B chunk `ch` of row `row` in a k-contig image ([rows][BKT bf16]):
+// 128-B rows (BKT 64, two rows per 256-B bank row): chunk ^= (row>>1)&7;
+// 256-B rows (BKT 128, one row per bank row): chunk ^= row&15, so the 16 lanes of a
+// ds_read_b128 group (16 consecutive rows, one logical chunk) hit 16 distinct chunks
 __device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + ((ch ^ kc_swz(row)) << 4); }
+template <int BKT>
+__device__ __forceinline__ int kc_swz_t(int row) { if constexpr (BKT == 128) return row & 15; else return kc_swz(row); }
+template <int BKT>
+__device__ __forceinline__ int kc_off_t(int row, int ch) { return row * (BKT * 2) + ((ch ^ kc_swz_t<BKT>(row)) << 4); }
 // byte offset of chunk `ch` of k-row `kr` in an m/n-contig image ([64][ROWLEN bf16])
 template <int ROWLEN>
 __device__ __forceinline__ int mn_swz(int kr) {
@@ -67,13 +74,15 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
 // One operand tile of ROWS (m or n) x 64 (k): ROWS*128 bytes = ROWS/8 wave
 // instructions of 1 KiB; NI per wave (NW waves).  KC image: 8 rows per
 // instruction; MN image: 1024 / (2*ROWS) k-rows per instruction.
-template <int ROWS, bool KC, bool GATHER, int NW>
+template <int ROWS, bool KC, bool GATHER, int NW, int BKT = BK>
 struct Loader {
-  static_assert(ROWS % (8 * NW) == 0, "operand tile must split evenly over the waves");
+  static_assert(BKT == 64 || (BKT == 128 && !GATHER), "128-deep k-tiles: plain operands only");
+  static constexpr int KCPR = BKT / 8;                   // 16-B chunks per k-contig row
+  static_assert(ROWS * BKT * 2 % (1024 * NW) == 0, "operand tile must split evenly over the waves");
   static_assert(KC || ROWS == 64 || ROWS == 128 || ROWS == 256, "m/n-contig image rows: 64, 128 or 256");
-  static constexpr int NI = ROWS / (8 * NW);
-  static constexpr int RPI = KC ? 8 : 1024 / (ROWS * 2);
-  static constexpr int CPR = KC ? 8 : ROWS / 8;          // 16-B chunks per image row
+  static constexpr int NI = ROWS * BKT * 2 / (1024 * NW);
+  static constexpr int RPI = KC ? 64 / KCPR : 1024 / (ROWS * 2);
+  static constexpr int CPR = KC ? KCPR : ROWS / 8;       // 16-B chunks per image row
   long off[NI];            // KC: element offset of (row, chunk) at k0 = 0; MN: column index
   int kof[NI];             // KC: k offset of the chunk inside the tile; MN: k-row inside the tile
   int g0[NI], g1[NI], g2[NI];
@@ -85,8 +94,8 @@ struct Loader {
     for (int j = 0; j < NI; ++j) {
       const int ins = w * NI + j;
       if constexpr (KC) {
-        const int row = ins * 8 + (l >> 3);
-        const int ch = (l & 7) ^ kc_swz(row);
+        const int row = ins * RPI + l / KCPR;
+        const int ch = (l % KCPR) ^ kc_swz_t<BKT>(row);
         const int grow = row0 + row;
         ok[j] = grow < nrows;
         kof[j] = ch * 8;
@@ -217,15 +226,15 @@ __device__ __forceinline__ void wait_lgkm() {
 // Per-lane LDS byte offsets of one operand's fragments (k-step 0), relative to
 // the operand image base.  KC: lane reads row (base + l&31), chunk 2s + (l>>5);
 // MN: two ds_read_b64_tr_b16 per fragment (k rows 16s+8h+q and +4).
-template <int ROWS, bool KC, int T>
+template <int ROWS, bool KC, int T, int BKT = BK>
 struct FragAddr {
-  uint32_t o[KC ? 4 : 2 * T];
+  uint32_t o[KC ? BKT / 16 : 2 * T];
   __device__ __forceinline__ void init(int row_base) {
     const int l = threadIdx.x & 63;
     if constexpr (KC) {
       const int row = row_base + (l & 31);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) o[s] = kc_off(row, 2 * s + (l >> 5));
+      for (int s = 0; s < BKT / 16; ++s) o[s] = kc_off_t<BKT>(row, 2 * s + (l >> 5));
     } else {
       const int h = l >> 5, g1 = (l >> 4) & 1, i16 = l & 15, q = i16 >> 2, p = i16 & 3;
 #pragma unroll
@@ -243,7 +252,7 @@ struct FragAddr {
 #pragma unroll
     for (int i = 0; i < T; ++i) {
       if constexpr (KC) {
-        f[i] = ds_b128(base + o[s] + i * 32 * 128);
+        f[i] = ds_b128(base + o[s] + i * 32 * (BKT * 2));
       } else {
         const uint32_t so = s * 16 * ROWS * 2;          // 16 k-rows per step; swizzle is s-invariant
         const i32x2_t lo = ds_tr16(base + o[2 * i] + so);
@@ -278,9 +287,9 @@ __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BM, int BN, int STAGES>
+template <int BM, int BN, int STAGES, int BKT = BK>
 struct TileCfg {
-  static constexpr int LDS = STAGES * (BM + BN) * BK * 2;       // LDS ring bytes
+  static constexpr int LDS = STAGES * (BM + BN) * BKT * 2;      // LDS ring bytes
 };
 
 // One output tile.  `bid` is the tile's linear id within its problem (the
@@ -309,12 +318,12 @@ __device__ __forceinline__ float epi_act(float v, int a) {
   return copysignf((1.f - e) / (1.f + e), v);
 }
 
-template <int BM, int BN, int STAGES, int NWM, int NWN, bool EXT = false>
+template <int BM, int BN, int STAGES, int NWM, int NWN, bool EXT = false, int BKT = BK>
 __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&acc)[BM / NWM / 32][BN / NWN / 32],
                                               const int z, const int m0, const int n0, const int mlim, char* smem) {
   constexpr int NW = NWM * NWN, NT = 64 * NW;
   constexpr int WM = BM / NWM, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
-  constexpr int ST_BYTES = (BM + BN) * BK * 2;
+  constexpr int ST_BYTES = (BM + BN) * BKT * 2;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int wm = w / NWN, wn = w % NWN;
   // epilogue: acc[i][j][4g+t] -> row m0+wm*WM+i*32+(l&31), col n0+wn*WN+j*32+8g+4(l>>5)+t.

@@ -204,6 +204,8 @@ def test_all_tile_configs_bitwise_identical(ops, pkg, layout):
     for cfg in range(1, n_cfg + 1):
         if (cfg in pkg.lib.GEMM_KC_B_ONLY and not b_kc) or cfg in pkg.lib.GEMM_PATCH_ONLY:
             continue
+        if cfg in pkg.lib.GEMM_BK128 and layout in ("conv", "convw"):     # no implicit-im2col operand
+            continue
         out = torch.empty(M, N, device="cuda")
         d = mk(out)
         d.config = cfg
@@ -283,7 +285,7 @@ def test_splitk_matches_reference_and_is_config_invariant(ops, pkg, layout, spli
         scale = 0.5 * (A.abs() @ Bm.abs()).max().item()
     outs = []
     cfgs = [c for c in sorted(pkg.lib.GEMM_TILES) if (layout in ("AB", "conv") or c not in pkg.lib.GEMM_KC_B_ONLY)
-            and c not in pkg.lib.GEMM_PATCH_ONLY]
+            and c not in pkg.lib.GEMM_PATCH_ONLY and c not in pkg.lib.GEMM_BK128]
     for cfg in cfgs:
         out = torch.full((M, N), float("nan"), device="cuda")
         d = mk(out)
@@ -300,6 +302,31 @@ def test_splitk_matches_reference_and_is_config_invariant(ops, pkg, layout, spli
     close(outs[0], ref, scale)
     for cfg, o in zip(cfgs[1:], outs[1:]):
         assert torch.equal(o, outs[0]), f"config {cfg} differs at splitk={splitk}"
+
+
+def test_bk128_configs_refuse_split_k_and_conv(ops, pkg):
+    """The 128-deep k-tile configs count k in 128-wide tiles: split-K (sliced in 64-deep
+    tiles) and the implicit-im2col operands are refused with an error, not run wrongly."""
+    M, N, K = 128, 128, 512
+    a, b = bf((M, K), seed=5), bf((N, K), seed=6)
+    out = torch.empty(M, N, device="cuda")
+    for cfg in pkg.lib.GEMM_BK128:
+        d = ops.gemm_desc(a, b, M, N, K, lda=K, ldb=K, c32=out, ldc32=N)
+        d.config = cfg
+        ops.set_splitk(d, 2)
+        ws = ops.splitk_workspace(d)
+        ops.set_splitk(d, 2, ws)
+        with pytest.raises(RuntimeError):
+            ops.run(d)
+    x = bf((2, 7, 7, 64), seed=7)
+    wt = bf((64, 3, 3, 64), 0.05, seed=8)
+    g = ops.conv_geom(2, 7, 7, 64, 7, 7, 3, 3, 1, 1)
+    out = torch.empty(98, 64, device="cuda")
+    for cfg in pkg.lib.GEMM_BK128:
+        d = ops.gemm_desc(x, wt, 98, 64, 576, lda=576, ldb=576, c32=out, ldc32=64, ga=g)
+        d.config = cfg
+        with pytest.raises(RuntimeError):
+            ops.run(d)
 
 
 def test_kc_b_only_configs_refuse_transposed_b(ops, pkg):

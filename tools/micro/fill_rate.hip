@@ -109,16 +109,16 @@ int main() {
     printf("%-34s grid %4d  %7.1f us  %6.1f GB/s per WG  %6.2f TB/s chip\n", tag, grid, ms * 1e3, tot / grid / (ms * 1e-3) / 1e9,
            tot / (ms * 1e-3) / 1e12);
   };
-  for (int grid : {256, 512}) {
+  for (int grid : {256, 384, 512}) {
+    rep("glds 32K 4 waves 2 stages", timeit(fill_glds<32768, 4, 2>, grid, 256, src, span, tiles, out), grid, 32768);
+    rep("glds 48K 4 waves 2 stages", timeit(fill_glds<49152, 4, 2>, grid, 256, src, span, tiles, out), grid, 49152);
+    rep("glds 64K 8 waves 2 stages", timeit(fill_glds<65536, 8, 2>, grid, 512, src, span, tiles, out), grid, 65536);
     rep("glds 16K 4 waves 2 stages", timeit(fill_glds<16384, 4, 2>, grid, 256, src, span, tiles, out), grid, 16384);
     rep("glds 16K 4 waves 3 stages", timeit(fill_glds<16384, 4, 3>, grid, 256, src, span, tiles, out), grid, 16384);
     rep("glds 16K 4 waves 4 stages", timeit(fill_glds<16384, 4, 4>, grid, 256, src, span, tiles, out), grid, 16384);
     rep("glds 16K 8 waves 3 stages", timeit(fill_glds<16384, 8, 3>, grid, 512, src, span, tiles, out), grid, 16384);
     rep("glds 32K 4 waves 3 stages", timeit(fill_glds<32768, 4, 3>, grid, 256, src, span, tiles, out), grid, 32768);
     rep("glds 32K 8 waves 3 stages", timeit(fill_glds<32768, 8, 3>, grid, 512, src, span, tiles, out), grid, 32768);
-    rep("reg  16K 4 waves (1 ahead)", timeit(fill_reg<16384, 4>, grid, 256, src, span, tiles, out), grid, 16384);
-    rep("reg  16K 8 waves (1 ahead)", timeit(fill_reg<16384, 8>, grid, 512, src, span, tiles, out), grid, 16384);
-    rep("reg  32K 4 waves (1 ahead)", timeit(fill_reg<32768, 4>, grid, 256, src, span, tiles, out), grid, 32768);
   }
   return 0;
 }

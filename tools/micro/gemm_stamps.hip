@@ -19,7 +19,7 @@ __device__ unsigned long long g_st[16384 * 8];
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
-template <int BM, int BN, int S, int NWM = 2, int NWN = 2>
+template <int BM, int BN, int S, int NWM = 2, int NWN = 2, int BKT = 64>
 void run(const char* tag, int M, int N, int K, bool res, int splitk = 0) {
   bf16_t *a, *b;
   float *c32, *r32;
@@ -54,7 +54,7 @@ void run(const char* tag, int M, int N, int K, bool res, int splitk = 0) {
   for (int r = 0; r < 25; ++r) {
     CK(hipEventRecord(e0, 0));
     GemmParams Q = P;
-    launch<BM, BN, S, NWM, NWN, true, true, false, false>(Q, 1, 0);
+    launch<BM, BN, S, NWM, NWN, true, true, false, false, BKT>(Q, 1, 0);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms;
@@ -80,40 +80,25 @@ void run(const char* tag, int M, int N, int K, bool res, int splitk = 0) {
   for (auto& v : ph) std::sort(v.begin(), v.end());
   auto med = [](std::vector<double>& v) { return v[v.size() / 2]; };
   auto mx = [](std::vector<double>& v) { return v.back(); };
-  printf("%-6s %4dx%4dx%4d %3dx%3d s%d k%d wg %4d | event %6.2f us | span %6.2f  entry-skew %5.2f | "
+  printf("%-6s %4dx%4dx%4d %3dx%3d s%d bk%3d k%d wg %4d | event %6.2f us | span %6.2f  entry-skew %5.2f | "
          "init %5.2f  first-tile %5.2f  k-loop %6.2f (max %6.2f)  epilogue %5.2f (max %5.2f)\n",
-         tag, M, N, K, BM, BN, S, P.splitk, nwg, ev[ev.size() / 2], (t4 - t0) * us, (t0max - t0) * us, med(ph[0]), med(ph[1]),
+         tag, M, N, K, BM, BN, S, BKT, P.splitk, nwg, ev[ev.size() / 2], (t4 - t0) * us, (t0max - t0) * us, med(ph[0]), med(ph[1]),
          med(ph[2]), mx(ph[2]), med(ph[3]), mx(ph[3]));
   CK(hipFree(a)); CK(hipFree(b)); CK(hipFree(c32)); CK(hipFree(r32));
   if (ws) CK(hipFree(ws));
 }
 
 int main() {
-  run<64, 64, 4>("o", 2048, 768, 768, true, 2);
-  run<64, 64, 4>("o", 2048, 768, 768, true, 3);
-  run<64, 64, 2>("o", 2048, 768, 768, true, 2);
-  run<128, 96, 3, 4, 1>("o", 2048, 768, 768, true);
-  run<128, 96, 3, 4, 1>("o", 2048, 768, 768, true, 2);
-  run<128, 96, 2, 4, 1>("o", 2048, 768, 768, true, 2);
-  run<64, 96, 3, 2, 1>("o", 2048, 768, 768, true);
-  run<64, 96, 4, 2, 1>("o", 2048, 768, 768, true);
-  run<64, 192, 3>("o", 2048, 768, 768, true, 2);
-  run<128, 128, 3>("o", 2048, 768, 768, true, 2);
-  run<64, 64, 4>("wo", 2048, 768, 3072, true);
-  run<64, 64, 4>("wo", 2048, 768, 3072, true, 2);
-  run<128, 96, 3, 4, 1>("wo", 2048, 768, 3072, true, 2);
-  run<64, 96, 4, 2, 1>("wo", 2048, 768, 3072, true);
-  run<64, 128, 3>("qkv", 2048, 2304, 768, false);
-  run<128, 96, 3, 4, 1>("qkv", 2048, 2304, 768, false);
-  run<64, 96, 4, 2, 1>("qkv", 2048, 2304, 768, false);
   run<64, 64, 2>("o", 2048, 768, 768, true);
-  run<64, 64, 3>("o", 2048, 768, 768, true);
-  run<64, 64, 4>("o", 2048, 768, 768, true);
-  run<128, 64, 2>("o", 2048, 768, 768, true);
+  run<64, 64, 2, 2, 2, 128>("o", 2048, 768, 768, true);
+  run<128, 64, 2, 2, 2, 128>("o", 2048, 768, 768, true);
   run<64, 128, 2>("qkv", 2048, 2304, 768, false);
-  run<64, 64, 3>("wo", 2048, 768, 3072, true);
-  run<64, 64, 2>("wo", 2048, 768, 3072, true);
-  run<64, 64, 2>("k64", 2048, 768, 64, true);
-  run<64, 64, 2>("k256", 2048, 768, 256, true);
+  run<64, 128, 2, 2, 2, 128>("qkv", 2048, 2304, 768, false);
+  run<64, 64, 2, 2, 2, 128>("qkv", 2048, 2304, 768, false);
+  run<64, 128, 2>("wi", 2048, 3072, 768, false);
+  run<64, 128, 2, 2, 2, 128>("wi", 2048, 3072, 768, false);
+  run<64, 64, 4>("wo", 2048, 768, 3072, true);
+  run<64, 64, 2, 2, 2, 128>("wo", 2048, 768, 3072, true);
+  run<128, 64, 2, 2, 2, 128>("wo", 2048, 768, 3072, true);
   return 0;
 }
