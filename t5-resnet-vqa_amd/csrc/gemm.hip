@@ -93,6 +93,12 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // rownorm: this lane's share of sum_k A[row]^2 for its fragment rows (row l&31 of block i;
+  // lanes l and l^32 see the two 8-wide halves of every 16-deep k-step)
+  float sq[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) sq[i] = 0.f;
+  const bool rown = AKC && !GA && P.rownorm;
 
   const int nk_all = (P.k + BKT - 1) / BKT;
   const int kb = S > 1 ? slice * P.kper : 0;                  // this slice's first k-tile
@@ -129,6 +135,16 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
         wait_lgkm<R>();
       } else {
         wait_lgkm<0>();
+      }
+      if (rown) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t u = (uint32_t)fa[s & 1][i][q];
+            const float lo = __uint_as_float(u << 16), hi = __uint_as_float(u & 0xffff0000u);
+            sq[i] = fmaf(lo, lo, fmaf(hi, hi, sq[i]));
+          }
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -208,6 +224,17 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
       }
   }
 
+  if (rown) {                                          // the RMSNorm row scale (no split-K: host check)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float t = sq[i] + __shfl_xor(sq[i], 32);
+      const float r = rsqrtf(t / (float)P.k + P.rn_eps);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] *= r;
+    }
+  }
   VQA_GEMM_STAMP(3);
   tile_epilogue<BM, BN, STAGES, NWM, NWN, EXT, BKT>(P, acc, z, m0, n0, P.m, smem);
   VQA_GEMM_STAMP(4);
@@ -421,6 +448,10 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
   P.drop = d->drop;
   P.sbias = d->stride_bias;
   P.dsite = d->drop_site_stride;
+  VQA_REQUIRE(!d->rownorm || (!d->a_trans && !d->a_conv && d->splitk <= 1 && d->batch == 1 && d->rownorm_eps > 0.f),
+              "vqa_gemm: rownorm needs a k-contiguous plain A, no split-K, batch 1 and eps > 0");
+  P.rownorm = d->rownorm;
+  P.rn_eps = d->rownorm_eps;
   P.splitk = 1;
   P.kper = 0;
   P.slab = nullptr;

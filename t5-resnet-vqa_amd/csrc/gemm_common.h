@@ -33,6 +33,8 @@ struct GemmParams {
   unsigned* cnt;           // [batch][tile] arrival counters (zero between launches)
   long sbias;              // bias stride per batch element
   int dsite;               // != 0: batch z uses dropout site + z*dsite, element indices from 0
+  int rownorm;             // scale output rows by rsqrt(mean_k(A^2) + rn_eps) (vqa_gemm_desc.rownorm)
+  float rn_eps;
 };
 
 // byte offset of 16-B chunk `ch` of row `row` in a k-contig image ([rows][BKT bf16]):

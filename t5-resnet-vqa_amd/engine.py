@@ -85,7 +85,18 @@ def _gemm_key(d):
     return (d.m, d.n, d.k, d.batch, d.a_trans, d.b_trans, d.a_conv, d.b_conv,
             geo(d.ga) if d.a_conv else None, geo(d.gb) if d.b_conv else None,
             bool(d.c32), bool(d.c16), bool(d.bias), bool(d.res32), bool(d.res16), bool(d.mask16), d.relu,
-            d.beta != 0.0, d.drop.p > 0.0)
+            d.beta != 0.0, d.drop.p > 0.0) + (("rownorm",) if d.rownorm else ())
+
+
+class _Seq:
+    """Several prepared calls issued as one (a deferred AdamW range and the folded
+    weights that follow it)."""
+    def __init__(self, calls):
+        self.calls = calls
+
+    def __call__(self, stream):
+        for c in self.calls:
+            c(stream)
 
 
 @contextlib.contextmanager
@@ -171,6 +182,11 @@ class VQAEngine:
         self.defer_embed = os.environ.get("VQA_DEFER_EMBED", "0") == "1"
         # stream steps: the grad-norm pass over [0, rel-bias) beside the embedding scatter
         self.sq_overlap = os.environ.get("VQA_SQ_OVERLAP", "1") != "0"
+        # T5 RMSNorms folded into the next projection (vqa_gemm_desc.rownorm): the chain runs the
+        # q|k|v (layers >= 1) and wi GEMMs on the unnormalised rows; the normalised rows the
+        # weight gradients need are made by one batched launch beside the SGA forward.  Off by
+        # default: 23 fewer launches on the chain measured no faster
+        self.norm_fold = os.environ.get("VQA_NORM_FOLD", "0") == "1"
         self.T = batch * seq_len
         self.lay = ParamLayout(vision, answer_spaces, num_blocks)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
@@ -183,12 +199,14 @@ class VQAEngine:
             self._plan_forward()
             self._plan_backward()
             self._plan_optimizer()
+            self._run(self.fold_all)                     # folded weights of the initial parameters
         self.graph = None
         self.allreduce = None            # set by the DP trainer: fn(G32 tensor) on the current stream
         self._side = torch.cuda.Stream(self.dev)
         self._wside = torch.cuda.Stream(self.dev)
         self._rstream = torch.cuda.Stream(self.dev)
         self._ostream = torch.cuda.Stream(self.dev)      # deferred AdamW ranges (run_forward_streams)
+        self._nstream = torch.cuda.Stream(self.dev)      # the batched off-chain RMSNorms (norm_fold)
         self.dw_stream = os.environ.get("VQA_DW_STREAM", "1" if self._default_dw else "0") == "1"
         self._scratch = None             # split-K workspace used while autotuning
 
@@ -354,6 +372,13 @@ class VQAEngine:
         self.FF = [self.FFS[nl - 1 - i] for i in range(nl)]
         self.R0 = [t(T) for _ in range(nl)]
         self.R1 = [t(T) for _ in range(nl)]
+        if self.norm_fold:
+            # bf16 copies of the residual stream (written by the o / wo epilogues beside the fp32
+            # rows) and the projection weights with the RMSNorm weight folded into their columns
+            self.HS16 = [None] + [t((T, D), BF16) for _ in range(1, nl)]
+            self.HM16 = [t((T, D), BF16) for _ in range(nl)]
+            self.WQF = [None] + [t((3 * D, D), BF16) for _ in range(1, nl)]
+            self.WIF = [t((S.T5_DFF, D), BF16) for _ in range(nl)]
         self.RF = t(T)
         self.TXT32, self.TXT16 = t((T, D)), t((T, D), BF16)
         # SGA blocks; the self-attention halves of all blocks share batched buffers:
@@ -570,24 +595,36 @@ class VQAEngine:
                    self._dptr(SITE_EMBED, kp), extra=kp + [self.RNG])
         self._call(f, "vqa_t5_relbias_fwd", self.p32["t5.relbias"], self.bucket, self.PB, S.T5_HEADS, Lq, Lq)
         self._t5_layer_start = []
+        fold = self.norm_fold
         for i in range(S.T5_LAYERS):
             self._t5_layer_start.append(len(f))
-            self._call(f, "vqa_rmsnorm_fwd", self.HS[i], self.p32[f"t5.{i}.ln0"], None, self.N0[i], self.R0[i], T, D,
-                       1e-6, None)
-            self._linear(f, self.N0[i], f"t5.{i}.qkv_w", T, out16=self.QKV[i], bias=False)
+            if fold and i > 0:        # rms(h) W^T = rstd(h) * (h16 (W o w)^T): the norm rides on the GEMM
+                self._gemm(f, self.HS16[i], self.WQF[i], T, 3 * D, D, lda=D, ldb=D, c16=self.QKV[i], ldc16=3 * D,
+                           rownorm_eps=1e-6)
+            else:
+                self._call(f, "vqa_rmsnorm_fwd", self.HS[i], self.p32[f"t5.{i}.ln0"], None, self.N0[i], self.R0[i], T,
+                           D, 1e-6, None)
+                self._linear(f, self.N0[i], f"t5.{i}.qkv_w", T, out16=self.QKV[i], bias=False)
             q = self.QKV[i]
             self._attn(f, "vqa_attn_fwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, o=self.O[i], ldo=D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B,
                        heads=S.T5_HEADS, lq=Lq, lk=Lq, dh=S.T5_DKV, scale=1.0, drop=t5_site(i, 0))
             # h + dropout(attention output)   (T5LayerSelfAttention :400)
-            self._linear(f, self.O[i], f"t5.{i}.o_w", T, out32=self.HM[i], bias=False, res32=self.HS[i],
-                         drop=t5_site(i, 1))
-            self._call(f, "vqa_rmsnorm_fwd", self.HM[i], self.p32[f"t5.{i}.ln1"], None, self.N1[i], self.R1[i], T, D,
-                       1e-6, None)
+            self._linear(f, self.O[i], f"t5.{i}.o_w", T, out32=self.HM[i], out16=self.HM16[i] if fold else None,
+                         bias=False, res32=self.HS[i], drop=t5_site(i, 1))
             # dropout(relu(wi h)) (T5DenseActDense :86), then h + dropout(wo .) (T5LayerFF :140)
-            self._linear(f, self.N1[i], f"t5.{i}.wi", T, out16=self.FF[i], bias=False, relu=True, drop=t5_site(i, 2))
-            self._linear(f, self.FF[i], f"t5.{i}.wo", T, out32=self.HS[i + 1], bias=False, res32=self.HM[i],
-                         drop=t5_site(i, 3))
+            if fold:
+                self._gemm(f, self.HM16[i], self.WIF[i], T, S.T5_DFF, D, lda=D, ldb=D, c16=self.FF[i],
+                           ldc16=S.T5_DFF, relu=True, rownorm_eps=1e-6)
+                self._set_drop(f[-1], t5_site(i, 2))
+            else:
+                self._call(f, "vqa_rmsnorm_fwd", self.HM[i], self.p32[f"t5.{i}.ln1"], None, self.N1[i], self.R1[i], T,
+                           D, 1e-6, None)
+                self._linear(f, self.N1[i], f"t5.{i}.wi", T, out16=self.FF[i], bias=False, relu=True,
+                             drop=t5_site(i, 2))
+            self._linear(f, self.FF[i], f"t5.{i}.wo", T, out32=self.HS[i + 1],
+                         out16=self.HS16[i + 1] if fold and i + 1 < S.T5_LAYERS else None, bias=False,
+                         res32=self.HM[i], drop=t5_site(i, 3))
         kp = []
         self._call(f, "vqa_rmsnorm_fwd", self.HS[-1], self.p32["t5.final_ln"], self.TXT32, self.TXT16, self.RF, T, D,
                    1e-6, self._dptr(SITE_FINAL, kp), extra=kp + [self.RNG])
@@ -645,6 +682,17 @@ class VQAEngine:
         last = self.sga[-1]["OUT"]
         self._call(f, "vqa_head_fwd", last, self.p32["pool_w"], self.p32["pool_b"], self.p32["cls_w"],
                    self.p32["cls_b"], self.TGT, self.ATT, self.POOLED, self.LOGP, self.NLL, self.LOSS, B, Lq, D, self.A)
+        # norm_fold: the normalised rows (and rstd) the weight gradients and the norm backward
+        # read, all 23 in one launch; graph steps run it beside the SGA blocks (run_forward_streams)
+        self._fnorm = None
+        if fold:
+            jobs = [(self.HS[i], self.p32[f"t5.{i}.ln0"], self.N0[i], self.R0[i]) for i in range(1, S.T5_LAYERS)]
+            jobs += [(self.HM[i], self.p32[f"t5.{i}.ln1"], self.N1[i], self.R1[i]) for i in range(S.T5_LAYERS)]
+            arr = (L.RmsNormJob * len(jobs))(*[L.RmsNormJob(*[ops.addr(x) for x in j]) for j in jobs])
+            raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.dev)
+            self._fnorm = len(f)
+            f.append(ops.Call("vqa_rmsnorm_fwd_batched", raw.data_ptr(), len(jobs), T, D, 1e-6,
+                              keep=(raw,) + tuple(x for j in jobs for x in j)))
 
     # ------------------------------------------------------------------ backward plan
     def _plan_backward(self):
@@ -943,11 +991,27 @@ class VQAEngine:
                 self.adam_embed = c
             else:
                 self.adam_segs.append((name, c))
+        # norm_fold: the folded weights W o w follow every update of W or w (each T5 layer's
+        # range carries its own: the layer's q|k|v, wi and norm weights all sit in it)
+        fold = {}
+        self.fold_all = []
+        if self.norm_fold:
+            for i in range(S.T5_LAYERS):
+                lst = []
+                if i > 0:
+                    self._call(lst, "vqa_scale_cols_bf16", self.p32[f"t5.{i}.qkv_w"], self.p32[f"t5.{i}.ln0"],
+                               self.WQF[i], 3 * D, D)
+                self._call(lst, "vqa_scale_cols_bf16", self.p32[f"t5.{i}.wi"], self.p32[f"t5.{i}.ln1"], self.WIF[i],
+                           S.T5_DFF, D)
+                fold[f"t5.{i}"] = lst
+                self.fold_all += lst
+        self.adam_segs = [(nm, _Seq([c] + fold[nm]) if nm in fold else c) for nm, c in self.adam_segs]
         lst = []
         self._call(lst, "vqa_zero", ops.addr(self.opt_state, L.ST_PENDING), 16, extra=[self.opt_state])
         self.clear_pending = lst[0]
         if not self.defer_opt:
             o.append(self.adam_full)
+            o += self.fold_all
         elif self.adam_embed is not None:
             o.append(self.adam_embed)
 
@@ -1070,7 +1134,18 @@ class VQAEngine:
             join = torch.cuda.Event()
             join.record(side)
             main.wait_event(join)
-        self._run(f[p2:])                                  # SGA + head
+        if self._fnorm is None:
+            self._run(f[p2:])                              # SGA + head
+            return
+        ev = torch.cuda.Event()                            # both branches are done: T5 outputs final
+        ev.record(main)
+        self._nstream.wait_event(ev)
+        with torch.cuda.stream(self._nstream):
+            self._run(f[self._fnorm:])                     # the batched off-chain RMSNorms
+        self._run(f[p2:self._fnorm])                       # SGA + head
+        done = torch.cuda.Event()
+        done.record(self._nstream)
+        main.wait_event(done)
 
     def _forward_branches_deferred(self, fork, main, side, vis, txt):
         """The two forward branches with the previous step's AdamW ranges on a third stream.
@@ -1100,9 +1175,9 @@ class VQAEngine:
         # branch's SGA block-0 k/v projection reads it), then layer i+2 at layer i
         if "embed" in segs:                               # defer_embed: the table's range leads
             issue("embed")
-        issue("t5.0")
-        if nl > 1:
-            issue("t5.1")
+        ahead = max(1, int(os.environ.get("VQA_OPT_AHEAD", "2")))   # layers a range runs ahead of its use
+        for i in range(min(ahead, nl)):
+            issue(f"t5.{i}")
         issue("scaler")
         issue("head")
         vpre = vis[:self._fvis_param - p0]                 # frozen ResNet calls (unpipelined engines)
@@ -1117,8 +1192,8 @@ class VQAEngine:
         for i in range(nl):
             if hook is not None and hook[0] == i:
                 hook[1]()
-            if i + 2 < nl:
-                issue(f"t5.{i + 2}")
+            if i + ahead < nl:
+                issue(f"t5.{i + ahead}")
             side.wait_event(ev[f"t5.{i}"])
             for t in range(bounds[i], bounds[i + 1]):
                 txt[t](hs)
@@ -1386,7 +1461,7 @@ class VQAEngine:
                     for sk in SPLITS:
                         # split only grids that leave CUs idle, with >= 2 k-tiles per slice
                         if sk > 1 and (tiles >= 512 or nk < 2 * sk or tiles > 16384 or d.a_conv == 2
-                                       or cfg in L.GEMM_BK128):
+                                       or cfg in L.GEMM_BK128 or d.rownorm):
                             continue
                         d.config = cfg
                         ops.set_splitk(d, sk)
@@ -1473,6 +1548,7 @@ class VQAEngine:
         """Re-derive the bf16 GEMM shadow from the fp32 masters (after writing weights through
         param_view / ParameterGroup views)."""
         self.P16.copy_(self.P32)
+        self._run(self.fold_all)
 
     def layer4_features(self):
         """The frozen ResNet's layer4 map of the current batch as NCHW fp32 (the kernels keep

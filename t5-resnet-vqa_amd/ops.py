@@ -29,7 +29,8 @@ def conv_geom(n, h, w, c, oh, ow, kh, kw, stride, pad):
 def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None, ldc32=0, c16=None, ldc16=0,
               bias=None, res32=None, res16=None, ldres=0, mask16=None, ldmask=0, alpha=1.0, beta=0.0,
               relu=False, ga=None, gb=None, batch=1, stride_a=0, stride_b=0, stride_c32=0, stride_c16=0,
-              stride_res=0, splitk=0, workspace=None, stride_bias=0, drop_site_stride=0, a_patch=False):
+              stride_res=0, splitk=0, workspace=None, stride_bias=0, drop_site_stride=0, a_patch=False,
+              rownorm_eps=0.0):
     for t in (a, b, c16, res16, mask16):
         assert not isinstance(t, torch.Tensor) or t.dtype == torch.bfloat16, "bf16 operand expected"
     for t in (c32, bias, res32):
@@ -56,6 +57,7 @@ def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None
     d.batch, d.stride_a, d.stride_b = batch, stride_a, stride_b
     d.stride_c32, d.stride_c16, d.stride_res = stride_c32, stride_c16, stride_res
     d.stride_bias, d.drop_site_stride = stride_bias, drop_site_stride
+    d.rownorm, d.rownorm_eps = int(rownorm_eps > 0.0), rownorm_eps      # RMSNorm of A's rows folded in
     set_splitk(d, splitk, workspace)
     return d
 

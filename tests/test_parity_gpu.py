@@ -256,3 +256,42 @@ def test_deferred_optimizer_update_is_bit_identical(cuda, pkg, monkeypatch):
         assert r[0] == res[0][0]
         for a, b in zip(r[1:], res[0][1:]):
             assert torch.equal(a, b)
+
+
+def test_folded_rmsnorm_matches_oracle_like_unfolded(cuda, pkg, parity_report, monkeypatch):
+    """VQA_NORM_FOLD=1 (T5 RMSNorm folded into the q|k|v / wi GEMMs, vqa_gemm_desc.rownorm;
+    off by default, measured no faster) against the fp32 oracle: log-probs, loss and grad
+    norm within the golden tolerances, and every T5 weight gradient's relative L2 error
+    no more than 10 % above the unfolded engine's on the same step."""
+    from oracle import vqa_oracle as orc
+    B, L, H, D = 4, 16, 96, 768
+    sd = pkg.synthetic.make_state_dict("resnet34", seed=0)
+    nb = pkg.synthetic.make_batch(B, L, H, seed=1)
+    ot = orc.OracleTrainer(sd, "resnet34", warmup=2, total=10, dropout=0.0)
+    olp, oloss = ot.forward_backward(orc.to_torch_batch(nb))
+    ogn = float(ot.grad_norm())
+    errs = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("VQA_NORM_FOLD", v)
+        e = pkg.engine.VQAEngine(sd, vision="resnet34", batch=B, seq_len=L, image_size=H, warmup=2, total=10,
+                                 dropout=0.0)
+        assert e.norm_fold == (v == "1")
+        lp, loss = e.forward_backward(nb)
+        gn = e.grad_norm()
+        assert float(np.abs(lp - olp.numpy()).max()) <= LP_TOL
+        assert abs(loss - float(oloss)) / abs(float(oloss)) <= LOSS_RTOL
+        assert abs(gn - ogn) / ogn <= GN_RTOL
+        r = {}
+        for i in range(12):
+            p = f"lang_model.block.{i}."
+            for w, ref in (("qkv_w", torch.cat([ot.sd[p + f"layer.0.SelfAttention.{x}.weight"].grad for x in "qkv"])),
+                           ("wi", ot.sd[p + "layer.1.DenseReluDense.wi.weight"].grad),
+                           ("ln0", ot.sd[p + "layer.0.layer_norm.weight"].grad),
+                           ("ln1", ot.sd[p + "layer.1.layer_norm.weight"].grad)):
+                g = e.segment_grad(f"t5.{i}.{w}").cpu().double().reshape(ref.shape)
+                r[f"{i}.{w}"] = float((g - ref.double()).norm() / ref.double().norm())
+        errs[v] = r
+        del e
+    parity_report["norm_fold_vs_unfolded_grad_rel_l2"] = {k: [errs["0"][k], errs["1"][k]] for k in errs["0"]}
+    for k in errs["0"]:
+        assert errs["1"][k] <= 1.1 * errs["0"][k] + 1e-3, (k, errs["0"][k], errs["1"][k])
