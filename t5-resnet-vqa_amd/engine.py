@@ -182,6 +182,8 @@ class VQAEngine:
         self.defer_embed = os.environ.get("VQA_DEFER_EMBED", "0") == "1"
         # stream steps: the grad-norm pass over [0, rel-bias) beside the embedding scatter
         self.sq_overlap = os.environ.get("VQA_SQ_OVERLAP", "1") != "0"
+        # ... and its [0, a) part as soon as the first T5 weight-gradient group is final
+        self._sq_early = os.environ.get("VQA_SQ_EARLY", "1") != "0"
         # T5 RMSNorms folded into the next projection (vqa_gemm_desc.rownorm): the chain runs the
         # q|k|v (layers >= 1) and wi GEMMs on the unnormalised rows; the normalised rows the
         # weight gradients need are made by one batched launch beside the SGA forward.  Off by
@@ -423,8 +425,8 @@ class VQAEngine:
         lib = L.load()
         self.WS_COL2 = t(lib.vqa_colsum_workspace_floats(V, D))
         self.WS_HEAD = t(lib.vqa_head_workspace_floats(B, Lq, D, self.A))
-        self.SQ_PARTS = 1024                              # per sqnorm range (two ranges, §3.7)
-        self.WS_SQ = t(2 * self.SQ_PARTS, torch.float64)
+        self.SQ_PARTS = 1024                              # per sqnorm range (three ranges, §3.7)
+        self.WS_SQ = t(3 * self.SQ_PARTS, torch.float64)
 
     # ------------------------------------------------------------------ call helpers
     # Every helper records the tensors it bakes into a call (ops.Call.keep), so no
@@ -714,6 +716,7 @@ class VQAEngine:
         # The flat layout is in backward-completion order, so finished gradients always form
         # a prefix of G32: DP all-reduces bucket [prev_end, end) as soon as it is final.
         self.ready_marks = []
+        self._sq_split = None        # (call index, prefix end) where the grad-norm pass can start early
 
         self._jobs = []
 
@@ -900,9 +903,13 @@ class VQAEngine:
                 k = int(np.searchsorted(ends, done))
                 self._t5_group_dw(b, i + self.t5_dw_groups[k] - 1, i)
                 mark(f"t5.{i}.ln1")
+                if self._sq_split is None and i > 0 and self._sq_early:   # the first T5 dW group is final
+                    self._sq_split = self.ready_marks[-1]
             elif ends is None and (done % G == 0 or i == 0):
                 self._t5_group_dw(b, i + (done - 1) % G, i)
                 mark(f"t5.{i}.ln1")
+                if self._sq_split is None and i > 0 and self._sq_early:
+                    self._sq_split = self.ready_marks[-1]
         # the relative-position bias is shared by all 12 layers: dPB = sum over (layer, sample) of dS,
         # one fixed-order reduction after the last layer instead of one per layer
         self._call(b, "vqa_batch_sum", self.dSB, S.T5_LAYERS * B, S.T5_HEADS * Lq * Lq, self.dPB, 0.0)
@@ -937,12 +944,18 @@ class VQAEngine:
         # squared-norm partials over two ranges: [0, rel-bias) is final once the backward's
         # deferred column sums are flushed, so graph steps run it beside the embedding-gradient
         # scatter (run_backward_streams); the rel-bias + embedding-table range follows it
+        # [0, a) is final once the first T5 weight-gradient group is (graph steps run that part
+        # beside the backward's last layers), [a, rel-bias) with the last group
         e0 = self.lay["t5.relbias"].offset
-        assert e0 % 4 == 0 and (n - e0) % 4 == 0
-        self._call(o, "vqa_grad_sqnorm", self.G32, e0, self.WS_SQ, self.SQ_PARTS)
-        self._call(o, "vqa_grad_sqnorm", ops.addr(self.G32, e0), n - e0, ops.addr(self.WS_SQ, self.SQ_PARTS),
-                   self.SQ_PARTS, extra=[self.G32, self.WS_SQ])
-        self._call(o, "vqa_optim_finalize", self.WS_SQ, 2 * self.SQ_PARTS, float(self.grad_scale), float(self.max_norm),
+        a = self._sq_split[1] if self._sq_split is not None else e0
+        assert a % 4 == 0 and e0 % 4 == 0 and (n - e0) % 4 == 0 and a <= e0
+        K = self.SQ_PARTS
+        self._call(o, "vqa_grad_sqnorm", self.G32, a, self.WS_SQ, K)
+        self._call(o, "vqa_grad_sqnorm", ops.addr(self.G32, a), e0 - a, ops.addr(self.WS_SQ, K), K,
+                   extra=[self.G32, self.WS_SQ])
+        self._call(o, "vqa_grad_sqnorm", ops.addr(self.G32, e0), n - e0, ops.addr(self.WS_SQ, 2 * K), K,
+                   extra=[self.G32, self.WS_SQ])
+        self._call(o, "vqa_optim_finalize", self.WS_SQ, 3 * K, float(self.grad_scale), float(self.max_norm),
                    int(self.warmup), int(self.total), float(self.betas[0]), float(self.betas[1]), self.opt_state)
         d = L.AdamWDesc()
         d.param, d.grad = self.P32.data_ptr(), self.G32.data_ptr()
@@ -1099,7 +1112,7 @@ class VQAEngine:
         self.run_forward_streams()
         if optimizer:
             self.run_backward_streams(sq_overlap=self.sq_overlap)
-            self._run(self.opt_calls[1:] if self.sq_overlap else self.opt_calls)
+            self._run(self.opt_calls[2:] if self.sq_overlap else self.opt_calls)
         else:
             self.run_backward_streams()
 
@@ -1216,9 +1229,10 @@ class VQAEngine:
         assert set(ev) == set(order)
 
     def run_backward_streams(self, sq_overlap=False):
-        """sq_overlap: also run the optimizer plan's first call (the squared-norm partials of
-        [0, rel-bias), final before the embedding scatter) on `side`, beside that scatter;
-        the caller then runs opt_calls[1:]."""
+        """sq_overlap: also run the optimizer plan's first two calls (the squared-norm partials
+        of [0, a), final once the first T5 weight-gradient group is, and of [a, rel-bias),
+        final before the embedding scatter) on `side`, beside the backward's tail; the caller
+        then runs opt_calls[2:]."""
         main = torch.cuda.current_stream(self.dev)
         side, wside = self._side, self._wside
         b = self.bwd_calls
@@ -1231,13 +1245,23 @@ class VQAEngine:
             self._run(b[q0:q1])                            # scaler dW / db
         if sq_overlap:
             assert b[-1] is self.emb_call
-            self._run_tagged(b[q1:-1], main, wside)        # T5 backward (+ deferred column sums)
-            for st in ((main, wside) if self.dw_stream else (main,)):   # all but the table's are final
-                ev = torch.cuda.Event()
-                ev.record(st)
-                side.wait_event(ev)
-            with torch.cuda.stream(side):
-                self._run(self.opt_calls[:1])
+
+            def to_side(calls):                            # after everything issued so far on main / wside
+                for st in ((main, wside) if self.dw_stream else (main,)):
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    self._run(calls)
+            m1 = self._sq_split[0] if self._sq_split is not None else None
+            if m1 is not None and q1 < m1 < len(b) - 1:
+                self._run_tagged(b[q1:m1], main, wside)    # T5 backward up to the first dW group
+                to_side(self.opt_calls[:1])                # grad-norm partials of [0, a), beside the rest
+                self._run_tagged(b[m1:-1], main, wside)
+                to_side(self.opt_calls[1:2])               # ... and of [a, rel-bias)
+            else:
+                self._run_tagged(b[q1:-1], main, wside)    # T5 backward (+ deferred column sums)
+                to_side(self.opt_calls[:2])
             self._run(b[-1:])                              # embedding rows
         else:
             self._run_tagged(b[q1:], main, wside)          # T5 backward + embedding
@@ -1295,7 +1319,7 @@ class VQAEngine:
         self.run_forward_streams()                         # ConvTranspose2d || T5 encoder, then SGA
         self._res_hook = None
         self.run_backward_streams(sq_overlap=self.sq_overlap)
-        self._run(self.opt_calls[1:] if self.sq_overlap else self.opt_calls)
+        self._run(self.opt_calls[2:] if self.sq_overlap else self.opt_calls)
         join = torch.cuda.Event()
         join.record(self._rstream)
         main.wait_event(join)
