@@ -212,10 +212,12 @@ int vqa_attn_fwd_long(const vqa_attn_desc* d, hipStream_t s);
 extern "C" int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t s) {
   VQA_REQUIRE(d && d->q && d->k && d->v, "attention: null q/k/v");
   if ((d->lq > 32 || d->lk > 64) && vqa_attn_long_ok(d)) return vqa_attn_fwd_long(d, s);   // ViT (config 4)
+  VQA_REQUIRE(d->o, "vqa_attn_fwd: null output");
+  VQA_REQUIRE(d->drop.p >= 0.f && d->drop.p < 1.f, "attention: dropout p must be in [0, 1)");
+  VQA_REQUIRE(d->batch > 0 && d->heads > 0, "attention: empty batch");
+  if (vqa_attn_mfma_ok(d)) return vqa_attn_fwd_mfma(d, s);        // the step's shapes (lk <= 160)
   AttnP P;
   if (int rc = fill(P, d)) return rc;
-  VQA_REQUIRE(d->o, "vqa_attn_fwd: null output");
-  if (vqa_attn_mfma_ok(d)) return vqa_attn_fwd_mfma(d, s);        // the step's shapes
   const size_t sm = fwd_smem(d->lq, d->lk, d->dh);
   VQA_REQUIRE(sm <= 65536, "vqa_attn_fwd: shape needs %zu B of LDS (> 64 KiB)", sm);
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(d->batch * d->heads), dim3(256), sm, s, P);
@@ -223,11 +225,14 @@ extern "C" int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t s) {
 }
 
 extern "C" int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t s) {
-  AttnP P;
-  if (int rc = fill(P, d)) return rc;
+  VQA_REQUIRE(d && d->q && d->k && d->v, "attention: null q/k/v");
   VQA_REQUIRE(d->p && d->dout && d->dq && d->dk && d->dv, "vqa_attn_bwd: null P / dO / dQ / dK / dV");
   VQA_REQUIRE(d->lddo % 8 == 0, "vqa_attn_bwd: dO stride must be a multiple of 8");
-  if (vqa_attn_mfma_ok(d)) return vqa_attn_bwd_mfma(d, s);
+  VQA_REQUIRE(d->drop.p >= 0.f && d->drop.p < 1.f, "attention: dropout p must be in [0, 1)");
+  VQA_REQUIRE(d->batch > 0 && d->heads > 0, "attention: empty batch");
+  if (vqa_attn_mfma_ok(d)) return vqa_attn_bwd_mfma(d, s);        // lk <= 160
+  AttnP P;
+  if (int rc = fill(P, d)) return rc;
   const size_t sm = bwd_smem(d->lq, d->lk, d->dh);
   VQA_REQUIRE(sm <= 65536, "vqa_attn_bwd: shape needs %zu B of LDS (> 64 KiB)", sm);
   hipLaunchKernelGGL(attn_bwd_kernel, dim3(d->batch * d->heads), dim3(256), sm, s, P);

@@ -122,7 +122,11 @@ __device__ __forceinline__ void store_tr(bf16_t* base, long ld, int row, bool ok
   }
 }
 
-constexpr int WPB = 2;                                  // waves (= (b, h) pairs) per block
+// waves (= (b, h) pairs) per block: two for the short key ranges; one from 3 key tiles on
+// (SGA cross-attention over larger layer4 maps, e.g. 144 keys at 384^2), whose LDS images
+// and saved-P transposes take up to ~100 KB per wave
+constexpr int wpb_for(int nt) { return nt <= 2 ? 2 : 1; }
+constexpr int MAX_NT = 5;                               // lk <= 160
 
 // Values row[key] for this lane's 16 X-layout keys of 32-key tile t (keys 32t + 8g +
 // 4h + 0..3 for register group g), loaded unconditionally at clamped keys: 4 float4
@@ -156,11 +160,12 @@ struct Geo {
 };
 
 // ------------------------------------------------------------------ forward
-// NT = number of 32-key tiles (1: lk <= 32, 2: lk <= 64), a template parameter so the
-// lk <= 32 shapes (T5, SGA blocks 1-2) issue no work for a second tile.
+// NT = number of 32-key tiles (1: lk <= 32, 2: lk <= 64, ... MAX_NT), a template parameter
+// so the lk <= 32 shapes (T5, SGA blocks 1-2) issue no work for a second tile.
 template <int DH, int NT>
-__global__ __launch_bounds__(64 * WPB) void attn_fwd_mfma(AttnM P) {
+__global__ __launch_bounds__(64 * wpb_for(NT)) void attn_fwd_mfma(AttnM P) {
   using G = Geo<DH>;
+  constexpr int WPB = wpb_for(NT);
   constexpr int KR = 32 * NT;                            // key rows of the V image
   __shared__ __attribute__((aligned(16))) char smem[WPB * KR * G::ROWB];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h5 = l >> 5, l31 = l & 31;
@@ -198,13 +203,13 @@ __global__ __launch_bounds__(64 * WPB) void attn_fwd_mfma(AttnM P) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) load_xrow(brow, lk, t, vec, add[t]);
   }
-  if (P.mask) {
+  if (NT <= 2 && P.mask) {                              // lk <= 64 (host check for the mask)
     const unsigned long long kb = key_bits(P.mask + (long)b * lk, lk);
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        add[t][r] += ((kb >> (32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5)) & 1ull) ? 0.f : MASK_MIN;
+        add[t][r] += ((kb >> ((32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5) & 63)) & 1ull) ? 0.f : MASK_MIN;
   }
 
   // S^T tiles (X layout: lane = query, registers = keys)
@@ -270,8 +275,9 @@ __global__ __launch_bounds__(64 * WPB) void attn_fwd_mfma(AttnM P) {
 
 // ------------------------------------------------------------------ backward
 template <int DH, int NT>
-__global__ __launch_bounds__(64 * WPB) void attn_bwd_mfma(AttnM P) {
+__global__ __launch_bounds__(64 * wpb_for(NT)) void attn_bwd_mfma(AttnM P) {
   using G = Geo<DH>;
+  constexpr int WPB = wpb_for(NT);
   constexpr int KR = 32 * NT;
   constexpr int IMG = (KR + 32 + 32) * G::ROWB;         // K [32*NT], dO [32], Q [32] images
   constexpr int PR = KR + 1;                             // row stride of the P / mask transposes (bank spread)
@@ -507,7 +513,8 @@ int vqa_attn_fwd_long(const vqa_attn_desc* d, hipStream_t s) {
 // host side: called by vqa_attn_fwd / vqa_attn_bwd (attention.hip) when the shape fits
 bool vqa_attn_mfma_ok(const vqa_attn_desc* d) {
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  return d->lq >= 1 && d->lq <= 32 && d->lk >= 1 && d->lk <= 64 && (d->dh == 64 || d->dh == 96) &&
+  return d->lq >= 1 && d->lq <= 32 && d->lk >= 1 && d->lk <= 32 * MAX_NT &&
+         (d->dh == 64 || d->dh == 96 || d->dh == 128) && (d->lk <= 64 || !d->key_mask) &&
          d->ldq % 8 == 0 && d->ldk % 8 == 0 && d->ldv % 8 == 0 && al16(d->q) && al16(d->k) && al16(d->v) &&
          (!d->o || (d->ldo % 4 == 0 && ((uintptr_t)d->o & 7) == 0)) &&
          (!d->dout || (d->lddo % 8 == 0 && al16(d->dout))) &&
@@ -527,32 +534,37 @@ static void fillm(AttnM& M, const vqa_attn_desc* d) {
   M.dbias = d->dbias; M.drop = d->drop;
 }
 
-int vqa_attn_fwd_mfma(const vqa_attn_desc* d, hipStream_t s) {
-  AttnM M;
-  fillm(M, d);
-  const dim3 grid(vqa::cdiv(M.pairs, WPB));
-  const bool two = d->lk > 32;
-  if (d->dh == 64) {
-    if (two) hipLaunchKernelGGL((attn_fwd_mfma<64, 2>), grid, dim3(64 * WPB), 0, s, M);
-    else hipLaunchKernelGGL((attn_fwd_mfma<64, 1>), grid, dim3(64 * WPB), 0, s, M);
-  } else {
-    if (two) hipLaunchKernelGGL((attn_fwd_mfma<96, 2>), grid, dim3(64 * WPB), 0, s, M);
-    else hipLaunchKernelGGL((attn_fwd_mfma<96, 1>), grid, dim3(64 * WPB), 0, s, M);
-  }
+template <int DH, int NT>
+int launch_fwd(AttnM& M, hipStream_t s) {
+  constexpr int W = wpb_for(NT);
+  hipLaunchKernelGGL((attn_fwd_mfma<DH, NT>), dim3(vqa::cdiv(M.pairs, W)), dim3(64 * W), 0, s, M);
   return vqa::check_launch("vqa_attn_fwd (mfma)");
 }
-
-int vqa_attn_bwd_mfma(const vqa_attn_desc* d, hipStream_t s) {
-  AttnM M;
-  fillm(M, d);
-  const dim3 grid(vqa::cdiv(M.pairs, WPB));
-  const bool two = d->lk > 32;
-  if (d->dh == 64) {
-    if (two) hipLaunchKernelGGL((attn_bwd_mfma<64, 2>), grid, dim3(64 * WPB), 0, s, M);
-    else hipLaunchKernelGGL((attn_bwd_mfma<64, 1>), grid, dim3(64 * WPB), 0, s, M);
-  } else {
-    if (two) hipLaunchKernelGGL((attn_bwd_mfma<96, 2>), grid, dim3(64 * WPB), 0, s, M);
-    else hipLaunchKernelGGL((attn_bwd_mfma<96, 1>), grid, dim3(64 * WPB), 0, s, M);
-  }
+template <int DH, int NT>
+int launch_bwd(AttnM& M, hipStream_t s) {
+  constexpr int W = wpb_for(NT);
+  hipLaunchKernelGGL((attn_bwd_mfma<DH, NT>), dim3(vqa::cdiv(M.pairs, W)), dim3(64 * W), 0, s, M);
   return vqa::check_launch("vqa_attn_bwd (mfma)");
 }
+template <int DH>
+int dispatch_nt(AttnM& M, int nt, bool bwd, hipStream_t s) {
+  switch (nt) {
+    case 1: return bwd ? launch_bwd<DH, 1>(M, s) : launch_fwd<DH, 1>(M, s);
+    case 2: return bwd ? launch_bwd<DH, 2>(M, s) : launch_fwd<DH, 2>(M, s);
+    case 3: return bwd ? launch_bwd<DH, 3>(M, s) : launch_fwd<DH, 3>(M, s);
+    case 4: return bwd ? launch_bwd<DH, 4>(M, s) : launch_fwd<DH, 4>(M, s);
+    default: return bwd ? launch_bwd<DH, 5>(M, s) : launch_fwd<DH, 5>(M, s);
+  }
+}
+int dispatch_dh(const vqa_attn_desc* d, bool bwd, hipStream_t s) {
+  AttnM M;
+  fillm(M, d);
+  const int nt = (d->lk + 31) / 32;
+  if (d->dh == 64) return dispatch_nt<64>(M, nt, bwd, s);
+  if (d->dh == 96) return dispatch_nt<96>(M, nt, bwd, s);
+  return dispatch_nt<128>(M, nt, bwd, s);
+}
+
+int vqa_attn_fwd_mfma(const vqa_attn_desc* d, hipStream_t s) { return dispatch_dh(d, false, s); }
+
+int vqa_attn_bwd_mfma(const vqa_attn_desc* d, hipStream_t s) { return dispatch_dh(d, true, s); }

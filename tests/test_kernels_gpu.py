@@ -93,7 +93,12 @@ def attn_ref(q, kk, v, scale, bias, mask, mult=None):
                                                  (2, 12, 16, 16, 64, True, 0.0), (4, 8, 32, 49, 96, False, 0.1),
                                                  (3, 12, 32, 32, 64, True, 0.1),
                                                  (2, 8, 48, 40, 96, False, 0.0),      # lq > 32: VALU kernel
-                                                 (2, 12, 40, 40, 64, True, 0.1)])
+                                                 (2, 12, 40, 40, 64, True, 0.1),
+                                                 # more vision keys (SGA block 0 at 384^2: 12 x 12) and
+                                                 # head dim 128 (d 1024 / 8 heads): one wave per block
+                                                 (2, 8, 32, 144, 96, False, 0.1), (3, 8, 32, 100, 96, False, 0.0),
+                                                 (2, 8, 16, 160, 128, False, 0.1), (2, 8, 32, 49, 128, False, 0.0),
+                                                 (2, 16, 32, 96, 64, False, 0.0)])
 def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5, pd):
     D = H * dh
     q16 = rnd((B * Lq, 3 * D), 10, dtype=torch.bfloat16)                   # fused qkv-like layout

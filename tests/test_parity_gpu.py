@@ -299,3 +299,27 @@ def test_folded_rmsnorm_matches_oracle_like_unfolded(cuda, pkg, parity_report, m
     assert e1.mean() <= 1.05 * e0.mean(), (e0.mean(), e1.mean())
     for k in errs["0"]:
         assert errs["1"][k] <= 1.35 * errs["0"][k] + 1e-3, (k, errs["0"][k], errs["1"][k])
+
+
+def test_engine_matches_oracle_at_384(cuda, pkg, parity_report):
+    """The step at 384 x 384 images (R50: a 12 x 12 layer4 map, so SGA block 0 attends over
+    144 vision tokens -- the 5-key-tile attention kernels) against the fp32 oracle, one
+    eval-mode step at B = 2, L = 16: log-probs, loss, total grad norm."""
+    from oracle import vqa_oracle as orc
+    B, L, H = 2, 16, 384
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    nb = pkg.synthetic.make_batch(B, L, H, seed=1)
+    eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, warmup=2, total=10,
+                               dropout=0.0)
+    assert eng.fh == 12 and eng.sga[0]["lk"] == 144
+    lp, loss = eng.forward_backward(nb)
+    ot = orc.OracleTrainer(sd, "resnet50", warmup=2, total=10, dropout=0.0)
+    olp, oloss = ot.forward_backward(orc.to_torch_batch(nb))
+    lp_err = float(np.abs(lp - olp.numpy()).max())
+    lrel = abs(loss - float(oloss)) / abs(float(oloss))
+    gn, ogn = eng.grad_norm(), float(ot.grad_norm())
+    nrel = abs(gn - ogn) / ogn
+    parity_report["oracle_r50_384_l16"] = {"log_prob_max_abs": lp_err, "loss_rel": lrel, "grad_norm_rel": nrel}
+    assert lp_err <= LP_TOL, lp_err
+    assert lrel <= LOSS_RTOL, lrel
+    assert nrel <= GN_RTOL, nrel
