@@ -58,6 +58,23 @@ def cpu_baseline(pkg, batch=64, steps=5, warm=2):
                       f"({t:.2f} s/step), torch CPU {threads} threads"}
 
 
+def calls_flop(eng):
+    """MFMA work of one step from the engine's prepared calls (GEMMs / implicit-GEMM convs:
+    2 m n k per batch item; attention: 4 lq lk dh forward, 8 backward, per (sample, head))."""
+    tot = 0.0
+    res = list(eng.res_calls) if eng.pipeline else []           # else they are in fwd_calls
+    for c in res + eng.fwd_calls + eng.bwd_calls:
+        if c.name == "vqa_gemm":
+            d = c.desc
+            tot += 2.0 * d.m * d.n * d.k * max(1, d.batch)
+        elif c.name == "vqa_gemm_pair":
+            tot += sum(2.0 * d.m * d.n * d.k for d in c.desc)
+        elif c.name in ("vqa_attn_fwd", "vqa_attn_bwd"):
+            d = c.desc
+            tot += (4.0 if c.name == "vqa_attn_fwd" else 8.0) * d.batch * d.heads * d.lq * d.lk * d.dh
+    return tot
+
+
 def vit_flop_per_pair(lq, ld, nv=197, d=768, dff=3072, vff=3072, layers=12):
     """Algorithmic FLOPs of one config-4 pair (VitVQAModel, vit_vqa_model.py:166-225): the frozen
     ViT forward, the T5 encoder and decoder forward + backward (x3: the input and weight
@@ -297,15 +314,18 @@ def main():
     # pair x B pairs; duration = the step's GPU time from HIP events on
     # the replay stream over the timed region; traffic = HBM bytes per step from the
     # committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes over every dispatch of one step.
-    step_flop = FLOP_PER_PAIR * B
+    # Other shapes (--image-size / --seq-len): the MFMA work of the prepared calls.
+    survey_cfg = (args.image_size, args.seq_len) == (224, 32)
+    step_flop = FLOP_PER_PAIR * B if survey_cfg else calls_flop(eng)
     step_tflops = step_flop / gpu_step / 1e12
-    st = pmc.get("step", {})
+    st = pmc.get("step", {}) if survey_cfg else {}
     roofline = {"bound": "mfma", "kernel": "whole train step (one hipGraph replay: ResNet50 fwd, ConvT, T5, 3xSGA, "
                                            "head, backward, clip, AdamW)",
                 "achieved": round(step_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(step_tflops / MFMA_PEAK_TFLOPS, 4),
                 "traffic": round(st["traffic_bytes"]) if "traffic_bytes" in st else None,
-                "flop_per_step": step_flop, "step_gpu_ms": round(gpu_step * 1e3, 4),
+                "flop_per_step": step_flop, "flop_per_step_calls": calls_flop(eng),
+                "step_gpu_ms": round(gpu_step * 1e3, 4),
                 "traffic_source": f"profiles/{PMC_FILE} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, all dispatches of one step)"}
     out = {
         "metric": "question-image pairs/sec, ResNet50+T5-base+SGA train step, 1/2/4/8 MI355X",
