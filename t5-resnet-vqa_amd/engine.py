@@ -184,6 +184,10 @@ class VQAEngine:
         self.sq_overlap = os.environ.get("VQA_SQ_OVERLAP", "1") != "0"
         # ... and its [0, a) part as soon as the first T5 weight-gradient group is final
         self._sq_early = os.environ.get("VQA_SQ_EARLY", "1") != "0"
+        # bias / norm-affine column sums tagged for the weight-gradient stream (with dw_stream).
+        # Off: the extra cross-stream edges cost more than the chain waits (same box: 6.92-7.00
+        # vs 6.73-6.77 ms per step)
+        self.colsum_side = os.environ.get("VQA_COLSUM_SIDE", "0") == "1"
         # T5 RMSNorms folded into the next projection (vqa_gemm_desc.rownorm): the chain runs the
         # q|k|v (layers >= 1) and wi GEMMs on the unnormalised rows; the normalised rows the
         # weight gradients need are made by one batched launch beside the SGA forward.  Off by
@@ -537,6 +541,9 @@ class VQAEngine:
             keep += list(k)
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.dev)
         lst.append(ops.Call("vqa_colsum_batched", raw.data_ptr(), len(self._jobs), blk, keep=tuple(keep) + (raw,)))
+        # nothing on the input-gradient chain reads a finished bias / norm-affine gradient, so
+        # (VQA_COLSUM_SIDE=1) the reduction may trail the chain on the weight-gradient stream
+        lst[-1].side = getattr(self, "colsum_side", False)
         self._jobs = []
 
     def _norm_ws(self):
@@ -555,6 +562,7 @@ class VQAEngine:
         n = dy16.shape[-1]
         ws = self._t(lib.vqa_colsum_workspace_floats(rows, n))
         self._call(lst, "vqa_colsum", dy16, 1, rows, n, n, None, 0.0, ws)
+        lst[-1].side = getattr(self, "colsum_side", False)
         self._defer(ws, lib.vqa_colsum_parts(rows), n, n, self.g32[bname])
 
     def _dw(self, lst, dy16, x16, wname, rows, bias_from=None, bias_bf16=True):
@@ -569,6 +577,7 @@ class VQAEngine:
             lib = L.load()
             ws = self._t(lib.vqa_colsum_workspace_floats(rows, n))
             self._call(lst, "vqa_colsum", bias_from, int(bias_bf16), rows, n, n, None, 0.0, ws)
+            lst[-1].side = getattr(self, "colsum_side", False)
             self._defer(ws, lib.vqa_colsum_parts(rows), n, n, self.g32[wname[:-1] + "b"])
 
     # ------------------------------------------------------------------ forward plan
@@ -832,6 +841,7 @@ class VQAEngine:
         lib = L.load()
         ws = self._t(lib.vqa_colsum_workspace_floats(T, NB * W3))
         self._call(b, "vqa_colsum", dq, 1, T, NB * W3, NB * W3, None, 0.0, ws)
+        b[-1].side = getattr(self, "colsum_side", False)
         self._defer(ws, lib.vqa_colsum_parts(T), NB * W3, NB * W3, self.g32["sga0.qkv1_b"])
         self._jobs[-1] = self._jobs[-1][:-1] + (self._jobs[-1][-1] + keep,)
         mark(f"sga{NB - 1}.m1_b")
