@@ -1,5 +1,5 @@
 // Answer head: AttentionPooler (resnet_vqa_model.py:14-26) + classification
-// Linear(768, A) + log_softmax + NLLLoss(mean) (resnet_vqa_model.py:152-160),
+// Linear(768, A) (D up to 1024 for T5-large widths) + log_softmax + NLLLoss(mean) (resnet_vqa_model.py:152-160),
 // forward and backward, fp32 end to end (straight from the fp32 masters).
 //   pooler kernels: one workgroup per sample, each thread keeps its D/256
 //     columns of all L rows in registers, so scores, softmax, pooling and the
@@ -33,33 +33,39 @@ constexpr int MAXA = 1024;
 //                      pooler-weight partial sum_l dscore_l x_l (the thread owns its columns)
 //   head_wgrad         classifier dWc / dbc tiles (16 answers x 256 columns) and the fixed-order
 //                      sum of the per-sample pooler partials, in one two-role launch
-// Pooler kernels: 768 threads = 4 row groups x 192 float4 columns (D <= 768, D % 4 == 0);
-// a thread holds RPG = LMAX/4 rows of one float4 column in registers, so each sample is
-// read once with 16-B loads and the 12 waves of the workgroup share the instruction stream
-// (one wave per SIMD spent ~4x longer issuing the scalar-load form).  Row sums: a
-// reduce-scatter inside each wave, then the 3 waves of the row group in a fixed order.
-constexpr int PC4 = 192;                               // float4 columns per row group
-template <int RPG>
-__device__ __forceinline__ void pool_row_sums(float (&part)[RPG], float* red /*[12][RPG]*/, float* out, int L) {
+// Pooler kernels: 4 * PC4 threads = 4 row groups x PC4 float4 columns, PC4 = 192 for
+// D <= 768 (T5-base) and 256 for D <= 1024 (T5-large), D % 4 == 0; a thread holds
+// RPG = LMAX/4 rows of one float4 column in registers, so each sample is read once with
+// 16-B loads and the 12 (16) waves of the workgroup share the instruction stream (one wave
+// per SIMD spent ~4x longer issuing the scalar-load form).  Row sums: a reduce-scatter
+// inside each wave, then the WPG = PC4/64 waves of the row group in a fixed order.
+// (At 1024 threads the register cap is 128: the L > 32, D > 768 variants spill ~80 B/lane.)
+template <int RPG, int WPG>
+__device__ __forceinline__ void pool_row_sums(float (&part)[RPG], float* red /*[4*WPG][RPG]*/, float* out, int L) {
   constexpr int SH = RPG == 4 ? 4 : (RPG == 8 ? 3 : 2);   // lane >> SH = row index after the scatter
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
   const float v = wave_sum_scatter<RPG>(part);
   if ((l & ((1 << SH) - 1)) == 0) red[wv * RPG + (l >> SH)] = v;
   __syncthreads();
-  if (threadIdx.x < 4 * RPG) {                          // row r = group * RPG + i: waves 3g, 3g+1, 3g+2
+  if (threadIdx.x < 4 * RPG) {                          // row r = group * RPG + i: waves WPG*g .. WPG*g+WPG-1
     const int g = threadIdx.x / RPG, i = threadIdx.x - g * RPG;
-    if (g * RPG + i < L)
-      out[g * RPG + i] = (red[(3 * g) * RPG + i] + red[(3 * g + 1) * RPG + i]) + red[(3 * g + 2) * RPG + i];
+    if (g * RPG + i < L) {
+      float t = red[(WPG * g) * RPG + i];
+#pragma unroll
+      for (int j = 1; j < WPG; ++j) t += red[(WPG * g + j) * RPG + i];
+      out[g * RPG + i] = t;
+    }
   }
   __syncthreads();
 }
 
-template <int LMAX>
-__global__ __launch_bounds__(768) void head_pool_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wp,
+template <int LMAX, int PC4>
+__global__ __launch_bounds__(4 * PC4) void head_pool_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wp,
                                                             const float* __restrict__ bp, float* __restrict__ att,
                                                             float* __restrict__ pooled, int L, int D) {
   constexpr int RPG = LMAX / 4;
-  __shared__ float red[12 * RPG], sc[LMAX];
+  constexpr int WPG = PC4 / 64;
+  __shared__ float red[4 * WPG * RPG], sc[LMAX];
   __shared__ __attribute__((aligned(16))) float4 pr[4][PC4];
   const int b = blockIdx.x, tid = threadIdx.x, g = tid / PC4, c4 = tid - g * PC4, C4 = D / 4;
   const float cm = c4 < C4 ? 1.f : 0.f;
@@ -75,7 +81,7 @@ __global__ __launch_bounds__(768) void head_pool_fwd_kernel(const float* __restr
     xr[i] = make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
     part[i] = xr[i].x * w.x + xr[i].y * w.y + xr[i].z * w.z + xr[i].w * w.w;
   }
-  pool_row_sums<RPG>(part, red, sc, L);
+  pool_row_sums<RPG, WPG>(part, red, sc, L);
   if (tid < 64) {                                     // softmax over the sequence (Softmax(dim=1))
     const float s = tid < L ? sc[tid] + bp[0] : -INFINITY;
     const float m = wave_max(s);
@@ -101,28 +107,30 @@ __global__ __launch_bounds__(768) void head_pool_fwd_kernel(const float* __restr
 }
 
 // logits[b, a] = pooled[b, :] . Wc[a, :] + bc[a] for 8 answers x 16 samples per workgroup:
-// a lane holds float4 columns (lane, lane+64, lane+128) of the 8 Wc rows, each wave takes
-// 4 samples; one wave_sum_scatter<8> per sample finishes 8 dots at once (D <= 768, D % 4 == 0)
+// a lane holds float4 columns (lane, lane+64, ..., lane+64(NJ-1)) of the 8 Wc rows, each wave
+// takes 4 samples; one wave_sum_scatter<8> per sample finishes 8 dots at once
+// (D <= 256 NJ, D % 4 == 0: NJ = 3 for D <= 768, 4 for D <= 1024)
+template <int NJ>
 __global__ __launch_bounds__(256) void head_logits_kernel(const float* __restrict__ pooled,
                                                           const float* __restrict__ wc, const float* __restrict__ bc,
                                                           float* __restrict__ logits, int B, int D, int A) {
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int a0 = blockIdx.x * 8, s0 = blockIdx.y * 16 + wv * 4;
-  float4 wr[8][3];
+  float4 wr[8][NJ];
 #pragma unroll
   for (int u = 0; u < 8; ++u)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int k = 4 * (l + 64 * j), a = a0 + u;
       const float4 t = *reinterpret_cast<const float4*>(wc + (long)min(a, A - 1) * D + min(k, D - 4));
       const float m = (a < A && k < D) ? 1.f : 0.f;
       wr[u][j] = make_float4(t.x * m, t.y * m, t.z * m, t.w * m);
     }
-  float4 pv[4][3];
+  float4 pv[4][NJ];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int k = 4 * (l + 64 * j);
       const float4 t = *reinterpret_cast<const float4*>(pooled + (long)min(s0 + q, B - 1) * D + min(k, D - 4));
       const float m = k < D ? 1.f : 0.f;
@@ -137,7 +145,7 @@ __global__ __launch_bounds__(256) void head_logits_kernel(const float* __restric
     for (int u = 0; u < 8; ++u) {
       float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
+      for (int j = 0; j < NJ; ++j)
         s += pv[q][j].x * wr[u][j].x + pv[q][j].y * wr[u][j].y + pv[q][j].z * wr[u][j].z + pv[q][j].w * wr[u][j].w;
       sv[u] = s;
     }
@@ -258,15 +266,16 @@ __global__ __launch_bounds__(256) void head_dpooled_kernel(const float* __restri
 // Pooler backward of one sample: da = x dpooled ; dscore = a (da - sum a da) ;
 // dx = a dpooled^T + dscore wp^T ; and the sample's pooler weight / bias partials
 // part[b, d] = sum_l dscore_l x[l, d], pbp[b] = sum_l dscore_l (summed over b by head_wgrad).
-// Same 4 row groups x 192 float4 columns layout as head_pool_fwd_kernel.
-template <int LMAX>
-__global__ __launch_bounds__(768) void head_pool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ att,
+// Same 4 row groups x PC4 float4 columns layout as head_pool_fwd_kernel.
+template <int LMAX, int PC4>
+__global__ __launch_bounds__(4 * PC4) void head_pool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ att,
                                                             const float* __restrict__ dpooled,
                                                             const float* __restrict__ wp, float* __restrict__ dx32,
                                                             bf16_t* __restrict__ dx16, float* __restrict__ part,
                                                             float* __restrict__ pbp, int L, int D) {
   constexpr int RPG = LMAX / 4;
-  __shared__ float red[12 * RPG], da[LMAX], a[LMAX];
+  constexpr int WPG = PC4 / 64;
+  __shared__ float red[4 * WPG * RPG], da[LMAX], a[LMAX];
   __shared__ __attribute__((aligned(16))) float4 pr[4][PC4];
   const int b = blockIdx.x, tid = threadIdx.x, g = tid / PC4, c4 = tid - g * PC4, C4 = D / 4;
   const float cm = c4 < C4 ? 1.f : 0.f;
@@ -285,7 +294,7 @@ __global__ __launch_bounds__(768) void head_pool_bwd_kernel(const float* __restr
     xr[i] = make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
     pt[i] = xr[i].x * dp.x + xr[i].y * dp.y + xr[i].z * dp.z + xr[i].w * dp.w;
   }
-  pool_row_sums<RPG>(pt, red, da, L);
+  pool_row_sums<RPG, WPG>(pt, red, da, L);
   if (tid < 64) {
     const float ai = tid < L ? a[tid] : 0.f, dai = tid < L ? da[tid] : 0.f;
     const float s = wave_sum(ai * dai);
@@ -407,6 +416,13 @@ int with_lmax(int L, F f) {
   return f(std::integral_constant<int, 64>());
 }
 
+// float4 columns per pooler row group: 192 up to D = 768 (unchanged T5-base kernels), 256 up to 1024
+template <typename F>
+int with_pc4(int D, F f) {
+  if (D <= 768) return f(std::integral_constant<int, 192>());
+  return f(std::integral_constant<int, 256>());
+}
+
 }  // namespace
 
 extern "C" int vqa_head_workspace_floats(int batch, int seq, int d, int answers) {
@@ -419,17 +435,23 @@ extern "C" int vqa_head_fwd(const float* x, const float* wp, const float* bp, co
                             const long long* targets, float* att, float* pooled, float* logp, float* nll, float* loss,
                             int batch, int seq, int d, int answers, hipStream_t s) {
   VQA_REQUIRE(x && wp && bp && wc && bc && att && pooled && logp, "vqa_head_fwd: null argument");
-  VQA_REQUIRE(seq <= 64 && d <= 768 && d % 4 == 0 && answers <= MAXA && batch <= 1024,
-              "vqa_head_fwd: shape out of range (L<=64, D<=768, D%4==0, A<=1024, B<=1024)");
+  VQA_REQUIRE(seq >= 1 && seq <= 64 && d >= 4 && d <= 1024 && d % 4 == 0 && answers >= 1 && answers <= MAXA &&
+                  batch >= 1 && batch <= 1024,
+              "vqa_head_fwd: shape out of range (1<=L<=64, 4<=D<=1024, D%4==0, 1<=A<=1024, 1<=B<=1024)");
   VQA_REQUIRE(!targets || (nll && loss), "vqa_head_fwd: targets need nll and loss outputs");
   int rc = with_lmax(seq, [&](auto lm) {
-    hipLaunchKernelGGL(head_pool_fwd_kernel<decltype(lm)::value>, dim3(batch), dim3(768), 0, s, x, wp, bp, att, pooled,
-                       seq, d);
-    return vqa::check_launch("vqa_head_fwd/pool");
+    return with_pc4(d, [&](auto pc) {
+      hipLaunchKernelGGL((head_pool_fwd_kernel<decltype(lm)::value, decltype(pc)::value>), dim3(batch),
+                         dim3(4 * decltype(pc)::value), 0, s, x, wp, bp, att, pooled, seq, d);
+      return vqa::check_launch("vqa_head_fwd/pool");
+    });
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(head_logits_kernel, dim3(vqa::cdiv(answers, 8), vqa::cdiv(batch, 16)), dim3(256), 0, s, pooled, wc,
-                     bc, logp, batch, d, answers);
+  const dim3 lg(vqa::cdiv(answers, 8), vqa::cdiv(batch, 16));
+  if (d <= 768)
+    hipLaunchKernelGGL(head_logits_kernel<3>, lg, dim3(256), 0, s, pooled, wc, bc, logp, batch, d, answers);
+  else
+    hipLaunchKernelGGL(head_logits_kernel<4>, lg, dim3(256), 0, s, pooled, wc, bc, logp, batch, d, answers);
   if ((rc = vqa::check_launch("vqa_head_fwd/logits"))) return rc;
   if (answers <= 256)
     hipLaunchKernelGGL(head_lse_kernel<4>, dim3(1), dim3(1024), 0, s, logp, targets, nll, loss, batch, answers);
@@ -445,7 +467,9 @@ extern "C" int vqa_head_bwd(const float* x, const float* att, const float* poole
                             int answers, hipStream_t s) {
   VQA_REQUIRE(x && att && pooled && logp && targets && wp && wc && dx32 && dwp && dbp && dwc && dbc && ws,
               "vqa_head_bwd: null argument");
-  VQA_REQUIRE(seq <= 64 && d <= 768 && answers <= 4 * DP_AQ, "vqa_head_bwd: shape out of range (A <= 192)");
+  VQA_REQUIRE(seq >= 1 && seq <= 64 && d >= 4 && d <= 1024 && d % 4 == 0 && answers >= 1 && answers <= 4 * DP_AQ &&
+                  batch >= 1,
+              "vqa_head_bwd: shape out of range (1<=L<=64, 4<=D<=1024, D%4==0, 1<=A<=192)");
   float* pbp = ws;
   float* dl = pbp + batch;
   float* dpool = dl + batch * answers;
@@ -455,9 +479,12 @@ extern "C" int vqa_head_bwd(const float* x, const float* att, const float* poole
   int rc = vqa::check_launch("vqa_head_bwd/dpooled");
   if (rc) return rc;
   rc = with_lmax(seq, [&](auto lm) {
-    hipLaunchKernelGGL(head_pool_bwd_kernel<decltype(lm)::value>, dim3(batch), dim3(768), 0, s, x, att, dpool, wp, dx32,
-                       (bf16_t*)dx16, part, pbp, seq, d);
-    return vqa::check_launch("vqa_head_bwd/pool");
+    return with_pc4(d, [&](auto pc) {
+      hipLaunchKernelGGL((head_pool_bwd_kernel<decltype(lm)::value, decltype(pc)::value>), dim3(batch),
+                         dim3(4 * decltype(pc)::value), 0, s, x, att, dpool, wp, dx32, (bf16_t*)dx16, part, pbp, seq,
+                         d);
+      return vqa::check_launch("vqa_head_bwd/pool");
+    });
   });
   if (rc) return rc;
   const int ncd = vqa::cdiv(d, 256), nca = vqa::cdiv(answers, 16);
