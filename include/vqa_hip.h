@@ -334,8 +334,8 @@ int vqa_xattn1_bwd(const void* dctx, long long ldd, float* dv32, void* dv16, lon
  * AttentionPooler (resnet_vqa_model.py:14-26) + classification_layer +
  * log_softmax + NLLLoss mean (:152-160).  fp32.  targets may be NULL in
  * forward (loss is then not computed, like annotation_ids=None).
- * Limits: seq <= 64, d <= 1024 (d % 4 == 0; 1024 = T5-large), batch <= 1024; answers <= 1024
- * forward, <= 192 backward.  The forward writes the logits through logp.
+ * Limits: seq <= 64, d <= 1024 (d % 4 == 0; 1024 = T5-large), batch <= 1024, answers <= 1024.
+ * The forward writes the logits through logp.
  * ws = vqa_head_workspace_floats(batch, seq, d, answers) floats. */
 int vqa_head_fwd(const float* x, const float* wp, const float* bp, const float* wc, const float* bc,
                  const long long* targets, float* att, float* pooled, float* logp, float* nll, float* loss,

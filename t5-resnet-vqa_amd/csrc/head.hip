@@ -205,9 +205,12 @@ __global__ __launch_bounds__(1024) void head_lse_kernel(float* __restrict__ lp, 
 }
 
 // dlogits (kept for the classifier weight gradient) and dpooled = dlogits Wc.
-// Workgroup = 64 columns x 16 samples; wave w sums answers [w*AQ, (w+1)*AQ) with all of its
-// Wc loads in flight, then the four wave partials are added in a fixed order through LDS.
-constexpr int DP_AQ = 48;                             // answers per wave (4 * 48 >= A)
+// Workgroup = 64 columns x 16 samples; the answers go in chunks of 4 * AQ = 192 (one chunk
+// for DAQUAR's 170): in each chunk wave w sums answers [c + w*AQ, c + (w+1)*AQ) with all of
+// its Wc loads in flight, carrying its partial from chunk to chunk; the four wave partials
+// are then added in a fixed order through LDS.
+constexpr int DP_AQ = 48;                             // answers per wave and chunk
+template <bool CHUNKED>                               // false: A <= 192, one chunk (straight-line code)
 __global__ __launch_bounds__(256) void head_dpooled_kernel(const float* __restrict__ lp,
                                                            const long long* __restrict__ tgt,
                                                            const float* __restrict__ wc, float* __restrict__ dl_out,
@@ -219,39 +222,44 @@ __global__ __launch_bounds__(256) void head_dpooled_kernel(const float* __restri
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const int c = blockIdx.x * 64 + l, s0 = blockIdx.y * 16;
   constexpr int FI = 16 * AP / 256;                   // fill elements per thread (all loads first)
-  float ev[FI];
-  int tv[FI];
-#pragma unroll
-  for (int k = 0; k < FI; ++k) {
-    const int i = tid + 256 * k, q = i / AP, a = i - q * AP, b = min(s0 + q, B - 1);
-    ev[k] = lp[(long)b * A + min(a, A - 1)];
-    tv[k] = (int)tgt[b];
-  }
-#pragma unroll
-  for (int k = 0; k < FI; ++k) {
-    const int i = tid + 256 * k, q = i / AP, a = i - q * AP, b = s0 + q;
-    const float g = (b < B && a < A) ? (__expf(ev[k]) - (a == tv[k] ? 1.f : 0.f)) * inv_b : 0.f;
-    dl[q][a] = g;
-    if (blockIdx.x == 0 && b < B && a < A) dl_out[(long)b * A + a] = g;
-  }
-  float w[DP_AQ];
-#pragma unroll
-  for (int i = 0; i < DP_AQ; ++i)
-    w[i] = wc[(long)min(wv * DP_AQ + i, A - 1) * D + min(c, D - 1)];   // masked through dl = 0 past A
-  __syncthreads();
   float acc[16];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    float s = 0.f;
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  for (int c0 = 0; c0 < (CHUNKED ? A : 1); c0 += AP) {
+    float ev[FI];
+    int tv[FI];
 #pragma unroll
-    for (int i = 0; i < DP_AQ; i += 4) {
-      const float4 g = *reinterpret_cast<const float4*>(&dl[q][wv * DP_AQ + i]);
-      s = fmaf(g.x, w[i], s);
-      s = fmaf(g.y, w[i + 1], s);
-      s = fmaf(g.z, w[i + 2], s);
-      s = fmaf(g.w, w[i + 3], s);
+    for (int k = 0; k < FI; ++k) {
+      const int i = tid + 256 * k, q = i / AP, a = c0 + i - q * AP, b = min(s0 + q, B - 1);
+      ev[k] = lp[(long)b * A + min(a, A - 1)];
+      tv[k] = (int)tgt[b];
     }
-    acc[q] = s;
+    if (c0) __syncthreads();                          // the previous chunk's dl has been read
+#pragma unroll
+    for (int k = 0; k < FI; ++k) {
+      const int i = tid + 256 * k, q = i / AP, j = i - q * AP, a = c0 + j, b = s0 + q;
+      const float g = (b < B && a < A) ? (__expf(ev[k]) - (a == tv[k] ? 1.f : 0.f)) * inv_b : 0.f;
+      dl[q][j] = g;
+      if (blockIdx.x == 0 && b < B && a < A) dl_out[(long)b * A + a] = g;
+    }
+    float w[DP_AQ];
+#pragma unroll
+    for (int i = 0; i < DP_AQ; ++i)
+      w[i] = wc[(long)min(c0 + wv * DP_AQ + i, A - 1) * D + min(c, D - 1)];   // masked through dl = 0 past A
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      float s = acc[q];                                 // 0 in the first chunk: A <= 192 sums as before
+#pragma unroll
+      for (int i = 0; i < DP_AQ; i += 4) {
+        const float4 g = *reinterpret_cast<const float4*>(&dl[q][wv * DP_AQ + i]);
+        s = fmaf(g.x, w[i], s);
+        s = fmaf(g.y, w[i + 1], s);
+        s = fmaf(g.z, w[i + 2], s);
+        s = fmaf(g.w, w[i + 3], s);
+      }
+      acc[q] = s;
+    }
   }
 #pragma unroll
   for (int q = 0; q < 16; ++q) red[wv][q][l] = acc[q];
@@ -467,15 +475,20 @@ extern "C" int vqa_head_bwd(const float* x, const float* att, const float* poole
                             int answers, hipStream_t s) {
   VQA_REQUIRE(x && att && pooled && logp && targets && wp && wc && dx32 && dwp && dbp && dwc && dbc && ws,
               "vqa_head_bwd: null argument");
-  VQA_REQUIRE(seq >= 1 && seq <= 64 && d >= 4 && d <= 1024 && d % 4 == 0 && answers >= 1 && answers <= 4 * DP_AQ &&
-                  batch >= 1,
-              "vqa_head_bwd: shape out of range (1<=L<=64, 4<=D<=1024, D%4==0, 1<=A<=192)");
+  VQA_REQUIRE(seq >= 1 && seq <= 64 && d >= 4 && d <= 1024 && d % 4 == 0 && answers >= 1 && answers <= MAXA &&
+                  batch >= 1 && batch <= 1024,
+              "vqa_head_bwd: shape out of range (1<=L<=64, 4<=D<=1024, D%4==0, 1<=A<=1024, 1<=B<=1024)");
   float* pbp = ws;
   float* dl = pbp + batch;
   float* dpool = dl + batch * answers;
   float* part = dpool + batch * d;
-  hipLaunchKernelGGL(head_dpooled_kernel, dim3(vqa::cdiv(d, 64), vqa::cdiv(batch, 16)), dim3(256), 0, s, logp, targets,
-                     wc, dl, dpool, batch, d, answers, 1.0f / batch);
+  const dim3 dg(vqa::cdiv(d, 64), vqa::cdiv(batch, 16));
+  if (answers <= 4 * DP_AQ)
+    hipLaunchKernelGGL(head_dpooled_kernel<false>, dg, dim3(256), 0, s, logp, targets, wc, dl, dpool, batch, d, answers,
+                       1.0f / batch);
+  else
+    hipLaunchKernelGGL(head_dpooled_kernel<true>, dg, dim3(256), 0, s, logp, targets, wc, dl, dpool, batch, d, answers,
+                       1.0f / batch);
   int rc = vqa::check_launch("vqa_head_bwd/dpooled");
   if (rc) return rc;
   rc = with_lmax(seq, [&](auto lm) {

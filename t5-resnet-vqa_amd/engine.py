@@ -138,10 +138,10 @@ class VQAEngine:
         self.vision, self.B, self.L, self.H = vision, batch, seq_len, image_size
         assert image_size % 2 == 0, "the space-to-depth stem needs an even image size"
         self.NB, self.A = num_blocks, answer_spaces
-        # the answer head's backward keeps one sample's answer logits in registers (head.hip
-        # vqa_head_bwd: A <= 192; DAQUAR has 170) and the pooler one sample's tokens (L <= 64)
-        if not 1 <= answer_spaces <= 192:
-            raise ValueError(f"answer_spaces={answer_spaces}: the fused answer head supports 1..192 answers")
+        # the answer head's log-softmax keeps one sample's answer logits in registers (head.hip:
+        # A <= 1024; DAQUAR has 170) and the pooler one sample's tokens (L <= 64)
+        if not 1 <= answer_spaces <= 1024:
+            raise ValueError(f"answer_spaces={answer_spaces}: the fused answer head supports 1..1024 answers")
         if not 1 <= seq_len <= 64:
             raise ValueError(f"seq_len={seq_len}: the attention / pooler kernels support 1..64 question tokens")
         self.warmup, self.total, self.max_norm = warmup, total, max_norm

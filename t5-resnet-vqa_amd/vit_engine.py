@@ -75,8 +75,8 @@ class VitVQAEngine:
                  device="cuda:0", warmup=10, total=100, answer_spaces=170, max_norm=1.0, betas=(0.9, 0.999),
                  eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0, group_lr=None):
         L.load()
-        if not 1 <= answer_spaces <= 192:
-            raise ValueError(f"answer_spaces={answer_spaces}: the fused answer head supports 1..192 answers")
+        if not 1 <= answer_spaces <= 1024:
+            raise ValueError(f"answer_spaces={answer_spaces}: the fused answer head supports 1..1024 answers")
         if not (1 <= seq_len <= 32 and 1 <= dec_len <= 32):
             raise ValueError("seq_len and dec_len must be in 1..32 (one 32-query MFMA attention tile)")
         if image_size % VM.VIT_PATCH:

@@ -157,10 +157,12 @@ def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5, pd):
 
 
 @pytest.mark.parametrize("B,L,A,D", [(8, 32, 170, 768), (64, 32, 170, 768), (37, 49, 13, 768), (5, 16, 192, 768),
-                                     (64, 32, 170, 1024), (19, 49, 37, 1024), (6, 16, 192, 836), (3, 7, 5, 20)])
+                                     (64, 32, 170, 1024), (19, 49, 37, 1024), (6, 16, 192, 836), (3, 7, 5, 20),
+                                     (16, 32, 193, 768), (21, 32, 700, 768), (5, 16, 1024, 1024)])
 def test_head_fwd_bwd(k, B, L, A, D):
     """D = 1024 is T5-large's width (BASELINE config 5); 836 / 20 exercise the masked
-    column tail of the 256- and 192-column pooler layouts."""
+    column tail of the 256- and 192-column pooler layouts; A > 192 the chunked answer
+    loop of the dpooled kernel (193: a one-answer second chunk)."""
     x = rnd((B, L, D), 20)
     wp, bp = 0.03 * rnd(D, 21), 0.1 * rnd(1, 22)
     wc, bc = 0.03 * rnd((A, D), 23), 0.1 * rnd(A, 24)

@@ -323,3 +323,28 @@ def test_engine_matches_oracle_at_384(cuda, pkg, parity_report):
     assert lp_err <= LP_TOL, lp_err
     assert lrel <= LOSS_RTOL, lrel
     assert nrel <= GN_RTOL, nrel
+
+
+def test_engine_matches_oracle_with_700_answers(cuda, pkg, parity_report):
+    """An answer vocabulary wider than one 192-answer chunk of the head backward
+    (answer_spaces is the dataset's answer count in the reference, resnet_vqa_model.py:89):
+    one eval-mode step at B = 3, L = 16 against the fp32 oracle, plus the classifier
+    gradient itself."""
+    from oracle import vqa_oracle as orc
+    B, L, H, A = 3, 16, 224, 700
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, answer_spaces=A)
+    nb = pkg.synthetic.make_batch(B, L, H, seed=1, answer_spaces=A)
+    eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, warmup=2, total=10,
+                               dropout=0.0, answer_spaces=A)
+    lp, loss = eng.forward_backward(nb)
+    assert lp.shape == (B, A)
+    ot = orc.OracleTrainer(sd, "resnet50", warmup=2, total=10, dropout=0.0)
+    olp, oloss = ot.forward_backward(orc.to_torch_batch(nb))
+    lp_err = float(np.abs(lp - olp.numpy()).max())
+    lrel = abs(loss - float(oloss)) / abs(float(oloss))
+    gn, ogn = eng.grad_norm(), float(ot.grad_norm())
+    nrel = abs(gn - ogn) / ogn
+    parity_report["oracle_r50_224_l16_a700"] = {"log_prob_max_abs": lp_err, "loss_rel": lrel, "grad_norm_rel": nrel}
+    assert lp_err <= LP_TOL, lp_err
+    assert lrel <= LOSS_RTOL, lrel
+    assert nrel <= GN_RTOL, nrel
