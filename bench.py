@@ -193,6 +193,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--seq-len", type=int, default=32)
     ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--blocks", type=int, default=3, help="SGA blocks (3: the reference default; 6: BASELINE config 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-kernel-rooflines", action="store_true", help="skip the per-kernel replays after the timed region")
@@ -235,9 +236,10 @@ def main():
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     pkg = load_package()
     B, L, H = args.batch, args.seq_len, args.image_size
-    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)       # identical init on every rank
+    NB = args.blocks
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, num_attention_blocks=NB)   # identical init on every rank
     pipe = not args.no_pipeline
-    eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev,
+    eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev, num_blocks=NB,
                                warmup=10, total=100000, dropout=0.1, seed=rank, pipeline=pipe,
                                t5_dw_group=None if world == 1 else pkg.dp.DP_T5_DW_GROUPS)
     del sd
@@ -315,11 +317,11 @@ def main():
     # the replay stream over the timed region; traffic = HBM bytes per step from the
     # committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes over every dispatch of one step.
     # Other shapes (--image-size / --seq-len): the MFMA work of the prepared calls.
-    survey_cfg = (args.image_size, args.seq_len) == (224, 32)
+    survey_cfg = (args.image_size, args.seq_len, NB) == (224, 32, 3)
     step_flop = FLOP_PER_PAIR * B if survey_cfg else calls_flop(eng)
     step_tflops = step_flop / gpu_step / 1e12
     st = pmc.get("step", {}) if survey_cfg else {}
-    roofline = {"bound": "mfma", "kernel": "whole train step (one hipGraph replay: ResNet50 fwd, ConvT, T5, 3xSGA, "
+    roofline = {"bound": "mfma", "kernel": f"whole train step (one hipGraph replay: ResNet50 fwd, ConvT, T5, {NB}xSGA, "
                                            "head, backward, clip, AdamW)",
                 "achieved": round(step_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(step_tflops / MFMA_PEAK_TFLOPS, 4),
@@ -332,8 +334,9 @@ def main():
         "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-        "config": {"workload": "ResNet50 + T5-base + 3xSGA train step (BASELINE configs[1]; configs[2] at N=8)",
-                   "model": "resnet50+t5-base+3xSGA", "global_batch": world * B, "per_gpu_batch": B,
+        "config": {"workload": (f"ResNet50 + T5-base + {NB}xSGA train step"
+                                + (" (BASELINE configs[1]; configs[2] at N=8)" if survey_cfg else "")),
+                   "model": f"resnet50+t5-base+{NB}xSGA", "global_batch": world * B, "per_gpu_batch": B,
                    "seq_len": L, "image_size": H, "answers": 170, "parallelism": f"dp{world}",
                    "world_size": (dist.get_world_size() if dist else 1), "graph": not args.no_graph,
                    "resnet_pipelined": pipe},
@@ -349,7 +352,7 @@ def main():
         dist.all_gather(ps, p)
         out["rehearsal_lockstep"] = all(torch.equal(q, ps[0]) for q in ps)
     elif not args.no_kernel_rooflines:
-        out.update(kernel_rooflines(eng, stream, pmc))
+        out.update(kernel_rooflines(eng, stream, pmc if survey_cfg else {}))   # PMC figures: the committed shape only
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pkg)
     if rank == 0:

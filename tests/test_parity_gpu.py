@@ -348,3 +348,27 @@ def test_engine_matches_oracle_with_700_answers(cuda, pkg, parity_report):
     assert lp_err <= LP_TOL, lp_err
     assert lrel <= LOSS_RTOL, lrel
     assert nrel <= GN_RTOL, nrel
+
+
+def test_engine_matches_oracle_six_blocks_at_384(cuda, pkg, parity_report):
+    """BASELINE config 5's SGA depth and image size (6 blocks, 384 x 384: block 0 attends over
+    144 vision tokens) at T5-base width, one eval-mode step at B = 2, L = 16 against the fp32
+    oracle; the engine's per-block plan, gradient groups and AdamW ranges grow with the depth."""
+    from oracle import vqa_oracle as orc
+    B, L, H, NB = 2, 16, 384, 6
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, num_attention_blocks=NB)
+    nb = pkg.synthetic.make_batch(B, L, H, seed=1)
+    eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, warmup=2, total=10,
+                               dropout=0.0, num_blocks=NB)
+    assert len(eng.sga) == NB
+    lp, loss = eng.forward_backward(nb)
+    ot = orc.OracleTrainer(sd, "resnet50", warmup=2, total=10, dropout=0.0, num_blocks=NB)
+    olp, oloss = ot.forward_backward(orc.to_torch_batch(nb))
+    lp_err = float(np.abs(lp - olp.numpy()).max())
+    lrel = abs(loss - float(oloss)) / abs(float(oloss))
+    gn, ogn = eng.grad_norm(), float(ot.grad_norm())
+    nrel = abs(gn - ogn) / ogn
+    parity_report["oracle_r50_384_l16_6blocks"] = {"log_prob_max_abs": lp_err, "loss_rel": lrel, "grad_norm_rel": nrel}
+    assert lp_err <= LP_TOL, lp_err
+    assert lrel <= LOSS_RTOL, lrel
+    assert nrel <= GN_RTOL, nrel
