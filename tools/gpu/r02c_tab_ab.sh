@@ -1,5 +1,6 @@
 #!/bin/bash
 # same-box A/B: config-2 bench with the table before the config-4 re-time vs the current table
+# (first: git show 4929727:t5-resnet-vqa_amd/tuning/gemm_gfx950.json > tools/gpu/_old_table.json)
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 i=0
