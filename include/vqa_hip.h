@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 11
+#define VQA_ABI_VERSION 12
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -187,6 +187,14 @@ typedef struct vqa_attn_desc {
 
 int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t stream);
 int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t stream);
+/* which kernel vqa_attn_fwd (backward = 0) / vqa_attn_bwd (1) runs for d: the MFMA kernels
+ * (lq <= 32, lk <= 160, dh 64 / 96 / 128; key mask only with lk <= 64), the long
+ * online-softmax forward, or the scalar VALU kernel every other shape falls back to (an
+ * order of magnitude slower: callers that plan a step check this and say so). */
+#define VQA_ATTN_MFMA 0
+#define VQA_ATTN_LONG 1
+#define VQA_ATTN_VALU 2
+int vqa_attn_path(const vqa_attn_desc* d, int backward);
 
 /* ----------------------------------------------------------------- norms ---
  * Rows of width d (d % 256 == 0, d <= 1024), fp32 in, fp32 and/or bf16 out.
@@ -304,6 +312,8 @@ int vqa_t5_relbias_bwd(const float* dbias, const int* bucket, float* dtable, int
 int vqa_batch_sum(const float* x, int batch, long long n, float* out, float beta, hipStream_t stream);
 int vqa_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t stream);
 int vqa_zero(void* p, long long bytes, hipStream_t stream);
+/* dst <- src, 16-byte aligned (a kernel, so a captured step holds no runtime memcpy node) */
+int vqa_copy(void* dst, const void* src, long long bytes, hipStream_t stream);
 
 /* ------------------------------------------------ config 4: ViT + T5 enc-dec ---
  * VitVQAModel (model/vit_vqa_model.py:127-227) data movement (vit.hip):

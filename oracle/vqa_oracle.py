@@ -29,8 +29,8 @@ import torch.nn.functional as F
 T5_EPS = 1e-6          # T5LayerNorm eps (t5-base config layer_norm_epsilon)
 LN_EPS = 1e-5          # nn.LayerNorm default (multi_head_vision_text_attn.py:123)
 BN_EPS = 1e-5          # torchvision BatchNorm2d default
-SGA_HEADS, SGA_DHEAD = 8, 96     # multi_head_vision_text_attn.py:7-14
-T5_HEADS, T5_DKV = 12, 64
+SGA_HEADS, SGA_DHEAD = 8, 96     # multi_head_vision_text_attn.py:7-14 (t5-base width; head dim = width / 8)
+T5_HEADS, T5_DKV = 12, 64        # t5-base; the encoder below reads heads / layers off the state dict
 T5_BUCKETS, T5_MAX_DIST = 32, 128
 
 
@@ -169,19 +169,23 @@ def t5_encoder(sd, ids, mask, prefix="lang_model.", drop=_nodrop):
     `drop` applies the train-mode dropouts (identity = eval mode)."""
     g = lambda k: sd[prefix + k]
     B, L = ids.shape
+    rel_emb = g("block.0.layer.0.SelfAttention.relative_attention_bias.weight")
+    nh = rel_emb.shape[1]                                              # 12 (t5-base) / 16 (t5-large)
+    dkv = g("block.0.layer.0.SelfAttention.q.weight").shape[0] // nh   # 64
+    nl = sum(1 for k in sd if k.startswith(prefix + "block.") and k.endswith(".layer.0.layer_norm.weight"))
     h = drop(SITE_EMBED, g("embed_tokens.weight")[ids])                # :678, dropout :725
     ext = (1.0 - mask[:, None, None, :].float()) * torch.finfo(torch.float32).min   # bidirectional mask
-    bias = t5_position_bias(g("block.0.layer.0.SelfAttention.relative_attention_bias.weight"), L, L)
-    for i in range(12):
+    bias = t5_position_bias(rel_emb, L, L)
+    for i in range(nl):
         p = f"block.{i}.layer."
         n = t5_rmsnorm(h, g(p + "0.layer_norm.weight"))                # T5LayerSelfAttention :384-401
-        q = (n @ g(p + "0.SelfAttention.q.weight").T).view(B, L, T5_HEADS, T5_DKV).transpose(1, 2)
-        k = (n @ g(p + "0.SelfAttention.k.weight").T).view(B, L, T5_HEADS, T5_DKV).transpose(1, 2)
-        v = (n @ g(p + "0.SelfAttention.v.weight").T).view(B, L, T5_HEADS, T5_DKV).transpose(1, 2)
+        q = (n @ g(p + "0.SelfAttention.q.weight").T).view(B, L, nh, dkv).transpose(1, 2)
+        k = (n @ g(p + "0.SelfAttention.k.weight").T).view(B, L, nh, dkv).transpose(1, 2)
+        v = (n @ g(p + "0.SelfAttention.v.weight").T).view(B, L, nh, dkv).transpose(1, 2)
         s = q @ k.transpose(2, 3)                                      # no 1/sqrt(d) (scaling = 1.0)
         s = s + bias + ext
         a = drop(t5_site(i, 0), torch.softmax(s.float(), dim=-1))     # :168
-        o = (a @ v).transpose(1, 2).reshape(B, L, T5_HEADS * T5_DKV)
+        o = (a @ v).transpose(1, 2).reshape(B, L, nh * dkv)
         h = h + drop(t5_site(i, 1), o @ g(p + "0.SelfAttention.o.weight").T)     # :400
         n = t5_rmsnorm(h, g(p + "1.layer_norm.weight"))                # T5LayerFF :126-141
         f = drop(t5_site(i, 2), F.relu(n @ g(p + "1.DenseReluDense.wi.weight").T))  # :86
@@ -195,14 +199,16 @@ def _linear(x, sd, p):
 
 
 def sga_mhatt(sd, p, v, k, q, drop=_nodrop, site=0):
-    """MHAtt.forward + att (multi_head_vision_text_attn.py:38-86), mask=None."""
+    """MHAtt.forward + att (multi_head_vision_text_attn.py:38-86), mask=None.  MULTI_HEAD = 8
+    heads of HIDDEN_SIZE / 8 (96 at the reference's 768, 128 at config 5's 1024)."""
     B = q.shape[0]
-    V = _linear(v, sd, p + ".linear_v").view(B, -1, SGA_HEADS, SGA_DHEAD).transpose(1, 2)
-    K = _linear(k, sd, p + ".linear_k").view(B, -1, SGA_HEADS, SGA_DHEAD).transpose(1, 2)
-    Q = _linear(q, sd, p + ".linear_q").view(B, -1, SGA_HEADS, SGA_DHEAD).transpose(1, 2)
-    s = (Q @ K.transpose(-2, -1)) / math.sqrt(SGA_DHEAD)
+    dh = sd[p + ".linear_q.weight"].shape[0] // SGA_HEADS
+    V = _linear(v, sd, p + ".linear_v").view(B, -1, SGA_HEADS, dh).transpose(1, 2)
+    K = _linear(k, sd, p + ".linear_k").view(B, -1, SGA_HEADS, dh).transpose(1, 2)
+    Q = _linear(q, sd, p + ".linear_q").view(B, -1, SGA_HEADS, dh).transpose(1, 2)
+    s = (Q @ K.transpose(-2, -1)) / math.sqrt(dh)
     a = drop(site, torch.softmax(s, dim=-1))                          # :83-84
-    o = (a @ V).transpose(1, 2).contiguous().view(B, -1, SGA_HEADS * SGA_DHEAD)
+    o = (a @ V).transpose(1, 2).contiguous().view(B, -1, SGA_HEADS * dh)
     return _linear(o, sd, p + ".linear_merge")
 
 

@@ -70,7 +70,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnP P) {
     const int i = idx / lk, j = idx - i * lk;
     float s = rowdot(Qs + i * st, Ks + j * st, w2) * P.scale;
     if (P.bias) s += P.bias[((long)h * lq + i) * lk + j];
-    if (P.mask && P.mask[(long)b * lk + j] == 0) s += MASK_MIN;
+    if (P.mask && P.mask[(long)b * lk + j] == 0 && !(P.bias && P.bias[((long)h * lq + i) * lk + j] <= 0.5f * MASK_MIN))
+      s += MASK_MIN;                                   // one finfo.min per masked pair (see attention_mfma.hip)
     S[i * sst + j] = s;
   }
   __syncthreads();
@@ -208,6 +209,12 @@ int vqa_attn_bwd_mfma(const vqa_attn_desc* d, hipStream_t s);
 
 bool vqa_attn_long_ok(const vqa_attn_desc* d);
 int vqa_attn_fwd_long(const vqa_attn_desc* d, hipStream_t s);
+
+extern "C" int vqa_attn_path(const vqa_attn_desc* d, int backward) {
+  if (!d) return -1;
+  if (!backward && (d->lq > 32 || d->lk > 64) && vqa_attn_long_ok(d)) return VQA_ATTN_LONG;
+  return vqa_attn_mfma_ok(d) ? VQA_ATTN_MFMA : VQA_ATTN_VALU;
+}
 
 extern "C" int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t s) {
   VQA_REQUIRE(d && d->q && d->k && d->v, "attention: null q/k/v");

@@ -204,12 +204,17 @@ __global__ __launch_bounds__(64 * wpb_for(NT)) void attn_fwd_mfma(AttnM P) {
     for (int t = 0; t < NT; ++t) load_xrow(brow, lk, t, vec, add[t]);
   }
   if (NT <= 2 && P.mask) {                              // lk <= 64 (host check for the mask)
+    // one finfo.min per masked pair, as HF's combined extended mask has it: a pair the bias
+    // already masks (the causal decoder's bucket < 0) does not take a second one (which
+    // would give -inf and, for a fully masked query, a one-hot instead of a uniform row)
     const unsigned long long kb = key_bits(P.mask + (long)b * lk, lk);
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        add[t][r] += ((kb >> ((32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5) & 63)) & 1ull) ? 0.f : MASK_MIN;
+      for (int r = 0; r < 16; ++r) {
+        const bool keep = (kb >> ((32 * t + (r & 3) + 8 * (r >> 2) + 4 * h5) & 63)) & 1ull;
+        add[t][r] = (keep || add[t][r] <= 0.5f * MASK_MIN) ? add[t][r] : add[t][r] + MASK_MIN;
+      }
   }
 
   // S^T tiles (X layout: lane = query, registers = keys)

@@ -209,6 +209,13 @@ int launch_patch(GemmParams& P, const PatchGeom& G, hipStream_t s) {
 
 }  // namespace
 
+// does the (R + 2) x (W + 2) input patch of a bm-row tile fit the kernel's LDS patch buffer?
+static bool patch_fits(const vqa_conv_geom& g, int bm) {
+  const int R = bm / g.w < g.h ? bm / g.w : g.h;
+  if (R < 1) return false;
+  return (R + 2) * (g.w + 2) <= (g.c == 64 ? PMAX_SB : PMAX_DB);
+}
+
 // called by vqa_gemm for a_conv == 2 (gemm.hip has validated the descriptor and filled P)
 static int conv_patch_dispatch(GemmParams& P, int config, hipStream_t s) {
   const vqa_conv_geom& g = P.ga;
@@ -216,11 +223,15 @@ static int conv_patch_dispatch(GemmParams& P, int config, hipStream_t s) {
               "vqa_gemm(a_conv=2): a 3x3 / stride-1 / pad-1 convolution is required");
   VQA_REQUIRE(g.c % 64 == 0 && P.k == 9 * g.c && P.m == g.n * g.h * g.w, "vqa_gemm(a_conv=2): C %% 64, K = 9C, M = NHW");
   VQA_REQUIRE(P.splitk <= 1 && P.alpha == 1.f, "vqa_gemm(a_conv=2): no split-K, alpha = 1");
-  const int bm = (config == 19 || config == 20) ? 64 : 128;
+  int bm = (config == 19 || config == 20) ? 64 : 128;
   const int bn = (config == 18 || config == 20) ? 128 : 64;
+  // a 128-row tile whose input patch exceeds the LDS buffer (e.g. C >= 128 at W 40-42 or 51-64,
+  // where R = 128 / W leaves (R + 2)(W + 2) > PMAX_DB) runs as the 64-row tile: the tile
+  // configs give the same bits, so this changes speed only
+  if (bm == 128 && !patch_fits(g, 128)) bm = 64;
+  VQA_REQUIRE(patch_fits(g, bm), "vqa_gemm(a_conv=2): no patch tile fits W = %d, C = %d", g.w, g.c);
   PatchGeom G;
   G.R = bm / g.w < g.h ? bm / g.w : g.h;
-  VQA_REQUIRE(G.R >= 1, "vqa_gemm(a_conv=2): image width %d > tile rows %d", g.w, bm);
   G.rbs = vqa::cdiv(g.h, G.R);
   G.npix = (G.R + 2) * (g.w + 2);
   G.pins = vqa::cdiv(G.npix, 8);

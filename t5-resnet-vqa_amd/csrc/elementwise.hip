@@ -371,6 +371,10 @@ __global__ __launch_bounds__(256) void zero_kernel(uint4* __restrict__ p, long n
     p[i] = make_uint4(0, 0, 0, 0);
 }
 
+__global__ __launch_bounds__(256) void copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, long n16) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) dst[i] = src[i];
+}
+
 }  // namespace
 
 extern "C" int vqa_image_to_s2d16(const float* img, void* out, int n, int h, int w, hipStream_t s) {
@@ -515,4 +519,16 @@ extern "C" int vqa_zero(void* p, long long bytes, hipStream_t s) {
   const int grid = (int)((n16 + 255) / 256 < 8192 ? (n16 + 255) / 256 : 8192);
   hipLaunchKernelGGL(zero_kernel, dim3(grid), dim3(256), 0, s, (uint4*)p, n16);
   return vqa::check_launch("vqa_zero");
+}
+
+// A kernel, not hipMemcpyAsync: inside a captured step a device-to-device copy would be the
+// graph's only non-kernel node (a runtime blit node); the step graphs stay kernel-only.
+extern "C" int vqa_copy(void* dst, const void* src, long long bytes, hipStream_t s) {
+  VQA_REQUIRE(dst && src && bytes >= 0 && ((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0 && bytes % 16 == 0,
+              "vqa_copy: pointers and size must be 16-byte aligned");
+  if (bytes == 0) return VQA_OK;
+  const long n16 = (long)(bytes / 16);
+  const int grid = (int)((n16 + 255) / 256 < 8192 ? (n16 + 255) / 256 : 8192);
+  hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, s, (uint4*)dst, (const uint4*)src, n16);
+  return vqa::check_launch("vqa_copy");
 }

@@ -114,15 +114,36 @@ class DaquarCollate:
     path on the GPU.  A data point is a dict with `image` (uint8 RGB array) or `image_path`,
     `question_ids` (token ids, ending in EOS), and `annotation_id` (answer index)."""
 
-    def __init__(self, resizing_dimensions=(256, 256), max_question_length=16, device="cuda", eval_mode=False):
+    # cv2 flags the reference collate accepts as `interpolation_strategy` (:156-164); only
+    # INTER_LINEAR (the default, cv2 constant 1) has a GPU kernel here
+    INTERPOLATIONS = {"linear": 1, "INTER_LINEAR": 1, 1: 1}
+
+    def __init__(self, resizing_dimensions=(256, 256), max_question_length=16, device="cuda", eval_mode=False,
+                 interpolation_strategy="linear", decode_workers=0):
+        if interpolation_strategy not in self.INTERPOLATIONS:
+            raise NotImplementedError(f"interpolation_strategy {interpolation_strategy!r}: only cv2.INTER_LINEAR is "
+                                      "implemented on the GPU (vqa_resize_linear_u8); LANCZOS4 / CUBIC would train "
+                                      "on different pixels")
         w, h = resizing_dimensions                      # the reference unpacks (width, height) (:132)
         self.batcher = ImageBatcher(h, w, device)
         self.max_len = int(max_question_length)
         self.eval_mode = eval_mode
         self.dev = torch.device(device)
+        # host JPEG decode is serial per image; decode_workers > 0 decodes a batch on a thread
+        # pool (PIL releases the GIL while it decodes)
+        self._pool = None
+        if decode_workers and decode_workers > 0:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=int(decode_workers))
+
+    def _decode(self, data_points):
+        get = lambda dp: dp["image"] if "image" in dp else decode_image(dp["image_path"])
+        if self._pool is None:
+            return [get(dp) for dp in data_points]
+        return list(self._pool.map(get, data_points))
 
     def __call__(self, data_points, out=None):
-        images = [dp["image"] if "image" in dp else decode_image(dp["image_path"]) for dp in data_points]
+        images = self._decode(data_points)
         ids, mask = pad_question_ids([dp["question_ids"] for dp in data_points], self.max_len)
         B = len(data_points)
         dec = np.zeros((B, 20), np.int64)                 # decoder_* / answer_* (ignored by the model)

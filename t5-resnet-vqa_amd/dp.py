@@ -103,7 +103,7 @@ class DataParallelStep:
         self.buckets = plan_buckets(e.ready_marks, emb.offset, bucket_mb << 20)
         calls = e.bwd_calls[:-1]                            # all but the local embedding scatter
         assert e.bwd_calls[-1] is e.emb_call
-        T, D = e.T, S.D_MODEL
+        T, D = e.T, e.D
         dev = e.dev
         self.GIDS = torch.zeros(self.world * T, dtype=torch.int64, device=dev)
         # the rows to re-zero are the previous step's GATHERED ids (every rank's rows were written);
@@ -178,7 +178,7 @@ class DataParallelStep:
         if not e.pipeline:
             return
         main = torch.cuda.current_stream(e.dev)
-        e.F4.copy_(e.F4N)
+        e.copy_f4(L.stream_handle(main))
         ev = torch.cuda.Event()
         ev.record(main)
         e._rstream.wait_event(ev)

@@ -42,7 +42,6 @@ from . import synthetic as S
 from .layout import ParamLayout, fold_bn, t5_bucket_map
 
 BF16, F32, I64 = torch.bfloat16, torch.float32, torch.int64
-D = S.D_MODEL
 
 # dropout site ids (the hash key of each nn.Dropout application of the step)
 SITE_EMBED, SITE_FINAL = 1, 2                  # T5Stack: dropout(inputs_embeds) :725, dropout(final_ln) :745
@@ -88,17 +87,6 @@ def _gemm_key(d):
             d.beta != 0.0, d.drop.p > 0.0) + (("rownorm",) if d.rownorm else ())
 
 
-class _Seq:
-    """Several prepared calls issued as one (a deferred AdamW range and the folded
-    weights that follow it)."""
-    def __init__(self, calls):
-        self.calls = calls
-
-    def __call__(self, stream):
-        for c in self.calls:
-            c(stream)
-
-
 @contextlib.contextmanager
 def no_gc_capture():
     """Stream capture with the cyclic garbage collector held off.  Engines (and the graphs /
@@ -116,6 +104,24 @@ def no_gc_capture():
             gc.enable()
 
 
+_WARNED_ATTN = set()
+
+
+def _check_attn_path(d, fn):
+    """Say it loudly (once per shape) when a planned attention call would run the scalar VALU
+    kernel (include/vqa_hip.h vqa_attn_path): it is correct but an order of magnitude slower
+    than the MFMA kernels, which cover lq <= 32, lk <= 160 (key mask: lk <= 64)."""
+    path = L.load().vqa_attn_path(ctypes.byref(d), int(fn == "vqa_attn_bwd"))
+    if path == L.ATTN_VALU:
+        key = (fn, d.lq, d.lk, d.dh, bool(d.key_mask))
+        if key not in _WARNED_ATTN:
+            _WARNED_ATTN.add(key)
+            import warnings
+            warnings.warn(f"{fn}: lq={d.lq} lk={d.lk} dh={d.dh} key_mask={bool(d.key_mask)} runs the scalar VALU "
+                          "attention kernel (no MFMA kernel covers this shape)", RuntimeWarning, stacklevel=3)
+    return path
+
+
 def _h2d(dst, src):
     """dst <- src (numpy / torch, host or device).  Asynchronous only from device or pinned
     memory: an async copy out of a pageable temporary (freed when this returns) may be read
@@ -128,7 +134,8 @@ class VQAEngine:
     def __init__(self, state_dict, vision="resnet50", batch=64, seq_len=32, image_size=224, device="cuda:0",
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0, pipeline=False,
-                 t5_dw_group=None):
+                 t5_dw_group=None, defer_optimizer=True, dw_stream=None, sga_dw_batch=True, pair_bwd=True,
+                 language_model="t5-base"):
         L.load()
         # pipeline: the frozen ResNet (no trainable input) of the NEXT batch runs on its own
         # stream beside this step's T5 / SGA / backward / optimizer (see train_step)
@@ -138,6 +145,12 @@ class VQAEngine:
         self.vision, self.B, self.L, self.H = vision, batch, seq_len, image_size
         assert image_size % 2 == 0, "the space-to-depth stem needs an even image size"
         self.NB, self.A = num_blocks, answer_spaces
+        # widths: t5-base (the reference) or t5-large (BASELINE configs[4]: the SGA blocks, scaler,
+        # pooler and classifier at the language model's width, synthetic.LM_DIMS)
+        self.dims = dm = S.lm_dims(language_model)
+        self.D, self.nl, self.h5, self.dkv, self.dff = dm.d_model, dm.t5_layers, dm.t5_heads, dm.t5_dkv, dm.t5_dff
+        self.sga_heads, self.sga_dh = dm.sga_heads, dm.sga_dhead
+        assert self.h5 * self.dkv == self.D and self.sga_heads * self.sga_dh == self.D
         # the answer head's log-softmax keeps one sample's answer logits in registers (head.hip:
         # A <= 1024; DAQUAR has 170) and the pooler one sample's tokens (L <= 64)
         if not 1 <= answer_spaces <= 1024:
@@ -148,53 +161,36 @@ class VQAEngine:
         self.betas, self.eps, self.wd = betas, eps, weight_decay
         self.grad_scale = grad_scale
         self.group_lr = {}                # per-group LR overrides (trainer optimizer_kwargs)
-        # dX + dW of a layer as one paired GEMM launch (VQA_PAIR_BWD=0: separate launches, A/B only)
-        self.pair_bwd = os.environ.get("VQA_PAIR_BWD", "1") != "0"
+        # dX + dW of a layer as one paired GEMM launch (pair_bwd=False: separate launches)
+        self.pair_bwd = bool(pair_bwd)
         # T5 weight gradients: per weight ONE launch batched over a group of layers (the
         # layers' activations / gradients stacked at constant strides).  `t5_dw_group` is a
         # group size (1: dX + dW paired per layer; 12: one group) or a sequence of group sizes,
-        # top layer first.  Default (single GPU): groups of 9 and 3 layers, the batched weight
+        # top layer first.  Default (single GPU): groups of 9 and 3 layers (3/4 and 1/4 of the
+        # stack: 18 and 6 for t5-large), the batched weight
         # gradients on a side stream beside the remaining input-gradient chain (measured 6.66 vs
         # 6.78-6.84 ms per step against one group of 12 on the chain; tools/gpu/ab_env.sh).
         # DP passes (4, 4, 3, 1): the buckets become final, and are all-reduced, while the
         # backward runs, and the last, exposed bucket is one layer.
-        # VQA_T5_DW_GROUP / VQA_T5_DW_GROUPS override (A/B).
         self._default_dw = t5_dw_group is None
         if t5_dw_group is None:
-            t5_dw_group = (9, 3)
-        env_g, env_gs = os.environ.get("VQA_T5_DW_GROUP"), os.environ.get("VQA_T5_DW_GROUPS")
-        if env_gs:
-            t5_dw_group = tuple(int(x) for x in env_gs.split(","))
-        elif env_g:
-            t5_dw_group = int(env_g)
+            t5_dw_group = (3 * self.nl // 4, self.nl - 3 * self.nl // 4)
         if isinstance(t5_dw_group, (list, tuple)):
             self.t5_dw_groups = [int(x) for x in t5_dw_group]
-            self.t5_dw_group = S.T5_LAYERS
-            assert sum(self.t5_dw_groups) == S.T5_LAYERS and min(self.t5_dw_groups) >= 1
+            self.t5_dw_group = self.nl
+            assert sum(self.t5_dw_groups) == self.nl and min(self.t5_dw_groups) >= 1
         else:
             self.t5_dw_groups = None
             self.t5_dw_group = int(t5_dw_group)
         # SGA blocks' q2 / m2 / fc1 / fc2 weight gradients batched over the blocks
-        self.sga_dw_batch = os.environ.get("VQA_SGA_DW_BATCH", "1") != "0"
+        self.sga_dw_batch = bool(sga_dw_batch)
         # AdamW of step k applied inside step k+1's forward (see _plan_optimizer)
-        self.defer_opt = os.environ.get("VQA_DEFER_OPT", "1") != "0"
-        # the embedding + rel-bias range deferred too (else applied at the end of the step)
-        self.defer_embed = os.environ.get("VQA_DEFER_EMBED", "0") == "1"
-        # stream steps: the grad-norm pass over [0, rel-bias) beside the embedding scatter
-        self.sq_overlap = os.environ.get("VQA_SQ_OVERLAP", "1") != "0"
-        # ... and its [0, a) part as soon as the first T5 weight-gradient group is final
-        self._sq_early = os.environ.get("VQA_SQ_EARLY", "1") != "0"
-        # bias / norm-affine column sums tagged for the weight-gradient stream (with dw_stream).
-        # Off: the extra cross-stream edges cost more than the chain waits (same box: 6.92-7.00
-        # vs 6.73-6.77 ms per step)
-        self.colsum_side = os.environ.get("VQA_COLSUM_SIDE", "0") == "1"
-        # T5 RMSNorms folded into the next projection (vqa_gemm_desc.rownorm): the chain runs the
-        # q|k|v (layers >= 1) and wi GEMMs on the unnormalised rows; the normalised rows the
-        # weight gradients need are made by one batched launch beside the SGA forward.  Off by
-        # default: 23 fewer launches on the chain measured no faster
-        self.norm_fold = os.environ.get("VQA_NORM_FOLD", "0") == "1"
+        self.defer_opt = bool(defer_optimizer)
+        # weight-gradient GEMMs (calls tagged `side`) on a stream of their own beside the
+        # input-gradient chain: on by default for the single-GPU grouping, off for DP groups
+        self.dw_stream = self._default_dw if dw_stream is None else bool(dw_stream)
         self.T = batch * seq_len
-        self.lay = ParamLayout(vision, answer_spaces, num_blocks)
+        self.lay = ParamLayout(vision, answer_spaces, num_blocks, dm)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
         self._frozen = {k: v for k, v in sd.items() if k not in set(self.lay.trainable_keys)}
         with torch.cuda.device(self.dev):
@@ -205,15 +201,11 @@ class VQAEngine:
             self._plan_forward()
             self._plan_backward()
             self._plan_optimizer()
-            self._run(self.fold_all)                     # folded weights of the initial parameters
         self.graph = None
         self.allreduce = None            # set by the DP trainer: fn(G32 tensor) on the current stream
         self._side = torch.cuda.Stream(self.dev)
         self._wside = torch.cuda.Stream(self.dev)
         self._rstream = torch.cuda.Stream(self.dev)
-        self._ostream = torch.cuda.Stream(self.dev)      # deferred AdamW ranges (run_forward_streams)
-        self._nstream = torch.cuda.Stream(self.dev)      # the batched off-chain RMSNorms (norm_fold)
-        self.dw_stream = os.environ.get("VQA_DW_STREAM", "1" if self._default_dw else "0") == "1"
         self._scratch = None             # split-K workspace used while autotuning
 
     @classmethod
@@ -292,6 +284,9 @@ class VQAEngine:
         # pipelined: the ResNet writes the next batch's layer4 map here; each step first
         # moves it into F4 (read by the ConvTranspose2d forward and weight gradient)
         self.F4N = self._t((B, hh, hh, cin), BF16) if self.pipeline else self.F4
+        # F4 <- F4N as a library kernel (a torch copy_ would put a runtime memcpy node in the graph)
+        self.copy_f4 = ops.Call("vqa_copy", self.F4.data_ptr(), self.F4N.data_ptr(), self.F4.numel() * 2,
+                                keep=(self.F4, self.F4N))
 
         # stem: conv7x7/2 + BN + ReLU, then maxpool 3x3/2
         # (as a 4x4 stride-1 conv over the space-to-depth image: K 256 instead of 7*7*8 = 392)
@@ -342,9 +337,8 @@ class VQAEngine:
         if kh == 1 and kw == 1 and stride == 1 and pad == 0:
             g = None                                   # a 1x1/1 conv is a plain GEMM over the NHWC rows
         # 3x3 / stride 1: the LDS-patch convolution (a_conv = 2), weights reordered to
-        # [Cout][C/64][9][64] (VQA_CONV_PATCH=0: the implicit-im2col path, A/B)
-        patch = (kh == 3 and kw == 3 and stride == 1 and pad == 1 and c % 64 == 0 and 14 <= w <= 64
-                 and os.environ.get("VQA_CONV_PATCH", "1") != "0")
+        # [Cout][C/64][9][64]; any W <= 64 has a patch tile that fits (conv_patch.inl patch_fits)
+        patch = kh == 3 and kw == 3 and stride == 1 and pad == 1 and c % 64 == 0 and 14 <= w <= 64
         if patch:
             w16 = w16.reshape(cout, 9, c // 64, 64).permute(0, 2, 1, 3).contiguous().reshape(cout, kh, kw, c)
             self._res_keep.append(w16)
@@ -352,6 +346,7 @@ class VQAEngine:
                    c16=out, ldc16=cout, bias=b32, relu=relu, res16=res16, ldres=cout, a_patch=patch)
 
     def _alloc_activations(self):
+        D = self.D
         B, Lq, T, NB, V = self.B, self.L, self.T, self.NB, self.V_TOK
         t = self._t
         # inputs
@@ -362,29 +357,22 @@ class VQAEngine:
         # vision tokens
         self.VIS32, self.VIS16 = t((V, D)), t((V, D), BF16)
         # T5
-        nl = S.T5_LAYERS
-        self.PB = t((S.T5_HEADS, Lq, Lq))
+        nl = self.nl
+        self.PB = t((self.h5, Lq, Lq))
         self.HS = [t((T, D)) for _ in range(nl + 1)]
         # GEMM inputs the weight gradients read, stacked in backward order (slot = 11 - layer) so
         # a group of consecutive layers' dW is one batched launch with constant strides
         self.N0S, self.OS, self.N1S = t((nl, T, D), BF16), t((nl, T, D), BF16), t((nl, T, D), BF16)
-        self.FFS = t((nl, T, S.T5_DFF), BF16)
+        self.FFS = t((nl, T, self.dff), BF16)
         self.N0 = [self.N0S[nl - 1 - i] for i in range(nl)]
         self.QKV = [t((T, 3 * D), BF16) for _ in range(nl)]
-        self.PT = [t((B, S.T5_HEADS, Lq, Lq)) for _ in range(nl)]
+        self.PT = [t((B, self.h5, Lq, Lq)) for _ in range(nl)]
         self.O = [self.OS[nl - 1 - i] for i in range(nl)]
         self.HM = [t((T, D)) for _ in range(nl)]
         self.N1 = [self.N1S[nl - 1 - i] for i in range(nl)]
         self.FF = [self.FFS[nl - 1 - i] for i in range(nl)]
         self.R0 = [t(T) for _ in range(nl)]
         self.R1 = [t(T) for _ in range(nl)]
-        if self.norm_fold:
-            # bf16 copies of the residual stream (written by the o / wo epilogues beside the fp32
-            # rows) and the projection weights with the RMSNorm weight folded into their columns
-            self.HS16 = [None] + [t((T, D), BF16) for _ in range(1, nl)]
-            self.HM16 = [t((T, D), BF16) for _ in range(nl)]
-            self.WQF = [None] + [t((3 * D, D), BF16) for _ in range(1, nl)]
-            self.WIF = [t((S.T5_DFF, D), BF16) for _ in range(nl)]
         self.RF = t(T)
         self.TXT32, self.TXT16 = t((T, D)), t((T, D), BF16)
         # SGA blocks; the self-attention halves of all blocks share batched buffers:
@@ -401,9 +389,9 @@ class VQAEngine:
             lk = self.fh * self.fh if n == 0 else Lq
             self.sga.append(dict(
                 ly=ly, lk=lk,
-                P1=t((B, S.SGA_HEADS, Lq, Lq)), O1=self.O1A[n], S1=self.S1A[n],
+                P1=t((B, self.sga_heads, Lq, Lq)), O1=self.O1A[n], S1=self.S1A[n],
                 X1=t((T, D)), X1h=self.X1hS[NB - 1 - n], MU1=t(T), RS1=t(T),
-                Q2=self.Q2S[NB - 1 - n], KV2=t((ly, 2 * D), BF16), P2=t((B, S.SGA_HEADS, Lq, lk)),
+                Q2=self.Q2S[NB - 1 - n], KV2=t((ly, 2 * D), BF16), P2=t((B, self.sga_heads, Lq, lk)),
                 O2=self.O2S[NB - 1 - n], S2=t((T, D)), X2=t((T, D)), X2h=self.X2hS[NB - 1 - n], MU2=t(T), RS2=t(T),
                 FFh=self.FFhS[NB - 1 - n], S3=t((T, D)), OUT=t((T, D)), OUTh=t((T, D), BF16), MU3=t(T), RS3=t(T)))
         # head
@@ -423,8 +411,8 @@ class VQAEngine:
         self.dVIS32, self.dVIS16 = t((V, D)), t((V, D), BF16)
         self.dH32 = t((T, D))
         self.dHM32 = t((T, D))
-        self.dPB = t((S.T5_HEADS, Lq, Lq), zero=True)
-        self.dSB = t((S.T5_LAYERS, B, S.T5_HEADS, Lq, Lq))   # per-layer, per-sample attention dS (rel-bias grad)
+        self.dPB = t((self.h5, Lq, Lq), zero=True)
+        self.dSB = t((self.nl, B, self.h5, Lq, Lq))   # per-layer, per-sample attention dS (rel-bias grad)
         self.WS_EMB = t(3 * T, torch.int32)
         lib = L.load()
         self.WS_COL2 = t(lib.vqa_colsum_workspace_floats(V, D))
@@ -470,6 +458,7 @@ class VQAEngine:
         if dd is not None:
             d.drop = dd
             ts = ts + (self.RNG,)
+        _check_attn_path(d, fn)
         lst.append(ops.Call(fn, ctypes.byref(d), keep=ts, desc=d))
 
     def _drop(self, site):
@@ -541,13 +530,11 @@ class VQAEngine:
             keep += list(k)
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.dev)
         lst.append(ops.Call("vqa_colsum_batched", raw.data_ptr(), len(self._jobs), blk, keep=tuple(keep) + (raw,)))
-        # nothing on the input-gradient chain reads a finished bias / norm-affine gradient, so
-        # (VQA_COLSUM_SIDE=1) the reduction may trail the chain on the weight-gradient stream
-        lst[-1].side = getattr(self, "colsum_side", False)
         self._jobs = []
 
     def _norm_ws(self):
         """A private partial-row workspace for one deferred norm backward."""
+        D = self.D
         return self._t(L.load().vqa_norm_bwd_workspace_floats(self.T, D))
 
     def _gbuf(self, name, shape):
@@ -562,7 +549,6 @@ class VQAEngine:
         n = dy16.shape[-1]
         ws = self._t(lib.vqa_colsum_workspace_floats(rows, n))
         self._call(lst, "vqa_colsum", dy16, 1, rows, n, n, None, 0.0, ws)
-        lst[-1].side = getattr(self, "colsum_side", False)
         self._defer(ws, lib.vqa_colsum_parts(rows), n, n, self.g32[bname])
 
     def _dw(self, lst, dy16, x16, wname, rows, bias_from=None, bias_bf16=True):
@@ -577,11 +563,11 @@ class VQAEngine:
             lib = L.load()
             ws = self._t(lib.vqa_colsum_workspace_floats(rows, n))
             self._call(lst, "vqa_colsum", bias_from, int(bias_bf16), rows, n, n, None, 0.0, ws)
-            lst[-1].side = getattr(self, "colsum_side", False)
             self._defer(ws, lib.vqa_colsum_parts(rows), n, n, self.g32[wname[:-1] + "b"])
 
     # ------------------------------------------------------------------ forward plan
     def _plan_forward(self):
+        D = self.D
         f = self.fwd_calls
         B, Lq, T = self.B, self.L, self.T
         if self.p_drop > 0.0:                                # fresh dropout masks every step
@@ -604,45 +590,34 @@ class VQAEngine:
         kp = []
         self._call(f, "vqa_embedding_fwd", self.IDS, self.p32["t5.embed"], self.HS[0], T, D, S.T5_VOCAB,
                    self._dptr(SITE_EMBED, kp), extra=kp + [self.RNG])
-        self._call(f, "vqa_t5_relbias_fwd", self.p32["t5.relbias"], self.bucket, self.PB, S.T5_HEADS, Lq, Lq)
+        self._call(f, "vqa_t5_relbias_fwd", self.p32["t5.relbias"], self.bucket, self.PB, self.h5, Lq, Lq)
         self._t5_layer_start = []
-        fold = self.norm_fold
-        for i in range(S.T5_LAYERS):
+        for i in range(self.nl):
             self._t5_layer_start.append(len(f))
-            if fold and i > 0:        # rms(h) W^T = rstd(h) * (h16 (W o w)^T): the norm rides on the GEMM
-                self._gemm(f, self.HS16[i], self.WQF[i], T, 3 * D, D, lda=D, ldb=D, c16=self.QKV[i], ldc16=3 * D,
-                           rownorm_eps=1e-6)
-            else:
-                self._call(f, "vqa_rmsnorm_fwd", self.HS[i], self.p32[f"t5.{i}.ln0"], None, self.N0[i], self.R0[i], T,
-                           D, 1e-6, None)
-                self._linear(f, self.N0[i], f"t5.{i}.qkv_w", T, out16=self.QKV[i], bias=False)
+            self._call(f, "vqa_rmsnorm_fwd", self.HS[i], self.p32[f"t5.{i}.ln0"], None, self.N0[i], self.R0[i], T,
+                       D, 1e-6, None)
+            self._linear(f, self.N0[i], f"t5.{i}.qkv_w", T, out16=self.QKV[i], bias=False)
             q = self.QKV[i]
             self._attn(f, "vqa_attn_fwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, o=self.O[i], ldo=D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B,
-                       heads=S.T5_HEADS, lq=Lq, lk=Lq, dh=S.T5_DKV, scale=1.0, drop=t5_site(i, 0))
+                       heads=self.h5, lq=Lq, lk=Lq, dh=self.dkv, scale=1.0, drop=t5_site(i, 0))
             # h + dropout(attention output)   (T5LayerSelfAttention :400)
-            self._linear(f, self.O[i], f"t5.{i}.o_w", T, out32=self.HM[i], out16=self.HM16[i] if fold else None,
-                         bias=False, res32=self.HS[i], drop=t5_site(i, 1))
+            self._linear(f, self.O[i], f"t5.{i}.o_w", T, out32=self.HM[i], bias=False, res32=self.HS[i],
+                         drop=t5_site(i, 1))
             # dropout(relu(wi h)) (T5DenseActDense :86), then h + dropout(wo .) (T5LayerFF :140)
-            if fold:
-                self._gemm(f, self.HM16[i], self.WIF[i], T, S.T5_DFF, D, lda=D, ldb=D, c16=self.FF[i],
-                           ldc16=S.T5_DFF, relu=True, rownorm_eps=1e-6)
-                self._set_drop(f[-1], t5_site(i, 2))
-            else:
-                self._call(f, "vqa_rmsnorm_fwd", self.HM[i], self.p32[f"t5.{i}.ln1"], None, self.N1[i], self.R1[i], T,
-                           D, 1e-6, None)
-                self._linear(f, self.N1[i], f"t5.{i}.wi", T, out16=self.FF[i], bias=False, relu=True,
-                             drop=t5_site(i, 2))
-            self._linear(f, self.FF[i], f"t5.{i}.wo", T, out32=self.HS[i + 1],
-                         out16=self.HS16[i + 1] if fold and i + 1 < S.T5_LAYERS else None, bias=False,
-                         res32=self.HM[i], drop=t5_site(i, 3))
+            self._call(f, "vqa_rmsnorm_fwd", self.HM[i], self.p32[f"t5.{i}.ln1"], None, self.N1[i], self.R1[i], T,
+                       D, 1e-6, None)
+            self._linear(f, self.N1[i], f"t5.{i}.wi", T, out16=self.FF[i], bias=False, relu=True,
+                         drop=t5_site(i, 2))
+            self._linear(f, self.FF[i], f"t5.{i}.wo", T, out32=self.HS[i + 1], bias=False, res32=self.HM[i],
+                         drop=t5_site(i, 3))
         kp = []
         self._call(f, "vqa_rmsnorm_fwd", self.HS[-1], self.p32["t5.final_ln"], self.TXT32, self.TXT16, self.RF, T, D,
                    1e-6, self._dptr(SITE_FINAL, kp), extra=kp + [self.RNG])
         self._fsplit.append(len(f))
         # SGA blocks: x = text always, y chained
         y16 = self.VIS16
-        sc = 1.0 / math.sqrt(S.SGA_DHEAD)
+        sc = 1.0 / math.sqrt(self.sga_dh)
         # self-attention halves of all blocks first (they only read the T5 output): one q|k|v
         # projection with N = 3 * 2304, the blocks' attentions, one batched merge
         NB, W3 = self.NB, 3 * D
@@ -653,7 +628,7 @@ class VQAEngine:
             q = self.QKV1A
             self._attn(f, "vqa_attn_fwd", q=ops.addr(q, c0), ldq=NB * W3, k=ops.addr(q, c0 + D), ldk=NB * W3,
                        v=ops.addr(q, c0 + 2 * D), ldv=NB * W3, o=s["O1"], ldo=D, p=s["P1"], batch=B,
-                       heads=S.SGA_HEADS, lq=Lq, lk=Lq, dh=S.SGA_DHEAD, scale=sc, drop=sga_site(n, 0),
+                       heads=self.sga_heads, lq=Lq, lk=Lq, dh=self.sga_dh, scale=sc, drop=sga_site(n, 0),
                        keep=(q,))
         self._gemm(f, self.O1A, self.p16["sga0.m1_w"], T, D, D, lda=D, ldb=D, c32=self.S1A, ldc32=D,
                    bias=self.p32["sga0.m1_b"], res32=self.TXT32, ldres=D, batch=NB, stride_a=T * D,
@@ -680,7 +655,7 @@ class VQAEngine:
                 self._linear(f, y16, p + "kv2_w", s["ly"], out16=s["KV2"])
             kv = s["KV2"]
             self._attn(f, "vqa_attn_fwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
-                       o=s["O2"], ldo=D, p=s["P2"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=s["lk"], dh=S.SGA_DHEAD,
+                       o=s["O2"], ldo=D, p=s["P2"], batch=B, heads=self.sga_heads, lq=Lq, lk=s["lk"], dh=self.sga_dh,
                        scale=sc, drop=sga_site(n, 2))
             self._linear(f, s["O2"], p + "m2_w", T, out32=s["S2"], res32=s["X1"], drop=sga_site(n, 3))
             self._call(f, "vqa_layernorm_fwd", s["S2"], self.p32[p + "ln2_g"], self.p32[p + "ln2_b"], s["X2"],
@@ -693,20 +668,10 @@ class VQAEngine:
         last = self.sga[-1]["OUT"]
         self._call(f, "vqa_head_fwd", last, self.p32["pool_w"], self.p32["pool_b"], self.p32["cls_w"],
                    self.p32["cls_b"], self.TGT, self.ATT, self.POOLED, self.LOGP, self.NLL, self.LOSS, B, Lq, D, self.A)
-        # norm_fold: the normalised rows (and rstd) the weight gradients and the norm backward
-        # read, all 23 in one launch; graph steps run it beside the SGA blocks (run_forward_streams)
-        self._fnorm = None
-        if fold:
-            jobs = [(self.HS[i], self.p32[f"t5.{i}.ln0"], self.N0[i], self.R0[i]) for i in range(1, S.T5_LAYERS)]
-            jobs += [(self.HM[i], self.p32[f"t5.{i}.ln1"], self.N1[i], self.R1[i]) for i in range(S.T5_LAYERS)]
-            arr = (L.RmsNormJob * len(jobs))(*[L.RmsNormJob(*[ops.addr(x) for x in j]) for j in jobs])
-            raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.dev)
-            self._fnorm = len(f)
-            f.append(ops.Call("vqa_rmsnorm_fwd_batched", raw.data_ptr(), len(jobs), T, D, 1e-6,
-                              keep=(raw,) + tuple(x for j in jobs for x in j)))
 
     # ------------------------------------------------------------------ backward plan
     def _plan_backward(self):
+        D = self.D
         b = self.bwd_calls
         B, Lq, T, NB = self.B, self.L, self.T, self.NB
         nparts = L.load().vqa_norm_bwd_parts(T)
@@ -734,7 +699,7 @@ class VQAEngine:
             sg = self.lay[seg]
             self.ready_marks.append((len(b), sg.offset + (sg.numel + 63) // 64 * 64))
         mark("pool_b")
-        sc = 1.0 / math.sqrt(S.SGA_DHEAD)
+        sc = 1.0 / math.sqrt(self.sga_dh)
         ks = self.drop_scale if self.p_drop > 0.0 else 1.0      # relu-mask dX: kept elements carry 1/(1-p)
         # the blocks' q2 / m2 / fc1 / fc2 weight gradients (768 x 768, K = 2048 each) are left
         # out of the sequential block chain and computed after it as one launch per weight
@@ -778,7 +743,7 @@ class VQAEngine:
             dxdw(b, dA2, s["O2"], p + "m2_w", T, out16=self.dO16)
             kv = s["KV2"]
             self._attn(b, "vqa_attn_bwd", q=s["Q2"], ldq=D, k=kv, ldk=2 * D, v=ops.addr(kv, D), ldv=2 * D,
-                       p=s["P2"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=s["lk"], dh=S.SGA_DHEAD, scale=sc,
+                       p=s["P2"], batch=B, heads=self.sga_heads, lq=Lq, lk=s["lk"], dh=self.sga_dh, scale=sc,
                        dout=self.dO16, lddo=D, dq=dQ, lddq=D, dk=dKV, lddk=2 * D,
                        dv=ops.addr(dKV, D), lddv=2 * D, drop=sga_site(n, 2))
             if batched:
@@ -827,8 +792,8 @@ class VQAEngine:
             s, c0 = self.sga[n], n * W3
             q = self.QKV1A
             self._attn(b, "vqa_attn_bwd", q=ops.addr(q, c0), ldq=NB * W3, k=ops.addr(q, c0 + D), ldk=NB * W3,
-                       v=ops.addr(q, c0 + 2 * D), ldv=NB * W3, p=s["P1"], batch=B, heads=S.SGA_HEADS, lq=Lq, lk=Lq,
-                       dh=S.SGA_DHEAD, scale=sc, dout=self.dO1A[n], lddo=D, dq=ops.addr(dq, c0), lddq=NB * W3,
+                       v=ops.addr(q, c0 + 2 * D), ldv=NB * W3, p=s["P1"], batch=B, heads=self.sga_heads, lq=Lq, lk=Lq,
+                       dh=self.sga_dh, scale=sc, dout=self.dO1A[n], lddo=D, dq=ops.addr(dq, c0), lddq=NB * W3,
                        dk=ops.addr(dq, c0 + D), lddk=NB * W3, dv=ops.addr(dq, c0 + 2 * D), lddv=NB * W3,
                        drop=sga_site(n, 0), keep=(q, dq))
         tmp = []
@@ -841,7 +806,6 @@ class VQAEngine:
         lib = L.load()
         ws = self._t(lib.vqa_colsum_workspace_floats(T, NB * W3))
         self._call(b, "vqa_colsum", dq, 1, T, NB * W3, NB * W3, None, 0.0, ws)
-        b[-1].side = getattr(self, "colsum_side", False)
         self._defer(ws, lib.vqa_colsum_parts(T), NB * W3, NB * W3, self.g32["sga0.qkv1_b"])
         self._jobs[-1] = self._jobs[-1][:-1] + (self._jobs[-1][-1] + keep,)
         mark(f"sga{NB - 1}.m1_b")
@@ -857,17 +821,17 @@ class VQAEngine:
         self._bsplit.append(len(b))
         # T5 encoder backward.  dH32 is the gradient of the residual stream h_i; dH16 the
         # dropout-masked gradient of the FF branch that produced it (T5LayerFF :140).
-        nl = S.T5_LAYERS
+        nl = self.nl
         # per-layer bf16 gradients the weight gradients read, stacked like the inputs (slot 11 - i)
         self.dH16S, self.dHMS = self._t((nl, T, D), BF16), self._t((nl, T, D), BF16)
-        self.dFS, self.dQKVS = self._t((nl, T, S.T5_DFF), BF16), self._t((nl, T, 3 * D), BF16)
+        self.dFS, self.dQKVS = self._t((nl, T, self.dff), BF16), self._t((nl, T, 3 * D), BF16)
         dH16 = [self.dH16S[nl - 1 - i] for i in range(nl)]               # FF-branch grad of layer i
         G = self.t5_dw_group
         kp = []
         ws = self._norm_ws()
         self._call(b, "vqa_rmsnorm_bwd", self.dTXT, self.HS[-1], self.RF, self.p32["t5.final_ln"], None, self.dH32,
                    dH16[-1], None, 0.0, ws, T, D,
-                   self._dptr(SITE_FINAL, kp), None, self._dptr(t5_site(S.T5_LAYERS - 1, 3), kp),
+                   self._dptr(SITE_FINAL, kp), None, self._dptr(t5_site(self.nl - 1, 3), kp),
                    extra=kp + [self.RNG])
         self._defer(ws, nparts, D, D, self.g32["t5.final_ln"])
         mark("t5.final_ln")
@@ -890,8 +854,8 @@ class VQAEngine:
             q = self.QKV[i]
             dq = dQKV
             self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
-                       ldv=3 * D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B, heads=S.T5_HEADS, lq=Lq,
-                       lk=Lq, dh=S.T5_DKV, scale=1.0, dout=self.dO16, lddo=D, dq=dq, lddq=3 * D,
+                       ldv=3 * D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B, heads=self.h5, lq=Lq,
+                       lk=Lq, dh=self.dkv, scale=1.0, dout=self.dO16, lddo=D, dq=dq, lddq=3 * D,
                        dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dSB[i],
                        drop=t5_site(i, 0))
             dxdw(b, dq, self.N0[i], f"t5.{i}.qkv_w", T, out32=self.dC32)
@@ -913,17 +877,17 @@ class VQAEngine:
                 k = int(np.searchsorted(ends, done))
                 self._t5_group_dw(b, i + self.t5_dw_groups[k] - 1, i)
                 mark(f"t5.{i}.ln1")
-                if self._sq_split is None and i > 0 and self._sq_early:   # the first T5 dW group is final
+                if self._sq_split is None and i > 0:      # the first T5 dW group is final
                     self._sq_split = self.ready_marks[-1]
             elif ends is None and (done % G == 0 or i == 0):
                 self._t5_group_dw(b, i + (done - 1) % G, i)
                 mark(f"t5.{i}.ln1")
-                if self._sq_split is None and i > 0 and self._sq_early:
+                if self._sq_split is None and i > 0:
                     self._sq_split = self.ready_marks[-1]
         # the relative-position bias is shared by all 12 layers: dPB = sum over (layer, sample) of dS,
         # one fixed-order reduction after the last layer instead of one per layer
-        self._call(b, "vqa_batch_sum", self.dSB, S.T5_LAYERS * B, S.T5_HEADS * Lq * Lq, self.dPB, 0.0)
-        self._call(b, "vqa_t5_relbias_bwd", self.dPB, self.bucket, self.g32["t5.relbias"], S.T5_HEADS, Lq, Lq,
+        self._call(b, "vqa_batch_sum", self.dSB, self.nl * B, self.h5 * Lq * Lq, self.dPB, 0.0)
+        self._call(b, "vqa_t5_relbias_bwd", self.dPB, self.bucket, self.g32["t5.relbias"], self.h5, Lq, Lq,
                    S.T5_BUCKETS)
         mark("t5.relbias")
         self._flush(b)
@@ -934,7 +898,7 @@ class VQAEngine:
     def _t5_group_dw(self, lst, i_hi, i_lo):
         """Weight gradients of T5 layers i_hi >= .. >= i_lo: per weight one launch batched over
         the layers (stack slot 11 - i, consecutive gradient segments at a constant stride)."""
-        nl, T = S.T5_LAYERS, self.T
+        nl, T = self.nl, self.T
         cnt, s0 = i_hi - i_lo + 1, nl - 1 - i_hi
         for w, dys, xs in (("wo", self.dH16S, self.FFS), ("wi", self.dFS, self.N1S), ("o_w", self.dHMS, self.OS),
                            ("qkv_w", self.dQKVS, self.N0S)):
@@ -991,8 +955,8 @@ class VQAEngine:
         # start behind its 0.9 GB pass).  Same arithmetic, same order of updates vs uses.
         lay = self.lay
         cuts = [("embed", lay["t5.relbias"].offset, n)]
-        for i in range(S.T5_LAYERS):
-            lo = lay[f"t5.{i}.qkv_w"].offset if i < S.T5_LAYERS - 1 else lay["t5.final_ln"].offset
+        for i in range(self.nl):
+            lo = lay[f"t5.{i}.qkv_w"].offset if i < self.nl - 1 else lay["t5.final_ln"].offset
             hi = lay[f"t5.{i - 1}.qkv_w"].offset if i > 0 else lay["t5.relbias"].offset
             cuts.append((f"t5.{i}", lo, hi))
         cuts.append(("scaler", lay["scaler_w"].offset, lay["t5.final_ln"].offset))
@@ -1010,31 +974,15 @@ class VQAEngine:
             for i, e in enumerate(ends):
                 ds.group_end[i] = e - lo
             c = ops.Call("vqa_adamw_amsgrad", ctypes.byref(ds), desc=ds, keep=keep)
-            if name == "embed" and not self.defer_embed:
+            if name == "embed":
                 self.adam_embed = c
             else:
                 self.adam_segs.append((name, c))
-        # norm_fold: the folded weights W o w follow every update of W or w (each T5 layer's
-        # range carries its own: the layer's q|k|v, wi and norm weights all sit in it)
-        fold = {}
-        self.fold_all = []
-        if self.norm_fold:
-            for i in range(S.T5_LAYERS):
-                lst = []
-                if i > 0:
-                    self._call(lst, "vqa_scale_cols_bf16", self.p32[f"t5.{i}.qkv_w"], self.p32[f"t5.{i}.ln0"],
-                               self.WQF[i], 3 * D, D)
-                self._call(lst, "vqa_scale_cols_bf16", self.p32[f"t5.{i}.wi"], self.p32[f"t5.{i}.ln1"], self.WIF[i],
-                           S.T5_DFF, D)
-                fold[f"t5.{i}"] = lst
-                self.fold_all += lst
-        self.adam_segs = [(nm, _Seq([c] + fold[nm]) if nm in fold else c) for nm, c in self.adam_segs]
         lst = []
         self._call(lst, "vqa_zero", ops.addr(self.opt_state, L.ST_PENDING), 16, extra=[self.opt_state])
         self.clear_pending = lst[0]
         if not self.defer_opt:
             o.append(self.adam_full)
-            o += self.fold_all
         elif self.adam_embed is not None:
             o.append(self.adam_embed)
 
@@ -1121,8 +1069,8 @@ class VQAEngine:
         the sequential order (and bit-identical: no cross-branch reductions)."""
         self.run_forward_streams()
         if optimizer:
-            self.run_backward_streams(sq_overlap=self.sq_overlap)
-            self._run(self.opt_calls[2:] if self.sq_overlap else self.opt_calls)
+            self.run_backward_streams(sq_overlap=True)
+            self._run(self.opt_calls[2:])
         else:
             self.run_backward_streams()
 
@@ -1157,18 +1105,7 @@ class VQAEngine:
             join = torch.cuda.Event()
             join.record(side)
             main.wait_event(join)
-        if self._fnorm is None:
-            self._run(f[p2:])                              # SGA + head
-            return
-        ev = torch.cuda.Event()                            # both branches are done: T5 outputs final
-        ev.record(main)
-        self._nstream.wait_event(ev)
-        with torch.cuda.stream(self._nstream):
-            self._run(f[self._fnorm:])                     # the batched off-chain RMSNorms
-        self._run(f[p2:self._fnorm])                       # SGA + head
-        done = torch.cuda.Event()
-        done.record(self._nstream)
-        main.wait_event(done)
+        self._run(f[p2:])                                  # SGA + head
 
     def _forward_branches_deferred(self, fork, main, side, vis, txt):
         """The two forward branches with the previous step's AdamW ranges on a third stream.
@@ -1177,11 +1114,9 @@ class VQAEngine:
         first held the T5 chain back ~0.47 ms); the vision branch's parameter-reading
         calls wait for the scaler range, the SGA / head for the last range."""
         hm, hs = L.stream_handle(main), L.stream_handle(side)
-        # the ranges run on the vision-branch stream (VQA_OPT_STREAM=1: a stream of their own);
-        # a fourth concurrent stream shares a hardware queue with one of the others anyway
-        ost = self._ostream if os.environ.get("VQA_OPT_STREAM", "0") == "1" else main
-        if ost is not main:
-            ost.wait_event(fork)
+        # the ranges run on the vision-branch stream: a fourth concurrent stream shares a
+        # hardware queue with one of the others anyway (measured 6.85 vs 6.81 ms)
+        ost = main
         hs_o = L.stream_handle(ost)
         segs = dict(self.adam_segs)
         order = [n for n, _ in self.adam_segs]
@@ -1196,9 +1131,7 @@ class VQAEngine:
         nl = len(starts)
         # ranges in issue order: layers 0, 1, the scaler, the SGA / head range (the vision
         # branch's SGA block-0 k/v projection reads it), then layer i+2 at layer i
-        if "embed" in segs:                               # defer_embed: the table's range leads
-            issue("embed")
-        ahead = max(1, int(os.environ.get("VQA_OPT_AHEAD", "2")))   # layers a range runs ahead of its use
+        ahead = 2                                          # layers a range runs ahead of its use
         for i in range(min(ahead, nl)):
             issue(f"t5.{i}")
         issue("scaler")
@@ -1207,14 +1140,9 @@ class VQAEngine:
         vpost = vis[self._fvis_param - p0:]                # ConvTranspose2d + SGA block 0 k/v
         bounds = starts + [len(txt)]
         j = 0
-        if "embed" in ev:
-            side.wait_event(ev["embed"])
         for t in range(bounds[0]):                         # embedding + rel-bias
             txt[t](hs)
-        hook = getattr(self, "_res_hook", None)
         for i in range(nl):
-            if hook is not None and hook[0] == i:
-                hook[1]()
             if i + ahead < nl:
                 issue(f"t5.{i + ahead}")
             side.wait_event(ev[f"t5.{i}"])
@@ -1282,10 +1210,12 @@ class VQAEngine:
 
     def _run_tagged(self, calls, main, wside):
         """Run `calls` in order on `main`, except runs of side-tagged calls (weight
-        gradients), which go to `wside` after an event on `main` at that point.
-        Off by default (`dw_stream`): measured on MI355X, each cross-stream edge
-        inside the graph costs ~10-20 us of idle time on the chain, more than
-        the overlap gains at this model's sizes."""
+        gradients), which go to `wside` after an event on `main` at that point
+        (`dw_stream`).  On for the single-GPU weight-gradient grouping (9, 3), where the
+        batched T5 dW launches trail the input-gradient chain (6.66 vs 6.78-6.84 ms per
+        step); off for the DP grouping, whose buckets must be final in chain order.  Every
+        bf16 gradient a side-tagged call reads has its own buffer (_gbuf), so no later chain
+        call overwrites it (tests: test_dw_stream_matches_single_stream_bitwise)."""
         if not self.dw_stream:
             self._run(calls)
             return
@@ -1310,26 +1240,18 @@ class VQAEngine:
         step's whole chain on the current stream; joined at the end.  The two sides share
         no buffer, so every result equals the unpipelined step's bit for bit."""
         main = torch.cuda.current_stream(self.dev)
-        self.F4.copy_(self.F4N)
+        self.copy_f4(L.stream_handle(main))
         fork = torch.cuda.Event()
         fork.record(main)
         self._rstream.wait_event(fork)
 
-        def issue_res():
-            with torch.cuda.stream(self._rstream):
-                self._run(self.res_calls)
-        # capture position of the ResNet branch (a replayed graph submits nodes in capture
-        # order): VQA_RES_AT = T5 layer index before whose calls it is issued (-1: first)
-        at = int(os.environ.get("VQA_RES_AT", "-1"))
-        if at < 0 or not self.defer_opt:
-            issue_res()
-            self._res_hook = None
-        else:
-            self._res_hook = (at, issue_res)
+        # the ResNet branch is captured first: a replayed graph submits nodes in capture order,
+        # and issuing it after T5 layer 0 / 1 / 3 measured 0.7 ms slower (DESIGN §3.8)
+        with torch.cuda.stream(self._rstream):
+            self._run(self.res_calls)
         self.run_forward_streams()                         # ConvTranspose2d || T5 encoder, then SGA
-        self._res_hook = None
-        self.run_backward_streams(sq_overlap=self.sq_overlap)
-        self._run(self.opt_calls[2:] if self.sq_overlap else self.opt_calls)
+        self.run_backward_streams(sq_overlap=True)
+        self._run(self.opt_calls[2:])
         join = torch.cuda.Event()
         join.record(self._rstream)
         main.wait_event(join)
@@ -1353,9 +1275,12 @@ class VQAEngine:
             self.allreduce(self.G32)
         self.optimizer_step()
 
-    def capture(self, warm=True):
+    def capture(self, warm=True, keep_graph=False):
         """Capture the step as hipGraph(s): one graph when single-GPU; with a DP
-        all-reduce hook, graph(fwd+bwd) -> eager collective -> graph(optimizer)."""
+        all-reduce hook, graph(fwd+bwd) -> eager collective -> graph(optimizer).
+        keep_graph: keep the hipGraph_t of each part (torch CUDAGraph keep_graph) so tests can
+        walk its nodes (raw_cuda_graph); the exec is instantiated here either way."""
+        self._keep_graph = bool(keep_graph)
         self.flush_optimizer()           # the warm-up's backward must not overwrite a pending update's G
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
@@ -1370,11 +1295,17 @@ class VQAEngine:
             parts = self._capture_parts(s)
         self.opt_state.copy_(saved)
         self.RNG.copy_(saved_rng)                       # the warm-up launch must not consume a dropout draw
+        for g in parts:
+            if self._keep_graph and not callable(g):
+                g.instantiate()
         self.graph = parts
+
+    def _new_graph(self):
+        return torch.cuda.CUDAGraph(keep_graph=getattr(self, "_keep_graph", False))
 
     def _capture_parts(self, s):
         if self.allreduce is None:
-            g = torch.cuda.CUDAGraph()
+            g = self._new_graph()
             with torch.cuda.graph(g, stream=s):
                 if self.pipeline:
                     self._step_pipelined()
@@ -1382,7 +1313,7 @@ class VQAEngine:
                     self._run_step_streams()
             parts = [g]
         else:
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            g1, g2 = self._new_graph(), self._new_graph()
             with torch.cuda.graph(g1, stream=s):
                 self.forward()
                 self.backward()
@@ -1549,7 +1480,7 @@ class VQAEngine:
         self.flush_optimizer()
         sd = dict(self._frozen)
         sd.update(self.lay.unpack(self.P32.cpu().numpy()))
-        specs = S.model_specs(self.vision, self.A, self.NB)
+        specs = S.model_specs(self.vision, self.A, self.NB, self.dims)
         return {k: sd[k] for k in specs}
 
     def segment_grad(self, name):
@@ -1561,7 +1492,7 @@ class VQAEngine:
         q|k|v and k|v stacks are row blocks, so their parts are exact reference-shaped views;
         the ConvTranspose2d scaler is stored as the flipped conv weight, so its view has the
         kernel layout [768, 3, 3, Cin] (layout.py).  None if `key` is not trainable here."""
-        specs = S.model_specs(self.vision, self.A, self.NB)
+        specs = S.model_specs(self.vision, self.A, self.NB, self.dims)
         for sg in self.lay.segments.values():
             if key not in sg.parts:
                 continue
@@ -1582,7 +1513,6 @@ class VQAEngine:
         """Re-derive the bf16 GEMM shadow from the fp32 masters (after writing weights through
         param_view / ParameterGroup views)."""
         self.P16.copy_(self.P32)
-        self._run(self.fold_all)
 
     def layer4_features(self):
         """The frozen ResNet's layer4 map of the current batch as NCHW fp32 (the kernels keep

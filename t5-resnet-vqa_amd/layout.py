@@ -49,9 +49,11 @@ class Segment:
 
 
 class ParamLayout:
-    def __init__(self, vision="resnet50", answer_spaces=170, num_blocks=3):
+    def __init__(self, vision="resnet50", answer_spaces=170, num_blocks=3, language_model="t5-base"):
         self.vision, self.answer_spaces, self.num_blocks = vision, answer_spaces, num_blocks
-        D, A = S.D_MODEL, answer_spaces
+        self.dims = dm = S.lm_dims(language_model)
+        D, A = dm.d_model, answer_spaces
+        HI = dm.t5_heads * dm.t5_dkv                 # T5 attention inner width (= D for t5-base/large)
         self.scaler = "downscale_layer" if vision == "resnet50" else "upscale_layer"
         self.scaler_cin = 2048 if vision == "resnet50" else 512
         segs = []
@@ -92,15 +94,15 @@ class ParamLayout:
         add("scaler_b", (D,), "scaler", [self.scaler + ".bias"])
         t5 = "lang_model."
         add("t5.final_ln", (D,), "lang_model", [t5 + "final_layer_norm.weight"])
-        for i in reversed(range(S.T5_LAYERS)):
+        for i in reversed(range(dm.t5_layers)):
             b = f"{t5}block.{i}.layer."
-            add(f"t5.{i}.qkv_w", (3 * D, D), "lang_model", [b + f"0.SelfAttention.{x}.weight" for x in "qkv"])
-            add(f"t5.{i}.o_w", (D, D), "lang_model", [b + "0.SelfAttention.o.weight"])
+            add(f"t5.{i}.qkv_w", (3 * HI, D), "lang_model", [b + f"0.SelfAttention.{x}.weight" for x in "qkv"])
+            add(f"t5.{i}.o_w", (D, HI), "lang_model", [b + "0.SelfAttention.o.weight"])
             add(f"t5.{i}.ln0", (D,), "lang_model", [b + "0.layer_norm.weight"])
-            add(f"t5.{i}.wi", (S.T5_DFF, D), "lang_model", [b + "1.DenseReluDense.wi.weight"])
-            add(f"t5.{i}.wo", (D, S.T5_DFF), "lang_model", [b + "1.DenseReluDense.wo.weight"])
+            add(f"t5.{i}.wi", (dm.t5_dff, D), "lang_model", [b + "1.DenseReluDense.wi.weight"])
+            add(f"t5.{i}.wo", (D, dm.t5_dff), "lang_model", [b + "1.DenseReluDense.wo.weight"])
             add(f"t5.{i}.ln1", (D,), "lang_model", [b + "1.layer_norm.weight"])
-        add("t5.relbias", (S.T5_BUCKETS, S.T5_HEADS), "lang_model",
+        add("t5.relbias", (S.T5_BUCKETS, dm.t5_heads), "lang_model",
             [t5 + "block.0.layer.0.SelfAttention.relative_attention_bias.weight"])
         add("t5.embed", (S.T5_VOCAB, D), "lang_model", [t5 + "embed_tokens.weight"])
 
@@ -144,7 +146,7 @@ class ParamLayout:
         """flat arena -> reference state_dict entries (reference shapes/layout)."""
         flat = np.asarray(flat)
         out = OrderedDict()
-        specs = S.model_specs(self.vision, self.answer_spaces, self.num_blocks)
+        specs = S.model_specs(self.vision, self.answer_spaces, self.num_blocks, self.dims)
         for s in self.segments.values():
             v = flat[s.offset:s.offset + s.numel].reshape(s.shape)
             if s.kind == "convT":

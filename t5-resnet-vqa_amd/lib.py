@@ -90,6 +90,7 @@ GEMM_KC_B_ONLY = (13, 14, 15, 16)        # tile configs that need a k-contiguous
 GEMM_BK128 = (21, 22, 23)                # 128-deep k-tiles: no implicit im2col operand, no split-K
 GEMM_WAVES = {c: ((4, 2) if c in (9, 12) else (2, 4) if c in (10, 11) else (2, 2)) for c in GEMM_TILES}
 
+ATTN_MFMA, ATTN_LONG, ATTN_VALU = 0, 1, 2          # vqa_attn_path
 MAX_GROUPS = 8
 ST_STEP, ST_GRAD_NORM, ST_CLIP_COEF, ST_LR_SCALE, ST_BC1, ST_BC2_SQRT = range(6)
 ST_PENDING, ST_FLOATS = 8, 16
@@ -139,6 +140,7 @@ def load():
     lib.vqa_gemm_pair.argtypes = [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc), c_void_p]
     lib.vqa_attn_fwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_attn_bwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
+    lib.vqa_attn_path.argtypes = [ctypes.POINTER(AttnDesc), c_int]
     lib.vqa_adamw_amsgrad.argtypes = [ctypes.POINTER(AdamWDesc), c_void_p]
     for name in ("vqa_norm_bwd_workspace_floats", "vqa_colsum_workspace_floats"):
         getattr(lib, name).argtypes = [c_int, c_int]
@@ -184,6 +186,7 @@ register("vqa_t5_relbias_bwd", P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_batch_sum", P, c_int, c_ll, P, c_float)
 register("vqa_cast_f32_bf16", P, P, c_ll)
 register("vqa_zero", P, c_ll)
+register("vqa_copy", P, P, c_ll)
 register("vqa_head_fwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_head_bwd", P, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_grad_sqnorm", P, c_ll, P, c_int)

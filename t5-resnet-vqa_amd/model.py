@@ -42,8 +42,8 @@ class ParameterGroup:
 
     def _keys(self):
         m = self._model
-        return [k for k in S.model_specs(m.vision_model_name, m.answer_spaces, m.num_attention_blocks)
-                if k.startswith(self.prefix + ".")]
+        return [k for k in S.model_specs(m.vision_model_name, m.answer_spaces, m.num_attention_blocks,
+                                         m.language_model_name) if k.startswith(self.prefix + ".")]
 
     def named_parameters(self):
         e = self._model.engine
@@ -90,9 +90,12 @@ class ResnetVQAModel:
         # fail here, with the reason.
         if vision_model_name not in SUPPORTED_VISION:
             raise ValueError(f"vision_model_name {vision_model_name!r}: this path supports {SUPPORTED_VISION}")
-        if language_model_name not in ("t5-base",):
-            raise ValueError("language_model_name must be 't5-base' (d_model 768 is hard-coded in the SGA blocks, "
-                             "multi_head_vision_text_attn.py:9,19)")
+        # t5-base is the reference's model (resnet_vqa_model.py:60-62); t5-large is BASELINE
+        # configs[4]: the encoder of the published t5-large sizes with the SGA blocks, scaler,
+        # pooler and classifier built at its width 1024 (the reference hard-codes 768 only in
+        # those constructors, multi_head_vision_text_attn.py:9,19, resnet_vqa_model.py:64-89)
+        if language_model_name not in S.LM_DIMS:
+            raise ValueError(f"language_model_name must be one of {tuple(S.LM_DIMS)}")
         if num_attention_blocks < 1:
             raise ValueError("num_attention_blocks must be >= 1")
         self.vision_model_name = vision_model_name
@@ -104,7 +107,8 @@ class ResnetVQAModel:
         self._cfg = dict(dropout=float(dropout), seed=int(dropout_seed))
         if state_dict is None:
             state_dict = S.make_state_dict(vision_model_name, seed=seed, answer_spaces=self.answer_spaces,
-                                           num_attention_blocks=self.num_attention_blocks)
+                                           num_attention_blocks=self.num_attention_blocks,
+                                           language_model=language_model_name)
         self._build(state_dict)
         self.training = True
         # the sub-module attributes the reference trainer reads (faster_rcnn_vqa_trainer.py:231-263)
@@ -121,15 +125,16 @@ class ResnetVQAModel:
     def _build(self, state_dict, **kw):
         sd = {k: (v.detach().cpu().float().numpy() if isinstance(v, torch.Tensor) else np.asarray(v))
               for k, v in state_dict.items()}
-        missing = [k for k in S.model_specs(self.vision_model_name, self.answer_spaces, self.num_attention_blocks)
-                   if k not in sd]
+        missing = [k for k in S.model_specs(self.vision_model_name, self.answer_spaces, self.num_attention_blocks,
+                                            self.language_model_name) if k not in sd]
         if missing:
             raise KeyError(f"state_dict lacks {len(missing)} reference keys, e.g. {missing[:3]}")
         opt = dict(getattr(self, "_opt", {}))
         opt.update(kw)
         self.engine = VQAEngine(sd, vision=self.vision_model_name, batch=self.batch_size, seq_len=self.seq_len,
                                 image_size=self.image_size, device=self.device, answer_spaces=self.answer_spaces,
-                                num_blocks=self.num_attention_blocks, **self._cfg, **opt)
+                                num_blocks=self.num_attention_blocks, language_model=self.language_model_name,
+                                **self._cfg, **opt)
         self._opt = opt
 
     def train(self, mode=True):

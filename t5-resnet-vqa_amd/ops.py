@@ -99,6 +99,51 @@ class Call:
             L.check(rc, self.name)
 
 
+_PTR_FIELDS = {"GemmDesc": ("a", "b", "c32", "c16", "bias", "res32", "res16", "mask16", "workspace"),
+               "AttnDesc": ("q", "k", "v", "o", "p", "bias", "key_mask", "dout", "dq", "dk", "dv", "dbias"),
+               "AdamWDesc": ("param", "grad", "exp_avg", "exp_avg_sq", "max_exp_avg_sq", "param16", "state")}
+
+
+def _pointers(call):
+    """(where, address) of every device / host address a prepared call passes: plain
+    integer arguments that can only be addresses, and the pointer fields of the descriptors
+    it passes by reference (with their dropout RNG pointers)."""
+    out = []
+    for i, a in enumerate(call.args):
+        if isinstance(a, int) and a >= 1 << 36:
+            out.append((f"arg{i}", a))
+        obj = getattr(a, "_obj", None)                      # ctypes.byref(desc)
+        if obj is not None:
+            for f in _PTR_FIELDS.get(type(obj).__name__, ()):
+                v = getattr(obj, f)
+                if v:
+                    out.append((f"arg{i}.{f}", v))
+            drop = getattr(obj, "drop", None)
+            if drop is not None and drop.rng:
+                out.append((f"arg{i}.drop.rng", drop.rng))
+    return out
+
+
+def uncovered_pointers(call):
+    """Addresses baked into `call` that no object in its `keep` owns (Call docstring: a
+    tensor freed behind a prepared call's back hands its memory to the next allocation).
+    A tensor covers its whole storage; a ctypes structure its own bytes."""
+    spans = []
+
+    def add(o):
+        if isinstance(o, torch.Tensor):
+            st = o.untyped_storage()
+            spans.append((st.data_ptr(), st.data_ptr() + st.nbytes()))
+        elif isinstance(o, ctypes.Structure):
+            spans.append((ctypes.addressof(o), ctypes.addressof(o) + ctypes.sizeof(o)))
+        elif isinstance(o, (tuple, list)):
+            for x in o:
+                add(x)
+    add(call.keep or ())
+    add(call.desc if call.desc is not None else ())
+    return [(w, hex(p)) for w, p in _pointers(call) if not any(a <= p < b for a, b in spans)]
+
+
 def gemm_call(desc, tensors=()):
     return Call("vqa_gemm", ctypes.byref(desc), keep=tuple(tensors), desc=desc)
 

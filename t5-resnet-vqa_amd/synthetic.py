@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import zlib
 from collections import OrderedDict
+from typing import NamedTuple
 
 import numpy as np
 
@@ -36,6 +37,37 @@ T5_MAX_DIST = 128
 SGA_HEADS = 8
 SGA_DHEAD = 96
 QUESTION_TOKEN = 32100      # id of the added "[Question]" special token
+
+
+
+class LMDims(NamedTuple):
+    """Widths of the language model and of the SGA blocks built to its width."""
+    name: str
+    d_model: int
+    t5_layers: int
+    t5_heads: int
+    t5_dkv: int
+    t5_dff: int
+    sga_heads: int          # MULTI_HEAD (multi_head_vision_text_attn.py:10)
+    sga_dhead: int          # HIDDEN_SIZE_HEAD = HIDDEN_SIZE // MULTI_HEAD (:11)
+
+
+# t5-base: the reference's configuration (TextConfiguration / ImageConfiguration, :7-24).
+# t5-large: BASELINE configs[4] -- the T5-large encoder (published t5-large sizes) with the SGA
+# blocks, scaler, pooler and classifier at its width 1024 (8 heads of 128, FF 1024), i.e. the
+# reference modules built from configuration instances with HIDDEN_SIZE = FF_SIZE = 1024.
+LM_DIMS = {"t5-base": LMDims("t5-base", 768, 12, 12, 64, 3072, 8, 96),
+           "t5-large": LMDims("t5-large", 1024, 24, 16, 64, 4096, 8, 128)}
+BASE = LM_DIMS["t5-base"]
+
+
+def lm_dims(language_model="t5-base") -> LMDims:
+    if isinstance(language_model, LMDims):
+        return language_model
+    if language_model not in LM_DIMS:
+        raise ValueError(f"language_model {language_model!r}: this path supports {tuple(LM_DIMS)}")
+    return LM_DIMS[language_model]
+
 
 RESNET_LAYERS = {"resnet18": (2, 2, 2, 2), "resnet34": (3, 4, 6, 3), "resnet50": (3, 4, 6, 3)}
 
@@ -79,55 +111,63 @@ def resnet_specs(arch: str):
     return specs
 
 
-def t5_specs():
+def t5_specs(dims=BASE):
+    d = lm_dims(dims)
+    D = d.d_model
     specs = OrderedDict()
-    specs["embed_tokens.weight"] = (T5_VOCAB, D_MODEL)
-    for i in range(T5_LAYERS):
+    specs["embed_tokens.weight"] = (T5_VOCAB, D)
+    for i in range(d.t5_layers):
         p = f"block.{i}.layer."
-        for n in "qkvo":
-            specs[f"{p}0.SelfAttention.{n}.weight"] = (D_MODEL, D_MODEL)
+        inner = d.t5_heads * d.t5_dkv
+        for n in "qkv":
+            specs[f"{p}0.SelfAttention.{n}.weight"] = (inner, D)
+        specs[f"{p}0.SelfAttention.o.weight"] = (D, inner)
         if i == 0:
-            specs[f"{p}0.SelfAttention.relative_attention_bias.weight"] = (T5_BUCKETS, T5_HEADS)
-        specs[f"{p}0.layer_norm.weight"] = (D_MODEL,)
-        specs[f"{p}1.DenseReluDense.wi.weight"] = (T5_DFF, D_MODEL)
-        specs[f"{p}1.DenseReluDense.wo.weight"] = (D_MODEL, T5_DFF)
-        specs[f"{p}1.layer_norm.weight"] = (D_MODEL,)
-    specs["final_layer_norm.weight"] = (D_MODEL,)
+            specs[f"{p}0.SelfAttention.relative_attention_bias.weight"] = (T5_BUCKETS, d.t5_heads)
+        specs[f"{p}0.layer_norm.weight"] = (D,)
+        specs[f"{p}1.DenseReluDense.wi.weight"] = (d.t5_dff, D)
+        specs[f"{p}1.DenseReluDense.wo.weight"] = (D, d.t5_dff)
+        specs[f"{p}1.layer_norm.weight"] = (D,)
+    specs["final_layer_norm.weight"] = (D,)
     return specs
 
 
-def sga_specs():
+def sga_specs(dims=BASE):
+    D = lm_dims(dims).d_model
     specs = OrderedDict()
     for m in ("mhatt1", "mhatt2"):
         for lin in ("linear_v", "linear_k", "linear_q", "linear_merge"):
-            specs[f"{m}.{lin}.weight"] = (D_MODEL, D_MODEL)
-            specs[f"{m}.{lin}.bias"] = (D_MODEL,)
+            specs[f"{m}.{lin}.weight"] = (D, D)
+            specs[f"{m}.{lin}.bias"] = (D,)
     for fc in ("fc1", "fc2"):
-        specs[f"ffn.mlp.{fc}.weight"] = (D_MODEL, D_MODEL)
-        specs[f"ffn.mlp.{fc}.bias"] = (D_MODEL,)
+        specs[f"ffn.mlp.{fc}.weight"] = (D, D)
+        specs[f"ffn.mlp.{fc}.bias"] = (D,)
     for n in ("norm1", "norm2", "norm3"):
-        specs[f"{n}.norm.weight"] = (D_MODEL,)
-        specs[f"{n}.norm.bias"] = (D_MODEL,)
+        specs[f"{n}.norm.weight"] = (D,)
+        specs[f"{n}.norm.bias"] = (D,)
     return specs
 
 
-def model_specs(vision: str = "resnet50", answer_spaces: int = 170, num_attention_blocks: int = 3):
+def model_specs(vision: str = "resnet50", answer_spaces: int = 170, num_attention_blocks: int = 3,
+                language_model="t5-base"):
     """Full `ResnetVQAModel.state_dict()` key -> shape, in module registration order."""
+    d = lm_dims(language_model)
+    D = d.d_model
     specs = OrderedDict()
     for k, s in resnet_specs(vision).items():
         specs["vision_model." + k] = s
-    for k, s in t5_specs().items():
+    for k, s in t5_specs(d).items():
         specs["lang_model." + k] = s
-    specs["upscale_layer.weight"] = (512, D_MODEL, 3, 3)
-    specs["upscale_layer.bias"] = (D_MODEL,)
-    specs["downscale_layer.weight"] = (2048, D_MODEL, 3, 3)
-    specs["downscale_layer.bias"] = (D_MODEL,)
+    specs["upscale_layer.weight"] = (512, D, 3, 3)
+    specs["upscale_layer.bias"] = (D,)
+    specs["downscale_layer.weight"] = (2048, D, 3, 3)
+    specs["downscale_layer.bias"] = (D,)
     for n in range(num_attention_blocks):
-        for k, s in sga_specs().items():
+        for k, s in sga_specs(d).items():
             specs[f"sga_modules.{n}.{k}"] = s
-    specs["classification_layer.weight"] = (answer_spaces, D_MODEL)
+    specs["classification_layer.weight"] = (answer_spaces, D)
     specs["classification_layer.bias"] = (answer_spaces,)
-    specs["attention_pooler.attention.0.weight"] = (1, D_MODEL)
+    specs["attention_pooler.attention.0.weight"] = (1, D)
     specs["attention_pooler.attention.0.bias"] = (1,)
     return specs
 
@@ -136,8 +176,10 @@ def _rng(seed: int, key: str) -> np.random.Generator:
     return np.random.Generator(np.random.PCG64([seed & 0xFFFFFFFF, zlib.crc32(key.encode())]))
 
 
-def init_param(key: str, shape, seed: int = 0, vision: str = "resnet50") -> np.ndarray:
+def init_param(key: str, shape, seed: int = 0, vision: str = "resnet50", dims=BASE) -> np.ndarray:
     """Closed-form initial value of one state-dict entry (float32; int64 for counters)."""
+    d = lm_dims(dims)
+    D_MODEL, T5_DKV, T5_DFF = d.d_model, d.t5_dkv, d.t5_dff
     if key.endswith("num_batches_tracked"):
         return np.array(0, dtype=np.int64)
     g = _rng(seed, key)
@@ -191,13 +233,14 @@ def init_param(key: str, shape, seed: int = 0, vision: str = "resnet50") -> np.n
 
 
 def make_state_dict(vision: str = "resnet50", seed: int = 0, answer_spaces: int = 170,
-                    num_attention_blocks: int = 3, keys=None) -> "OrderedDict[str, np.ndarray]":
-    specs = model_specs(vision, answer_spaces, num_attention_blocks)
+                    num_attention_blocks: int = 3, keys=None, language_model="t5-base") -> "OrderedDict[str, np.ndarray]":
+    d = lm_dims(language_model)
+    specs = model_specs(vision, answer_spaces, num_attention_blocks, d)
     out = OrderedDict()
     for k, s in specs.items():
         if keys is not None and k not in keys:
             continue
-        out[k] = init_param(k, s, seed, vision)
+        out[k] = init_param(k, s, seed, vision, d)
     return out
 
 

@@ -1,14 +1,13 @@
-"""The benched step (BASELINE configs[1]) against the CPU oracle, in a process of its own.
+"""The benched step (BASELINE configs[1]) against the CPU oracle.
 
-  python tests/bench_step_worker.py OUT.json
+  python tests/bench_step_worker.py OUT.json      (stand-alone: writes the report to OUT.json)
 
-Run by tests/test_parity_full_gpu.py::test_bench_step_b64_matches_oracle.  The engine is
-built exactly as bench.py main() builds it (R50, B=64, 224x224, L=32, pipelined frozen
-ResNet, tuned tile / split-K table, captured hipGraph step, deferred AdamW, dropout 0.1
-from the shared counter hash) in a fresh process, as bench.py runs it, so that the state
-of the 200-odd GPU tests before it in the session (engines, graphs and streams created
-and destroyed) cannot reach it.  Writes the measured errors and the failed checks to
-OUT.json; the test asserts on them (trainer/faster_rcnn_vqa_trainer.py:391-406)."""
+`run()` is called in the pytest session process by
+tests/test_z_bench_step_gpu.py::test_bench_step_b64_matches_oracle, after every other GPU
+test.  The engine is built exactly as bench.py main() builds it (R50, B=64, 224x224, L=32,
+pipelined frozen ResNet, tuned tile / split-K table, captured hipGraph step, deferred AdamW,
+dropout 0.1 from the shared counter hash) and stepped against the CPU oracle
+(trainer/faster_rcnn_vqa_trainer.py:391-406)."""
 import json
 import os
 import sys
@@ -36,7 +35,8 @@ def _dev(nb):
     return {k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None}
 
 
-def main(out_path):
+def run():
+    """Build, tune, capture and step the benched engine against the oracle; returns (report, fails)."""
     pkg = load_package()
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     B, L, H = 64, 32, 224
@@ -96,8 +96,13 @@ def main(out_path):
             den += float((do ** 2).sum())
         delta[g] = (num / den) ** 0.5 if den > 0 else 0.0
     rep["update_rel_l2"] = delta
-    json.dump({"report": rep, "fails": fails}, open(out_path, "w"), indent=1)
     torch.cuda.synchronize()
+    return rep, fails
+
+
+def main(out_path):
+    rep, fails = run()
+    json.dump({"report": rep, "fails": fails}, open(out_path, "w"), indent=1)
 
 
 if __name__ == "__main__":

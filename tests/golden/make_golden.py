@@ -49,6 +49,8 @@ sys.modules["torchvision.models"] = tvm
 T5_BASE = dict(vocab_size=32128, d_model=768, d_kv=64, d_ff=3072, num_layers=12, num_decoder_layers=12,
                num_heads=12, relative_attention_num_buckets=32, relative_attention_max_distance=128,
                dropout_rate=0.1, layer_norm_epsilon=1e-6, feed_forward_proj="relu")
+# t5-large (BASELINE configs[4]): the published t5-large hyper-parameters
+T5_LARGE = dict(T5_BASE, d_model=1024, d_ff=4096, num_layers=24, num_decoder_layers=24, num_heads=16)
 
 
 def _from_pretrained(cls, name, **kw):
@@ -60,7 +62,7 @@ def _from_pretrained(cls, name, **kw):
 T5ForQuestionAnswering.from_pretrained = classmethod(_from_pretrained)
 
 sys.path.insert(0, "/root/reference")
-from model.resnet_vqa_model import ResnetVQAModel  # noqa: E402
+from model.resnet_vqa_model import AttentionPooler, ResnetVQAModel  # noqa: E402
 from model.multi_head_vision_text_attn import SGA, ImageConfiguration, TextConfiguration  # noqa: E402
 
 from __graft_entry__ import load_package  # noqa: E402
@@ -113,9 +115,9 @@ def group_norms(model):
     return np.array([np.sqrt(acc[g]) for g in GROUPS])
 
 
-def full_model_case(vision, B, L, H, nsteps=3, warmup=2, total=20, seed=1):
+def full_model_case(vision, B, L, H, nsteps=3, warmup=2, total=20, seed=1, builder=None, blocks=3, lm="t5-base"):
     torch.manual_seed(0)
-    model = build_model(vision)
+    model = build_model(vision) if builder is None else builder()
     opt = optimizer_groups(model)
     sched = transformers.get_linear_schedule_with_warmup(opt, num_warmup_steps=warmup, num_training_steps=total)
     nb = syn.make_batch(B, L, H, seed=seed)
@@ -148,10 +150,10 @@ def full_model_case(vision, B, L, H, nsteps=3, warmup=2, total=20, seed=1):
     sd = model.state_dict()
     out["post_t5_q0"] = sd["lang_model.block.0.layer.0.SelfAttention.q.weight"][:4, :16].numpy().copy()
     out["post_cls_w"] = sd["classification_layer.weight"][:4, :16].numpy().copy()
-    out["post_sga_fc1"] = sd["sga_modules.2.ffn.mlp.fc1.weight"][:4, :16].numpy().copy()
+    out["post_sga_fc1"] = sd[f"sga_modules.{blocks - 1}.ffn.mlp.fc1.weight"][:4, :16].numpy().copy()
     scaler = "downscale_layer" if vision == "resnet50" else "upscale_layer"
     out["post_scaler_w"] = sd[scaler + ".weight"][:4, :4].numpy().copy()
-    init = syn.make_state_dict(vision, seed=0)
+    init = syn.make_state_dict(vision, seed=0, num_attention_blocks=blocks, language_model=lm)
     delta = {g: 0.0 for g in GROUPS}
     for k, v in sd.items():
         if k.startswith("vision_model"):
@@ -196,6 +198,88 @@ def t5_case():
             "rel": rel.numpy(), "buckets": buckets.numpy()}
 
 
+# --------------------------------------------------------------------------- config 5 (width 1024)
+def wide_configs(hidden=1024):
+    """The reference SGA reads its widths from configuration INSTANCES
+    (multi_head_vision_text_attn.py:7-24, 128-143): instances with HIDDEN_SIZE 1024 (8 heads of
+    128, FF 1024) give the reference's own SGA at T5-large width; no reference file changes."""
+    cfgs = []
+    for cls in (ImageConfiguration, TextConfiguration):
+        c = cls()
+        c.HIDDEN_SIZE, c.FF_SIZE = hidden, hidden
+        c.HIDDEN_SIZE_HEAD = c.HIDDEN_SIZE // c.MULTI_HEAD
+        cfgs.append(c)
+    return cfgs
+
+
+def t5_large_encoder():
+    cfg = T5Config(**T5_LARGE)
+    cfg._attn_implementation = "eager"
+    return T5ForQuestionAnswering(cfg).encoder
+
+
+def build_model_c5(num_blocks=6):
+    """ResnetVQAModel at config-5 width: the reference class with its width-dependent children
+    replaced by the same module types at d = 1024 (resnet_vqa_model.py:60-89 hard-codes 768
+    only in these constructors); the reference forward() runs unchanged."""
+    m = ResnetVQAModel("resnet50", "t5-base", answer_spaces=170, num_attention_blocks=num_blocks)
+    img_c, txt_c = wide_configs()
+    m.lang_model = t5_large_encoder()
+    m.upscale_layer = torch.nn.ConvTranspose2d(512, 1024, kernel_size=3, stride=1, padding=1)
+    m.downscale_layer = torch.nn.ConvTranspose2d(2048, 1024, kernel_size=3, stride=1, padding=1)
+    m.sga_modules = torch.nn.ModuleList([SGA(img_c, txt_c) for _ in range(num_blocks)])
+    m.classification_layer = torch.nn.Linear(1024, 170)
+    m.attention_pooler = AttentionPooler(1024)
+    sd = syn.make_state_dict("resnet50", seed=0, num_attention_blocks=num_blocks, language_model="t5-large")
+    m.load_state_dict({k: torch.as_tensor(v) for k, v in sd.items()}, strict=True)
+    m.eval()
+    return m
+
+
+def sga1024_case():
+    torch.manual_seed(0)
+    blk = SGA(*wide_configs())
+    sd = {k[len("sga_modules.0."):]: torch.as_tensor(v)
+          for k, v in syn.make_state_dict("resnet50", seed=0, language_model="t5-large").items()
+          if k.startswith("sga_modules.0.")}
+    blk.load_state_dict(sd, strict=True)
+    blk.eval()
+    g = np.random.Generator(np.random.PCG64(8))
+    x = torch.tensor(g.standard_normal((2, 32, 1024), dtype=np.float32), requires_grad=True)
+    y = torch.tensor(g.standard_normal((2, 144, 1024), dtype=np.float32), requires_grad=True)   # 384^2: 12 x 12
+    out = blk(x, y)
+    gout = torch.tensor(g.standard_normal((2, 32, 1024), dtype=np.float32))
+    (out * gout).sum().backward()
+    pn = np.array([float(p.grad.norm()) for _, p in blk.named_parameters()])
+    return {"x": x.detach().numpy(), "y": y.detach().numpy(), "gout": gout.numpy(), "out": out.detach().numpy(),
+            "dx": x.grad.numpy(), "dy": y.grad.numpy(), "param_grad_norms": pn,
+            "param_names": np.array([n for n, _ in blk.named_parameters()])}
+
+
+def t5_large_case():
+    torch.manual_seed(0)
+    enc = t5_large_encoder()
+    sd = syn.make_state_dict("resnet50", seed=0, language_model="t5-large")
+    enc.load_state_dict({k[len("lang_model."):]: torch.as_tensor(v) for k, v in sd.items()
+                         if k.startswith("lang_model.")}, strict=True)
+    enc.eval()
+    nb = syn.make_batch(2, 32, 32, seed=3)
+    ids, mask = torch.as_tensor(nb["question_input_ids"]), torch.as_tensor(nb["question_attention_masks"])
+    h = enc(input_ids=ids, attention_mask=mask).last_hidden_state
+    return {"ids": nb["question_input_ids"], "mask": nb["question_attention_masks"], "hidden": h.detach().numpy()}
+
+
+def main_c5():
+    np.savez_compressed(os.path.join(HERE, "sga1024_block.npz"), **sga1024_case())
+    print("sga1024 done", flush=True)
+    np.savez_compressed(os.path.join(HERE, "t5_large_encoder.npz"), **t5_large_case())
+    print("t5-large done", flush=True)
+    np.savez_compressed(os.path.join(HERE, "model_c5_r50_384_l32.npz"),
+                        **full_model_case("resnet50", 2, 32, 384, builder=build_model_c5, blocks=6,
+                                          lm="t5-large"))
+    print("config-5 model done", flush=True)
+
+
 def main():
     os.makedirs(HERE, exist_ok=True)
     np.savez_compressed(os.path.join(HERE, "sga_block.npz"), **sga_case())
@@ -211,4 +295,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["c5"]:
+        main_c5()
+    else:
+        main()

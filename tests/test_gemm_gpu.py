@@ -343,7 +343,10 @@ def test_kc_b_only_configs_refuse_transposed_b(ops, pkg):
 
 
 @pytest.mark.parametrize("nb,h,c,co", [(2, 14, 64, 96), (3, 7, 128, 64), (2, 28, 256, 128), (2, 56, 64, 64),
-                                       (1, 10, 192, 136), (2, 8, 512, 128)])
+                                       (1, 10, 192, 136), (2, 8, 512, 128),
+                                       # multi-chunk patches too large for the 128-row tile (W 41, 56, 64:
+                                       # R = 128 // W leaves (R+2)(W+2) > 208): dispatched as 64-row tiles
+                                       (1, 41, 128, 64), (1, 56, 128, 128), (1, 64, 128, 64)])
 def test_patch_conv_matches_reference(ops, pkg, nb, h, c, co):
     """a_conv = 2 (3x3 / stride 1 / pad 1 read from LDS input patches, k = (c/64, kh, kw, c%64))
     == F.conv2d in fp32 (bias, ReLU, bf16 residual epilogue), for every patch tile config

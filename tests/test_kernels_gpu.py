@@ -156,6 +156,45 @@ def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5, pd):
         torch.testing.assert_close(red - 3.0, bf.grad, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("Lq", [20, 40])
+def test_causal_bias_with_key_mask_one_finfo_min(k, Lq):
+    """The T5 decoder's causal pairs (bias = finfo.min, vqa_t5_relbias_fwd bucket < 0) under a
+    key-padding mask: HF adds ONE combined extended mask (rel-bias + finfo.min where causal OR
+    padded), so a fully masked query row is a uniform softmax over its keys, not -inf / one-hot
+    (TF modeling_t5.py: position_bias + mask; vit_vqa_model.py:199-205).  Lq 40: VALU kernel."""
+    B, H, dh = 3, 12, 64
+    D, Lk = H * dh, Lq
+    fmin = torch.finfo(torch.float32).min
+    q16 = rnd((B * Lq, D), 40, dtype=torch.bfloat16)
+    kv16 = rnd((B * Lk, 2 * D), 41, dtype=torch.bfloat16)
+    rel = rnd((H, Lq, Lk), 42)
+    causal = torch.triu(torch.ones(Lq, Lk, device="cuda", dtype=torch.bool), 1)
+    bias = torch.where(causal, torch.full_like(rel, fmin), rel)
+    mask = torch.ones(B, Lk, device="cuda", dtype=torch.long)
+    mask[0] = 0                                                   # an empty decoder question
+    mask[1, 5:] = 0
+    L = k.lib
+    o = torch.empty(B * Lq, D, device="cuda", dtype=torch.bfloat16)
+    p = torch.empty(B, H, Lq, Lk, device="cuda")
+    d = L.AttnDesc()
+    A = k.ops.addr
+    d.q, d.ldq, d.k, d.ldk, d.v, d.ldv = A(q16), D, A(kv16), 2 * D, A(kv16, D), 2 * D
+    d.o, d.ldo, d.p, d.bias, d.key_mask = A(o), D, A(p), A(bias), A(mask)
+    d.batch, d.heads, d.lq, d.lk, d.dh, d.scale = B, H, Lq, Lk, dh, 1.0
+    L.check(L.load().vqa_attn_fwd(ctypes.byref(d), L.stream_handle()), "fwd")
+    torch.cuda.synchronize()
+    qf = q16.float().view(B, Lq, H, dh).transpose(1, 2)
+    kf = kv16[:, :D].float().view(B, Lk, H, dh).transpose(1, 2)
+    vf = kv16[:, D:].float().view(B, Lk, H, dh).transpose(1, 2)
+    ext = (causal[None, None] | (mask[:, None, None, :] == 0)).float() * fmin
+    pr = torch.softmax(qf @ kf.transpose(-1, -2) + rel + ext, -1)
+    ref = (pr @ vf).transpose(1, 2).reshape(B * Lq, D)
+    assert torch.isfinite(p).all()
+    torch.testing.assert_close(p, pr, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(o.float(), ref, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(p[0], torch.full_like(p[0], 1.0 / Lk))   # fully masked: uniform
+
+
 @pytest.mark.parametrize("B,L,A,D", [(8, 32, 170, 768), (64, 32, 170, 768), (37, 49, 13, 768), (5, 16, 192, 768),
                                      (64, 32, 170, 1024), (19, 49, 37, 1024), (6, 16, 192, 836), (3, 7, 5, 20),
                                      (16, 32, 193, 768), (21, 32, 700, 768), (5, 16, 1024, 1024)])

@@ -24,6 +24,25 @@ def test_trainable_count_and_roundtrip(pkg, vision, count):
         assert s.offset % 64 == 0
 
 
+def test_t5_large_config5_layout_roundtrip(pkg):
+    """BASELINE configs[4] widths (t5-large encoder, 6 SGA blocks, scaler / pooler / classifier at
+    1024): the arena holds exactly the trainable entries of the reference state dict built at that
+    width, and packs / unpacks them bit for bit."""
+    S = pkg.synthetic
+    lay = pkg.layout.ParamLayout("resnet50", 170, 6, "t5-large")
+    specs = S.model_specs("resnet50", 170, 6, "t5-large")
+    trainable = {k: v for k, v in specs.items() if not k.startswith(("vision_model.", "upscale_layer."))}
+    assert set(lay.trainable_keys) == set(trainable)
+    assert lay.num_params == sum(int(np.prod(v)) for v in trainable.values()) == 417_003_179
+    assert specs["lang_model.block.23.layer.1.DenseReluDense.wi.weight"] == (4096, 1024)
+    assert specs["lang_model.block.0.layer.0.SelfAttention.relative_attention_bias.weight"] == (32, 16)
+    keys = {k for k in trainable if k.startswith(("sga_modules.5.", "lang_model.block.23.", "classification"))}
+    sd = S.make_state_dict("resnet50", seed=5, num_attention_blocks=6, language_model="t5-large")
+    back = lay.unpack(lay.pack(sd))
+    for k in keys:
+        np.testing.assert_array_equal(back[k], sd[k])
+
+
 def test_convT_repack_is_equivalent_conv(pkg):
     lay = pkg.layout
     g = torch.Generator().manual_seed(0)

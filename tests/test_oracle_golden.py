@@ -21,19 +21,26 @@ def test_relative_position_buckets(golden):
     np.testing.assert_array_equal(got, g["buckets"])
 
 
-def test_t5_encoder_matches_reference(golden, pkg):
-    g = golden("t5_encoder")
-    keys = {k for k in pkg.synthetic.model_specs("resnet50") if k.startswith("lang_model.")}
-    sd = {k: torch.as_tensor(v) for k, v in pkg.synthetic.make_state_dict("resnet50", keys=keys).items()}
+@pytest.mark.parametrize("case,lm", [("t5_encoder", "t5-base"), ("t5_large_encoder", "t5-large")])
+def test_t5_encoder_matches_reference(golden, pkg, case, lm):
+    """t5-large: transformers' T5Stack built from a T5Config of the published t5-large sizes
+    (24 layers, d 1024, 16 heads, d_ff 4096; BASELINE configs[4])."""
+    g = golden(case)
+    keys = {k for k in pkg.synthetic.model_specs("resnet50", language_model=lm) if k.startswith("lang_model.")}
+    sd = {k: torch.as_tensor(v)
+          for k, v in pkg.synthetic.make_state_dict("resnet50", keys=keys, language_model=lm).items()}
     h = orc.t5_encoder(sd, torch.as_tensor(g["ids"]), torch.as_tensor(g["mask"]))
     np.testing.assert_allclose(h.numpy(), g["hidden"], atol=2e-5, rtol=1e-4)
 
 
-def test_sga_block_matches_reference(golden, pkg):
-    g = golden("sga_block")
-    keys = {k for k in pkg.synthetic.model_specs("resnet50") if k.startswith("sga_modules.0.")}
+@pytest.mark.parametrize("case,lm", [("sga_block", "t5-base"), ("sga1024_block", "t5-large")])
+def test_sga_block_matches_reference(golden, pkg, case, lm):
+    """sga1024_block: the reference SGA built from configuration instances with HIDDEN_SIZE =
+    FF_SIZE = 1024 (8 heads of 128), x [2, 32, 1024], y [2, 144, 1024] (config 5's 12 x 12 map)."""
+    g = golden(case)
+    keys = {k for k in pkg.synthetic.model_specs("resnet50", language_model=lm) if k.startswith("sga_modules.0.")}
     sd = {k: torch.as_tensor(v).requires_grad_(True)
-          for k, v in pkg.synthetic.make_state_dict("resnet50", keys=keys).items()}
+          for k, v in pkg.synthetic.make_state_dict("resnet50", keys=keys, language_model=lm).items()}
     x = torch.tensor(g["x"], requires_grad=True)
     y = torch.tensor(g["y"], requires_grad=True)
     out = orc.sga_block(sd, "sga_modules.0", x, y)
@@ -47,9 +54,15 @@ def test_sga_block_matches_reference(golden, pkg):
     np.testing.assert_allclose(got, g["param_grad_norms"], rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("case,vision", [("model_r50_224_l32", "resnet50"), ("model_r34_256_l16", "resnet34"),
-                                          ("model_r18_256_l16", "resnet18")])
-def test_full_step_matches_reference(golden, pkg, case, vision):
+@pytest.mark.parametrize("case,vision,blocks,lm", [("model_r50_224_l32", "resnet50", 3, "t5-base"),
+                                                    ("model_r34_256_l16", "resnet34", 3, "t5-base"),
+                                                    ("model_r18_256_l16", "resnet18", 3, "t5-base"),
+                                                    ("model_c5_r50_384_l32", "resnet50", 6, "t5-large")])
+def test_full_step_matches_reference(golden, pkg, case, vision, blocks, lm):
+    """model_c5_*: BASELINE configs[4] widths -- the reference ResnetVQAModel with its
+    width-dependent children rebuilt at 1024 (t5-large encoder, 6 SGA blocks from 1024-wide
+    configuration instances, ConvTranspose2d 2048 -> 1024, pooler and classifier at 1024) and
+    its own forward, at 384 x 384 images (tests/golden/make_golden.py build_model_c5)."""
     g = golden(case)
     B, L, H = int(g["B"]), int(g["L"]), int(g["H"])
     nb = pkg.synthetic.make_batch(B, L, H, seed=1)
@@ -57,8 +70,8 @@ def test_full_step_matches_reference(golden, pkg, case, vision):
     np.testing.assert_array_equal(nb["question_input_ids"], g["ids"])
     np.testing.assert_array_equal(nb["question_attention_masks"], g["mask"])
     np.testing.assert_array_equal(nb["annotation_ids"], g["targets"])
-    sd = pkg.synthetic.make_state_dict(vision, seed=0)
-    tr = orc.OracleTrainer(sd, vision, warmup=int(g["warmup"]), total=int(g["total"]))
+    sd = pkg.synthetic.make_state_dict(vision, seed=0, num_attention_blocks=blocks, language_model=lm)
+    tr = orc.OracleTrainer(sd, vision, warmup=int(g["warmup"]), total=int(g["total"]), num_blocks=blocks)
     batch = orc.to_torch_batch(nb)
     losses, norms, gnorms = [], [], []
     for s in range(len(g["losses"])):
@@ -81,5 +94,5 @@ def test_full_step_matches_reference(golden, pkg, case, vision):
                                g["post_t5_q0"], atol=1e-5, rtol=1e-4)  # Adam step ~5e-3: 0.2% of one update
     np.testing.assert_allclose(sdp["classification_layer.weight"][:4, :16].detach().numpy(), g["post_cls_w"],
                                atol=1e-7, rtol=1e-5)
-    np.testing.assert_allclose(sdp["sga_modules.2.ffn.mlp.fc1.weight"][:4, :16].detach().numpy(),
+    np.testing.assert_allclose(sdp[f"sga_modules.{blocks - 1}.ffn.mlp.fc1.weight"][:4, :16].detach().numpy(),
                                g["post_sga_fc1"], atol=1e-5, rtol=1e-4)

@@ -25,11 +25,12 @@ def cuda():
         pytest.skip("needs a GPU")
 
 
-def _sga_engine(pkg):
-    B, L, H = 2, 32, 224                                     # 7x7 = 49 vision tokens (the fixture's y)
-    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, num_attention_blocks=1)
+def _sga_engine(pkg, lm="t5-base"):
+    # 7x7 = 49 vision tokens (sga_block's y) at 224; 12x12 = 144 (sga1024_block's) at 384
+    B, L, H = 2, 32, (224 if lm == "t5-base" else 384)
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, num_attention_blocks=1, language_model=lm)
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, warmup=2, total=10,
-                               num_blocks=1, dropout=0.0)
+                               num_blocks=1, dropout=0.0, language_model=lm)
     eng.load_batch(pkg.synthetic.make_batch(B, L, H, seed=1))
     eng.forward()
     eng.backward()
@@ -37,11 +38,13 @@ def _sga_engine(pkg):
     return eng
 
 
-def test_sga_block_matches_reference(cuda, pkg, golden, parity_report):
+@pytest.mark.parametrize("case,lm", [("sga_block", "t5-base"), ("sga1024_block", "t5-large")])
+def test_sga_block_matches_reference(cuda, pkg, golden, parity_report, case, lm):
     """SGA block 0 (x = given text, y = given vision tokens) through the HIP kernels:
-    output, dL/dx, dL/dy and every parameter-gradient norm for dL/dout = gout."""
-    g = golden("sga_block")
-    eng = _sga_engine(pkg)
+    output, dL/dx, dL/dy and every parameter-gradient norm for dL/dout = gout.
+    sga1024_block: the reference SGA at config 5's width (1024, 8 heads of 128, 144 keys)."""
+    g = golden(case)
+    eng = _sga_engine(pkg, lm)
     T = eng.T
     x = torch.as_tensor(g["x"]).reshape(T, -1).cuda()
     y = torch.as_tensor(g["y"]).reshape(eng.V_TOK, -1).cuda()
@@ -72,21 +75,22 @@ def test_sga_block_matches_reference(cuda, pkg, golden, parity_report):
     prel = np.abs(pn - ref)[big] / ref[big]
     rep["param_grad_norm_rel_max"] = float(prel.max())
     rep["param_grad_norm_rel"] = dict(zip([n for n, k in zip(names, big) if k], map(float, prel)))
-    parity_report["sga_block"] = rep
+    parity_report[case] = rep
     # bf16 GEMM operands (8 bits of mantissa) through a post-LN block: a few 1e-3 of the range
     assert rep["out_max_rel"] <= 2e-2 and rep["dx_max_rel"] <= 3e-2 and rep["dy_max_rel"] <= 3e-2, rep
     assert rep["param_grad_norm_rel_max"] <= 2e-2, rep
 
 
-def test_t5_encoder_matches_reference(cuda, pkg, golden, parity_report):
-    """T5-base encoder last_hidden_state (eval) through the HIP kernels vs the fixture."""
-    g = golden("t5_encoder")
+@pytest.mark.parametrize("case,lm", [("t5_encoder", "t5-base"), ("t5_large_encoder", "t5-large")])
+def test_t5_encoder_matches_reference(cuda, pkg, golden, parity_report, case, lm):
+    """T5-base / T5-large encoder last_hidden_state (eval) through the HIP kernels vs the fixture."""
+    g = golden(case)
     B, L, H = 2, 32, 32
     nb = pkg.synthetic.make_batch(B, L, H, seed=3)
     np.testing.assert_array_equal(nb["question_input_ids"], g["ids"])
-    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, language_model=lm)
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, warmup=2, total=10,
-                               dropout=0.0)
+                               dropout=0.0, language_model=lm)
     eng.load_batch(nb)
     eng.forward()
     torch.cuda.synchronize()
@@ -94,5 +98,5 @@ def test_t5_encoder_matches_reference(cuda, pkg, golden, parity_report):
     ref = g["hidden"]
     err = float(np.abs(h - ref).max() / np.abs(ref).max())
     cos = float((h * ref).sum() / np.sqrt((h * h).sum() * (ref * ref).sum()))
-    parity_report["t5_encoder"] = {"hidden_max_rel": err, "cosine": cos}
+    parity_report[case] = {"hidden_max_rel": err, "cosine": cos}
     assert err <= 3e-2 and cos >= 0.9995, (err, cos)

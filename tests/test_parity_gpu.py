@@ -28,19 +28,23 @@ def cuda():
         pytest.skip("needs a GPU")
 
 
-@pytest.mark.parametrize("case,vision", [("model_r50_224_l32", "resnet50"), ("model_r34_256_l16", "resnet34"),
-                                          ("model_r18_256_l16", "resnet18")])
-def test_engine_matches_reference_golden(cuda, pkg, golden, parity_report, case, vision):
+@pytest.mark.parametrize("case,vision,blocks,lm", [("model_r50_224_l32", "resnet50", 3, "t5-base"),
+                                                    ("model_r34_256_l16", "resnet34", 3, "t5-base"),
+                                                    ("model_r18_256_l16", "resnet18", 3, "t5-base"),
+                                                    ("model_c5_r50_384_l32", "resnet50", 6, "t5-large")])
+def test_engine_matches_reference_golden(cuda, pkg, golden, parity_report, case, vision, blocks, lm):
     """Three eval-mode steps against the reference's own outputs: log-probs, loss, grad
     norms (total and per group) per step, then the parameters after the three updates
-    (slices and per-group sum |p - p0|, make_golden.py:147-162)."""
+    (slices and per-group sum |p - p0|, make_golden.py:147-162).  model_c5_*: BASELINE
+    configs[4] widths (t5-large, 6 SGA blocks at 1024, 384 x 384 images; make_golden.py
+    build_model_c5), B = 2."""
     g = golden(case)
     B, L, H = int(g["B"]), int(g["L"]), int(g["H"])
-    sd = pkg.synthetic.make_state_dict(vision, seed=0)
+    sd = pkg.synthetic.make_state_dict(vision, seed=0, num_attention_blocks=blocks, language_model=lm)
     nb = pkg.synthetic.make_batch(B, L, H, seed=1)
     # the fixtures are eval-mode (dropout off): the reference's train-mode masks come from torch's RNG
     eng = pkg.engine.VQAEngine(sd, vision=vision, batch=B, seq_len=L, image_size=H, warmup=int(g["warmup"]),
-                               total=int(g["total"]), dropout=0.0)
+                               total=int(g["total"]), dropout=0.0, num_blocks=blocks, language_model=lm)
     losses, norms, gnorms = [], [], []
     lp_err = None
     for s in range(len(g["losses"])):
@@ -60,9 +64,9 @@ def test_engine_matches_reference_golden(cuda, pkg, golden, parity_report, case,
     scaler = "downscale_layer" if vision == "resnet50" else "upscale_layer"
     slices = {"post_t5_q0": post["lang_model.block.0.layer.0.SelfAttention.q.weight"][:4, :16],
               "post_cls_w": post["classification_layer.weight"][:4, :16],
-              "post_sga_fc1": post["sga_modules.2.ffn.mlp.fc1.weight"][:4, :16],
+              "post_sga_fc1": post[f"sga_modules.{blocks - 1}.ffn.mlp.fc1.weight"][:4, :16],
               "post_scaler_w": post[scaler + ".weight"][:4, :4]}
-    init = pkg.synthetic.make_state_dict(vision, seed=0)
+    init = pkg.synthetic.make_state_dict(vision, seed=0, num_attention_blocks=blocks, language_model=lm)
     delta = {k: 0.0 for k in GROUPS}
     for k, v in post.items():
         if k.startswith("vision_model"):
@@ -77,7 +81,7 @@ def test_engine_matches_reference_golden(cuda, pkg, golden, parity_report, case,
         ref = g[name]
         p0 = {"post_t5_q0": init["lang_model.block.0.layer.0.SelfAttention.q.weight"][:4, :16],
               "post_cls_w": init["classification_layer.weight"][:4, :16],
-              "post_sga_fc1": init["sga_modules.2.ffn.mlp.fc1.weight"][:4, :16],
+              "post_sga_fc1": init[f"sga_modules.{blocks - 1}.ffn.mlp.fc1.weight"][:4, :16],
               "post_scaler_w": init[scaler + ".weight"][:4, :4]}[name]
         # relative L2 error of the slice's update vector (p - p0): AdamW's m / sqrt(v) turns
         # the bf16 rounding of near-zero gradients into O(lr) update differences elementwise
@@ -203,7 +207,7 @@ def test_pipelined_resnet_step_is_bit_identical(cuda, pkg):
         assert torch.equal(eng.P32, ref.P32), graph
 
 
-def test_t5_weight_gradient_grouping_is_bit_identical(cuda, pkg, monkeypatch):
+def test_t5_weight_gradient_grouping_is_bit_identical(cuda, pkg):
     """The T5 weight gradients as per-layer paired launches (group 1), batched over groups
     of 4 layers (the DP default) and over all 12 layers (single GPU), and the SGA blocks'
     weight gradients paired per block or batched over the blocks, give the same bits:
@@ -213,16 +217,15 @@ def test_t5_weight_gradient_grouping_is_bit_identical(cuda, pkg, monkeypatch):
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
     nb = pkg.synthetic.make_batch(B, L, H, seed=3)
     grads = []
-    for g, sga in ((1, "0"), (4, "1"), (12, "1"), ((4, 4, 3, 1), "1")):
-        monkeypatch.setenv("VQA_SGA_DW_BATCH", sga)
+    for g, sga in ((1, False), (4, True), (12, True), ((4, 4, 3, 1), True)):
         eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=20, dropout=0.1, seed=1,
-                                   t5_dw_group=g)
+                                   t5_dw_group=g, sga_dw_batch=sga)
         eng.forward_backward(nb)
         grads.append(eng.G32.clone())
     assert all(torch.equal(grads[0], x) for x in grads[1:])
 
 
-def test_deferred_optimizer_update_is_bit_identical(cuda, pkg, monkeypatch):
+def test_deferred_optimizer_update_is_bit_identical(cuda, pkg):
     """AdamW applied inside the next forward (parameter ranges on their own stream, the
     default) == AdamW at the end of the step: same losses, and the same parameters and
     optimizer state once the pending update is flushed; an eval forward between steps
@@ -232,11 +235,11 @@ def test_deferred_optimizer_update_is_bit_identical(cuda, pkg, monkeypatch):
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
     batches = [pkg.synthetic.make_batch(B, L, H, seed=20 + i) for i in range(4)]
     res = []
-    for defer in ("0", "1"):
-        monkeypatch.setenv("VQA_DEFER_OPT", defer)
+    for defer in (False, True):
         for graph in (False, True):
-            eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.1, seed=2)
-            assert eng.defer_opt == (defer == "1")
+            eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.1, seed=2,
+                                       defer_optimizer=defer)
+            assert eng.defer_opt == defer
             losses = []
             for k, nb in enumerate(batches):
                 eng.load_batch(nb)
@@ -258,47 +261,36 @@ def test_deferred_optimizer_update_is_bit_identical(cuda, pkg, monkeypatch):
             assert torch.equal(a, b)
 
 
-def test_folded_rmsnorm_matches_oracle_like_unfolded(cuda, pkg, parity_report, monkeypatch):
-    """VQA_NORM_FOLD=1 (T5 RMSNorm folded into the q|k|v / wi GEMMs, vqa_gemm_desc.rownorm;
-    off by default, measured no faster) against the fp32 oracle: log-probs, loss and grad
-    norm within the golden tolerances, and the T5 weight gradients' relative L2 errors as
-    large as the unfolded engine's on the same step: mean over the 48 tensors within 5 %,
-    each within 35 % (two bf16 evaluations: per-tensor errors at B = 4 are single noisy
-    realisations, measured ratios 0.88-1.21, means 0.0250 vs 0.0249)."""
-    from oracle import vqa_oracle as orc
-    B, L, H, D = 4, 16, 96, 768
-    sd = pkg.synthetic.make_state_dict("resnet34", seed=0)
-    nb = pkg.synthetic.make_batch(B, L, H, seed=1)
-    ot = orc.OracleTrainer(sd, "resnet34", warmup=2, total=10, dropout=0.0)
-    olp, oloss = ot.forward_backward(orc.to_torch_batch(nb))
-    ogn = float(ot.grad_norm())
-    errs = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("VQA_NORM_FOLD", v)
-        e = pkg.engine.VQAEngine(sd, vision="resnet34", batch=B, seq_len=L, image_size=H, warmup=2, total=10,
-                                 dropout=0.0)
-        assert e.norm_fold == (v == "1")
-        lp, loss = e.forward_backward(nb)
-        gn = e.grad_norm()
-        assert float(np.abs(lp - olp.numpy()).max()) <= LP_TOL
-        assert abs(loss - float(oloss)) / abs(float(oloss)) <= LOSS_RTOL
-        assert abs(gn - ogn) / ogn <= GN_RTOL
-        r = {}
-        for i in range(12):
-            p = f"lang_model.block.{i}."
-            for w, ref in (("qkv_w", torch.cat([ot.sd[p + f"layer.0.SelfAttention.{x}.weight"].grad for x in "qkv"])),
-                           ("wi", ot.sd[p + "layer.1.DenseReluDense.wi.weight"].grad),
-                           ("ln0", ot.sd[p + "layer.0.layer_norm.weight"].grad),
-                           ("ln1", ot.sd[p + "layer.1.layer_norm.weight"].grad)):
-                g = e.segment_grad(f"t5.{i}.{w}").cpu().double().reshape(ref.shape)
-                r[f"{i}.{w}"] = float((g - ref.double()).norm() / ref.double().norm())
-        errs[v] = r
-        del e
-    parity_report["norm_fold_vs_unfolded_grad_rel_l2"] = {k: [errs["0"][k], errs["1"][k]] for k in errs["0"]}
-    e0, e1 = np.array(list(errs["0"].values())), np.array([errs["1"][k] for k in errs["0"]])
-    assert e1.mean() <= 1.05 * e0.mean(), (e0.mean(), e1.mean())
-    for k in errs["0"]:
-        assert errs["1"][k] <= 1.35 * errs["0"][k] + 1e-3, (k, errs["0"][k], errs["1"][k])
+def test_dw_stream_matches_single_stream_bitwise(cuda, pkg):
+    """The default single-GPU step runs the side-tagged weight-gradient calls on a stream of
+    their own (dw_stream); every bf16 gradient they read has a private buffer, so the
+    captured step equals the single-stream step bit for bit (losses, log-probs, parameters,
+    optimizer state) over three train-mode steps."""
+    import torch
+    B, L, H = 4, 32, 64
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    batches = [pkg.synthetic.make_batch(B, L, H, seed=40 + i) for i in range(4)]
+    res = []
+    for dws in (True, False):
+        eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.1, seed=3,
+                                   pipeline=True, dw_stream=dws)
+        assert eng.dw_stream == dws
+        imgs = [torch.as_tensor(b["image_tensors"]).cuda() for b in batches]
+        eng.prime(imgs[0])
+        eng.load_batch(batches[0], next_images=imgs[1])
+        eng.capture()
+        eng.prime(imgs[0])
+        losses = []
+        for i in range(3):
+            eng.load_batch(batches[i], next_images=imgs[i + 1])
+            eng.train_step()
+            losses.append(float(eng.LOSS.item()))
+        eng.flush_optimizer()
+        torch.cuda.synchronize()
+        res.append((losses, eng.LOGP.clone(), eng.P32.clone(), eng.M.clone(), eng.VMAX.clone()))
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(a, b)
 
 
 def test_engine_matches_oracle_at_384(cuda, pkg, parity_report):

@@ -8,14 +8,11 @@ same batches and dropout masks, step by step: log-probs, loss, total and per-gro
 grad norms, then the parameters after the updates
 (trainer/faster_rcnn_vqa_trainer.py:391-406).
 
-It runs in a process of its own (tests/bench_step_worker.py), as bench.py does: a
-host SIGSEGV inside hipGraphLaunch was seen on the first replay of this graph
-after 240 other GPU tests in the same process, never in a process of its own.
-The worker is started before this process touches the GPU (this file sorts first
-in the session; the skip check counts devices without initialising them)."""
-import json
+It runs in the session process, after every other GPU test (this file sorts last):
+round 2 saw a host SIGSEGV inside hipGraphLaunch on the first replay of this graph
+late in a session and moved the test into a subprocess; DESIGN.md §3.8 records what
+was found and changed, and this placement is the regression check for it."""
 import os
-import subprocess
 import sys
 
 import pytest
@@ -28,19 +25,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 DELTA_RTOL = 0.1
 
 
-@pytest.fixture(scope="module")
-def gpu():
+def test_bench_step_b64_matches_oracle(parity_report):
     import torch
-    if torch.cuda.device_count() < 1:                     # counts devices without initialising them
+    if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
-
-
-def test_bench_step_b64_matches_oracle(gpu, tmp_path, parity_report):
-    out = str(tmp_path / "bench_step.json")
-    rc = subprocess.run([sys.executable, os.path.join(HERE, "bench_step_worker.py"), out], timeout=140).returncode
-    assert rc == 0, f"bench_step_worker exited with {rc}"
-    res = json.load(open(out))
-    rep, fails = res["report"], res["fails"]
+    sys.path.insert(0, HERE)
+    import bench_step_worker
+    rep, fails = bench_step_worker.run()
     assert rep["splitk_launches"] > 0, "the tuned table should give split-K launches at B=64"
     parity_report["bench_b64"] = rep
     assert not fails, (fails, rep)
