@@ -32,6 +32,7 @@ from __graft_entry__ import load_package  # noqa: E402
 
 FLOP_PER_PAIR = 30.95e9        # fwd+bwd algorithmic FLOPs, R50 @224, L=32
 MFMA_PEAK_TFLOPS = 2517.0      # bf16 dense: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md)
+FP8_PEAK_TFLOPS = 5034.0       # e4m3 dense, block-scaled MFMA (2x the bf16 rate per clock, MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 PMC_FILE = "r02_pmc.json"               # rocprofv3 PMC summary this bench quotes (tools/pmc_step.py)
 
@@ -58,12 +59,15 @@ def cpu_baseline(pkg, batch=64, steps=5, warm=2):
                       f"({t:.2f} s/step), torch CPU {threads} threads"}
 
 
-def calls_flop(eng):
+def calls_flop(eng, fp8_only=False):
     """MFMA work of one step from the engine's prepared calls (GEMMs / implicit-GEMM convs:
-    2 m n k per batch item; attention: 4 lq lk dh forward, 8 backward, per (sample, head))."""
+    2 m n k per batch item; attention: 4 lq lk dh forward, 8 backward, per (sample, head)).
+    fp8_only: the e4m3 GEMMs' share."""
     tot = 0.0
     res = list(eng.res_calls) if eng.pipeline else []           # else they are in fwd_calls
     for c in res + eng.fwd_calls + eng.bwd_calls:
+        if fp8_only and not (c.name == "vqa_gemm" and c.desc.fp8):
+            continue
         if c.name == "vqa_gemm":
             d = c.desc
             tot += 2.0 * d.m * d.n * d.k * max(1, d.batch)
@@ -194,6 +198,9 @@ def main():
     ap.add_argument("--seq-len", type=int, default=32)
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--blocks", type=int, default=3, help="SGA blocks (3: the reference default; 6: BASELINE config 5)")
+    ap.add_argument("--config5", action="store_true",
+                    help="BASELINE configs[4]: ResNet50 + T5-large + 6xSGA at width 1024, 384x384 images, fp8 (e4m3) "
+                         "forward weight GEMMs (per GPU; DP over N GPUs as for config 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-kernel-rooflines", action="store_true", help="skip the per-kernel replays after the timed region")
@@ -235,13 +242,19 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     pkg = load_package()
+    if args.config5:
+        args.image_size, args.blocks = 384, 6
+    lm = "t5-large" if args.config5 else "t5-base"
     B, L, H = args.batch, args.seq_len, args.image_size
     NB = args.blocks
-    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, num_attention_blocks=NB)   # identical init on every rank
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, num_attention_blocks=NB,
+                                       language_model=lm)      # identical init on every rank
     pipe = not args.no_pipeline
+    dp_groups = pkg.dp.dp_t5_dw_groups(pkg.synthetic.lm_dims(lm).t5_layers)
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev, num_blocks=NB,
                                warmup=10, total=100000, dropout=0.1, seed=rank, pipeline=pipe,
-                               t5_dw_group=None if world == 1 else pkg.dp.DP_T5_DW_GROUPS)
+                               t5_dw_group=None if world == 1 else dp_groups, language_model=lm,
+                               fp8=args.config5)
     del sd
     pool = []
     for i in range(4):
@@ -317,26 +330,34 @@ def main():
     # the replay stream over the timed region; traffic = HBM bytes per step from the
     # committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes over every dispatch of one step.
     # Other shapes (--image-size / --seq-len): the MFMA work of the prepared calls.
-    survey_cfg = (args.image_size, args.seq_len, NB) == (224, 32, 3)
+    survey_cfg = (args.image_size, args.seq_len, NB) == (224, 32, 3) and not args.config5
     step_flop = FLOP_PER_PAIR * B if survey_cfg else calls_flop(eng)
     step_tflops = step_flop / gpu_step / 1e12
     st = pmc.get("step", {}) if survey_cfg else {}
-    roofline = {"bound": "mfma", "kernel": f"whole train step (one hipGraph replay: ResNet50 fwd, ConvT, T5, {NB}xSGA, "
+    # config 5 mixes e4m3 (forward weight GEMMs) and bf16 MFMA work: the peak is the rate at which
+    # the step's FLOP mix would run with every launch at its dtype's dense peak
+    f8 = calls_flop(eng, fp8_only=True)
+    peak = MFMA_PEAK_TFLOPS if f8 == 0 else calls_flop(eng) / (f8 / FP8_PEAK_TFLOPS + (calls_flop(eng) - f8) /
+                                                               MFMA_PEAK_TFLOPS)
+    roofline = {"bound": "mfma", "kernel": f"whole train step (one hipGraph replay: ResNet50 fwd, ConvT, {lm}, {NB}xSGA, "
                                            "head, backward, clip, AdamW)",
-                "achieved": round(step_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(step_tflops / MFMA_PEAK_TFLOPS, 4),
+                "achieved": round(step_tflops, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(step_tflops / peak, 4),
+                **({"fp8_flop_per_step": f8, "peak_note": "e4m3 FLOPs at 5034, bf16 FLOPs at 2517 TFLOP/s"} if f8 else {}),
                 "traffic": round(st["traffic_bytes"]) if "traffic_bytes" in st else None,
                 "flop_per_step": step_flop, "flop_per_step_calls": calls_flop(eng),
                 "step_gpu_ms": round(gpu_step * 1e3, 4),
                 "traffic_source": f"profiles/{PMC_FILE} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, all dispatches of one step)"}
     out = {
-        "metric": "question-image pairs/sec, ResNet50+T5-base+SGA train step, 1/2/4/8 MI355X",
+        "metric": ("question-image pairs/sec, ResNet50+T5-large+6xSGA 384x384 fp8-weight train step (BASELINE configs[4])"
+                   if args.config5 else "question-image pairs/sec, ResNet50+T5-base+SGA train step, 1/2/4/8 MI355X"),
         "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-        "config": {"workload": (f"ResNet50 + T5-base + {NB}xSGA train step"
-                                + (" (BASELINE configs[1]; configs[2] at N=8)" if survey_cfg else "")),
-                   "model": f"resnet50+t5-base+{NB}xSGA", "global_batch": world * B, "per_gpu_batch": B,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp8+bf16" if args.config5 else "bf16", "data": "synthetic",
+        "config": {"workload": (f"ResNet50 + {lm} + {NB}xSGA train step"
+                                + (" (BASELINE configs[1]; configs[2] at N=8)" if survey_cfg else "")
+                                + (" (BASELINE configs[4]: e4m3 forward weight GEMMs)" if args.config5 else "")),
+                   "model": f"resnet50+{lm}+{NB}xSGA", "global_batch": world * B, "per_gpu_batch": B,
                    "seq_len": L, "image_size": H, "answers": 170, "parallelism": f"dp{world}",
                    "world_size": (dist.get_world_size() if dist else 1), "graph": not args.no_graph,
                    "resnet_pipelined": pipe},

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 12
+#define VQA_ABI_VERSION 13
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -128,6 +128,18 @@ typedef struct vqa_gemm_desc {
    * A k-contiguous, no implicit im2col, no split-K, batch 1. */
   int rownorm;
   float rownorm_eps;
+  /* fp8 != 0: e4m3 (OCP float8_e4m3fn) operands for the forward weight GEMMs of BASELINE
+   * configs[4] ("fp8 MFMA weights"): a = X8 [m][k] bytes (lda in bytes), b = W8 [n][k] bytes
+   * (a_trans = b_trans = 0), both row-wise quantised by vqa_quant_rows_fp8; the accumulator
+   * is scaled by scale_a[z*stride_scale_a + row] * scale_b[z*stride_scale_b + col] before the
+   * epilogue (bias / residual / ReLU / dropout as usual).  k and lda / ldb multiples of 16,
+   * n % 4 == 0, no conv operand, no rownorm, no GELU / tanh.  Products of e4m3 values are
+   * exact in fp32, so the result differs from an fp32 GEMM of the dequantised operands only
+   * by accumulation order. */
+  int fp8;
+  const float* scale_a;
+  const float* scale_b;
+  long long stride_scale_a, stride_scale_b;
 } vqa_gemm_desc;
 
 /* tile configs: 1 128x128/3 stages, 2 128x64/4, 3 64x64/4, 4 64x64/2, 5 64x64/3, 6 128x64/2,
@@ -138,6 +150,11 @@ typedef struct vqa_gemm_desc {
 #define VQA_GEMM_PATCH_FIRST 17    /* configs 17..20: a_conv = 2 only */
 #define VQA_GEMM_PATCH_LAST 20
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
+/* Row-wise e4m3 quantisation for vqa_gemm_desc.fp8: per row r of x (fp32, or bf16 when
+ * x_bf16), scale[r] = max_c |x[r][c]| / 448 (1 for an all-zero row) and
+ * q[r][c] = e4m3(x[r][c] / scale[r]) (round to nearest even).  cols, ldx, ldq multiples of 8. */
+int vqa_quant_rows_fp8(const void* x, int x_bf16, long long ldx, int rows, int cols, void* q, long long ldq,
+                       float* scale, hipStream_t stream);
 /* tile configuration (1..VQA_GEMM_CONFIGS) that vqa_gemm would run for this descriptor */
 int vqa_gemm_select(const vqa_gemm_desc* d);
 /* workspace bytes vqa_gemm needs for d (its config and splitk; 0 when splitk <= 1) */

@@ -97,6 +97,41 @@ def _nodrop(site, x):
     return x
 
 
+# --------------------------------------------------------------------------- fp8 (config 5)
+# BASELINE configs[4] trains with "fp8 MFMA weights": the engine's forward weight GEMMs of the
+# T5 layers and SGA blocks take row-wise e4m3 quantisations of the bf16 activation and of the
+# fp32 weight (scale = row amax / 448, round to nearest even; include/vqa_hip.h
+# vqa_quant_rows_fp8), the backward the unquantised operands.  No reference path computes in
+# fp8, so this is the restatement of that arithmetic the fp8 engine is checked against, and
+# the fp32 oracle (fp8=False) measures what the quantisation costs.
+def fp8_rows(x):
+    """Row-wise e4m3 quantise-dequantise (torch.float8_e4m3fn rounds to nearest even)."""
+    amax = x.abs().amax(-1, keepdim=True)
+    s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    return (x / s).to(torch.float8_e4m3fn).float() * s
+
+
+class _Fp8Matmul(torch.autograd.Function):
+    """y = q(bf16(x)) q(w)^T; dx = dy w, dw = dy^T x (unquantised operands, as the engine)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return fp8_rows(x.bfloat16().float()) @ fp8_rows(w).T
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dy @ w
+        dw = dy.reshape(-1, dy.shape[-1]).T @ x.reshape(-1, x.shape[-1])
+        return dx, dw
+
+
+def _mm(x, w, fp8=False):
+    """x @ w^T (a Linear without bias), or its fp8 form."""
+    return _Fp8Matmul.apply(x, w) if fp8 else x @ w.T
+
+
 # --------------------------------------------------------------------------- ResNet
 def _bn_eval(x, sd, p):
     """Frozen BatchNorm2d in eval mode (resnet_vqa_model.py:127 `vision_model.eval()`)."""
@@ -163,7 +198,7 @@ def t5_rmsnorm(h, w):
     return w * (h * torch.rsqrt(var + T5_EPS))
 
 
-def t5_encoder(sd, ids, mask, prefix="lang_model.", drop=_nodrop):
+def t5_encoder(sd, ids, mask, prefix="lang_model.", drop=_nodrop, fp8=False):
     """T5Stack encoder forward (modeling_t5.py:640-751), called from
     resnet_vqa_model.py:137-140.  Returns last_hidden_state [B, L, 768].
     `drop` applies the train-mode dropouts (identity = eval mode)."""
@@ -179,54 +214,54 @@ def t5_encoder(sd, ids, mask, prefix="lang_model.", drop=_nodrop):
     for i in range(nl):
         p = f"block.{i}.layer."
         n = t5_rmsnorm(h, g(p + "0.layer_norm.weight"))                # T5LayerSelfAttention :384-401
-        q = (n @ g(p + "0.SelfAttention.q.weight").T).view(B, L, nh, dkv).transpose(1, 2)
-        k = (n @ g(p + "0.SelfAttention.k.weight").T).view(B, L, nh, dkv).transpose(1, 2)
-        v = (n @ g(p + "0.SelfAttention.v.weight").T).view(B, L, nh, dkv).transpose(1, 2)
+        q = _mm(n, g(p + "0.SelfAttention.q.weight"), fp8).view(B, L, nh, dkv).transpose(1, 2)
+        k = _mm(n, g(p + "0.SelfAttention.k.weight"), fp8).view(B, L, nh, dkv).transpose(1, 2)
+        v = _mm(n, g(p + "0.SelfAttention.v.weight"), fp8).view(B, L, nh, dkv).transpose(1, 2)
         s = q @ k.transpose(2, 3)                                      # no 1/sqrt(d) (scaling = 1.0)
         s = s + bias + ext
         a = drop(t5_site(i, 0), torch.softmax(s.float(), dim=-1))     # :168
         o = (a @ v).transpose(1, 2).reshape(B, L, nh * dkv)
-        h = h + drop(t5_site(i, 1), o @ g(p + "0.SelfAttention.o.weight").T)     # :400
+        h = h + drop(t5_site(i, 1), _mm(o, g(p + "0.SelfAttention.o.weight"), fp8))     # :400
         n = t5_rmsnorm(h, g(p + "1.layer_norm.weight"))                # T5LayerFF :126-141
-        f = drop(t5_site(i, 2), F.relu(n @ g(p + "1.DenseReluDense.wi.weight").T))  # :86
-        h = h + drop(t5_site(i, 3), f @ g(p + "1.DenseReluDense.wo.weight").T)    # :140
+        f = drop(t5_site(i, 2), F.relu(_mm(n, g(p + "1.DenseReluDense.wi.weight"), fp8)))  # :86
+        h = h + drop(t5_site(i, 3), _mm(f, g(p + "1.DenseReluDense.wo.weight"), fp8))    # :140
     return drop(SITE_FINAL, t5_rmsnorm(h, g("final_layer_norm.weight")))         # :745
 
 
 # --------------------------------------------------------------------------- SGA
-def _linear(x, sd, p):
-    return x @ sd[p + ".weight"].T + sd[p + ".bias"]
+def _linear(x, sd, p, fp8=False):
+    return _mm(x, sd[p + ".weight"], fp8) + sd[p + ".bias"]
 
 
-def sga_mhatt(sd, p, v, k, q, drop=_nodrop, site=0):
+def sga_mhatt(sd, p, v, k, q, drop=_nodrop, site=0, fp8=False):
     """MHAtt.forward + att (multi_head_vision_text_attn.py:38-86), mask=None.  MULTI_HEAD = 8
     heads of HIDDEN_SIZE / 8 (96 at the reference's 768, 128 at config 5's 1024)."""
     B = q.shape[0]
     dh = sd[p + ".linear_q.weight"].shape[0] // SGA_HEADS
-    V = _linear(v, sd, p + ".linear_v").view(B, -1, SGA_HEADS, dh).transpose(1, 2)
-    K = _linear(k, sd, p + ".linear_k").view(B, -1, SGA_HEADS, dh).transpose(1, 2)
-    Q = _linear(q, sd, p + ".linear_q").view(B, -1, SGA_HEADS, dh).transpose(1, 2)
+    V = _linear(v, sd, p + ".linear_v", fp8).view(B, -1, SGA_HEADS, dh).transpose(1, 2)
+    K = _linear(k, sd, p + ".linear_k", fp8).view(B, -1, SGA_HEADS, dh).transpose(1, 2)
+    Q = _linear(q, sd, p + ".linear_q", fp8).view(B, -1, SGA_HEADS, dh).transpose(1, 2)
     s = (Q @ K.transpose(-2, -1)) / math.sqrt(dh)
     a = drop(site, torch.softmax(s, dim=-1))                          # :83-84
     o = (a @ V).transpose(1, 2).contiguous().view(B, -1, SGA_HEADS * dh)
-    return _linear(o, sd, p + ".linear_merge")
+    return _linear(o, sd, p + ".linear_merge", fp8)
 
 
 def _layernorm(x, sd, p):
     return F.layer_norm(x, (x.shape[-1],), sd[p + ".norm.weight"], sd[p + ".norm.bias"], LN_EPS)
 
 
-def sga_block(sd, p, x, y, drop=_nodrop, block=0):
+def sga_block(sd, p, x, y, drop=_nodrop, block=0, fp8=False):
     """SGA.forward (multi_head_vision_text_attn.py:145-158): post-LN; `drop` = train-mode dropouts."""
     st = lambda kind: sga_site(block, kind)
-    x = _layernorm(x + drop(st(1), sga_mhatt(sd, p + ".mhatt1", x, x, x, drop, st(0))), sd, p + ".norm1")
-    x = _layernorm(x + drop(st(3), sga_mhatt(sd, p + ".mhatt2", y, y, x, drop, st(2))), sd, p + ".norm2")
-    f = _linear(drop(st(4), F.relu(_linear(x, sd, p + ".ffn.mlp.fc1"))), sd, p + ".ffn.mlp.fc2")   # MLP :97-101
+    x = _layernorm(x + drop(st(1), sga_mhatt(sd, p + ".mhatt1", x, x, x, drop, st(0), fp8)), sd, p + ".norm1")
+    x = _layernorm(x + drop(st(3), sga_mhatt(sd, p + ".mhatt2", y, y, x, drop, st(2), fp8)), sd, p + ".norm2")
+    f = _linear(drop(st(4), F.relu(_linear(x, sd, p + ".ffn.mlp.fc1", fp8))), sd, p + ".ffn.mlp.fc2", fp8)  # :97-101
     return _layernorm(x + drop(st(5), f), sd, p + ".norm3")
 
 
 # --------------------------------------------------------------------------- full model
-def model_forward(sd, batch, vision="resnet50", num_blocks=3, return_features=False, drop=_nodrop):
+def model_forward(sd, batch, vision="resnet50", num_blocks=3, return_features=False, drop=_nodrop, fp8=False):
     """ResnetVQAModel.forward (resnet_vqa_model.py:101-165); eval mode unless
     `drop` (a HashDropout) supplies train-mode dropout.
     Returns (log_probs [B, A], loss scalar or None)."""
@@ -234,11 +269,11 @@ def model_forward(sd, batch, vision="resnet50", num_blocks=3, return_features=Fa
         feat = resnet_features(sd, batch["image_tensors"], vision)
     scaler = "downscale_layer" if vision == "resnet50" else "upscale_layer"
     vis = F.conv_transpose2d(feat, sd[scaler + ".weight"], sd[scaler + ".bias"], stride=1, padding=1)
-    txt = t5_encoder(sd, batch["question_input_ids"], batch["question_attention_masks"], drop=drop)
+    txt = t5_encoder(sd, batch["question_input_ids"], batch["question_attention_masks"], drop=drop, fp8=fp8)
     y = vis.view(vis.shape[0], vis.shape[1], -1).permute(0, 2, 1)      # :142-143
     fused = None
     for n in range(num_blocks):                                        # :147-149 (Q4)
-        fused = sga_block(sd, f"sga_modules.{n}", txt, y, drop, n)
+        fused = sga_block(sd, f"sga_modules.{n}", txt, y, drop, n, fp8)
         y = fused
     w = sd["attention_pooler.attention.0.weight"]                      # AttentionPooler :14-26
     a = torch.softmax(fused @ w.T + sd["attention_pooler.attention.0.bias"], dim=1)
@@ -286,8 +321,9 @@ class OracleTrainer:
     """zero_grad -> fwd -> bwd -> clip_grad_norm_(1.0) -> AdamW(amsgrad) -> sched
     (faster_rcnn_vqa_trainer.py:391-406), all restated in fp32 on the CPU."""
 
-    def __init__(self, sd, vision="resnet50", warmup=10, total=100, num_blocks=3, dropout=0.0, seed=0):
+    def __init__(self, sd, vision="resnet50", warmup=10, total=100, num_blocks=3, dropout=0.0, seed=0, fp8=False):
         self.vision, self.warmup, self.total, self.num_blocks = vision, warmup, total, num_blocks
+        self.fp8 = bool(fp8)
         self.dropout, self.seed, self.rng_counter = float(dropout), int(seed), 0
         self.sd = OrderedDict((k, torch.as_tensor(v).clone()) for k, v in sd.items())
         self.keys = trainable_keys(self.sd, vision)
@@ -305,7 +341,7 @@ class OracleTrainer:
         if self.dropout > 0.0:                     # one draw per forward, like the engine's rng advance
             self.rng_counter += 1
             drop = HashDropout(self.dropout, self.seed, self.rng_counter)
-        lp, loss = model_forward(self.sd, batch, self.vision, self.num_blocks, drop=drop)
+        lp, loss = model_forward(self.sd, batch, self.vision, self.num_blocks, drop=drop, fp8=self.fp8)
         loss.backward()
         return lp.detach(), loss.detach()
 

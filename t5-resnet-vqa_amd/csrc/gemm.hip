@@ -22,229 +22,9 @@
 // matrix / conv padding read a 16-B zero page instead (no predication).
 // Block ids are remapped so that blocks sharing an XCD (b % 8) get a
 // contiguous range of tiles (bijective form, cdna_hip_programming.md §5).
-#include "gemm_common.h"
-
-// diagnostic phase stamps (tools/micro/gemm_stamps.hip defines it; a no-op in the library)
-#ifndef VQA_GEMM_STAMP
-#define VQA_GEMM_STAMP(i)
-#endif
+#include "gemm_body.h"
 
 namespace {
-
-template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, bool EXT = false,
-          int BKT = BK>
-__device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, char* smem) {
-  constexpr int NW = NWM * NWN, NT = 64 * NW;
-  constexpr int WM = BM / NWM, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
-  static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "wave sub-tile must be whole 32x32 blocks");
-  constexpr int A_BYTES = BM * BKT * 2, B_BYTES = BN * BKT * 2, ST_BYTES = A_BYTES + B_BYTES;
-  using LA = Loader<BM, AKC, GA, NW, BKT>;
-  using LB = Loader<BN, BKC, GB, NW, BKT>;
-  constexpr int NL = LA::NI + LB::NI;                 // glds instructions per thread per K-tile
-
-  // XCD-aware bijective remap of the linear block id; with split-K the slices of
-  // one tile are consecutive ids, i.e. (mostly) on one XCD, next to their reducer
-  const int S = P.splitk > 1 ? P.splitk : 1;
-  const int ntile = P.tiles_m * P.tiles_n;
-  const int nwg = ntile * S;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = wg / S, slice = wg - tile * S;
-  int tm = tile / P.tiles_n, tn = tile - tm * P.tiles_n;
-  if constexpr (GB) {
-    // implicit-im2col B (ConvTranspose2d dW: column = tap * C + c): order the tiles channel
-    // block first, so the consecutive tiles an XCD gets are every tap and row tile of ONE
-    // channel block -- the 9 taps re-read that slice of the layer4 map from this XCD's L2
-    // instead of fetching the whole map 9 times from the Infinity Cache / HBM
-    const int cb = P.gb.c / BN;
-    if (cb > 0 && P.gb.c % BN == 0 && P.tiles_n % cb == 0) {
-      const int taps = P.tiles_n / cb, per = P.tiles_m * taps;
-      const int cblk = tile / per, r = tile - cblk * per;
-      tm = r / taps;
-      tn = (r - tm * taps) * cb + cblk;
-    }
-  }
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  const int z = blockIdx.z;
-  const bf16_t* A = P.a + (long)z * P.sa;
-  const bf16_t* B = P.b + (long)z * P.sb;
-
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int wm = w / NWN, wn = w % NWN;
-
-  VQA_GEMM_STAMP(0);
-  LA la;
-  LB lb;
-  la.init(m0, P.m, P.lda, P.ga);
-  lb.init(n0, P.n, P.ldb, P.gb);
-  using FA = FragAddr<BM, AKC, TM, BKT>;
-  using FB = FragAddr<BN, BKC, TN, BKT>;
-  FA fra;
-  FB frb;
-  fra.init(wm * WM);
-  frb.init(wn * WN);
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-
-  f32x16_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  // rownorm: this lane's share of sum_k A[row]^2 for its fragment rows (row l&31 of block i;
-  // lanes l and l^32 see the two 8-wide halves of every 16-deep k-step)
-  float sq[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) sq[i] = 0.f;
-  const bool rown = AKC && !GA && P.rownorm;
-
-  const int nk_all = (P.k + BKT - 1) / BKT;
-  const int kb = S > 1 ? slice * P.kper : 0;                  // this slice's first k-tile
-  const int nk = S > 1 ? min(nk_all - kb, P.kper) : nk_all;   // >= 1 (host checks)
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s) {
-    if (s < nk) {
-      la.issue(A, P.lda, smem + s * ST_BYTES, (kb + s) * BKT, P.k, P.ga);
-      lb.issue(B, P.ldb, smem + s * ST_BYTES + A_BYTES, (kb + s) * BKT, P.k, P.gb);
-    }
-  }
-  VQA_GEMM_STAMP(1);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = min(nk - 1, kt + STAGES - 2) - kt;
-    wait_tiles<NL, STAGES>(ahead);
-    barrier();
-    if (kt == 0) VQA_GEMM_STAMP(2);
-    const int nt = kt + STAGES - 1;
-    if (nt < nk) {
-      char* st = smem + (nt % STAGES) * ST_BYTES;
-      la.issue(A, P.lda, st, (kb + nt) * BKT, P.k, P.ga);
-      lb.issue(B, P.ldb, st + A_BYTES, (kb + nt) * BKT, P.k, P.gb);
-    }
-    const uint32_t cur = lds0 + (kt % STAGES) * ST_BYTES;
-    constexpr int R = FA::READS + FB::READS;
-    i32x4_t fa[2][TM], fb[2][TN];
-    fra.read(cur, 0, fa[0]);
-    frb.read(cur + A_BYTES, 0, fb[0]);
-#pragma unroll
-    for (int s = 0; s < BKT / 16; ++s) {
-      if (s + 1 < BKT / 16) {
-        fra.read(cur, s + 1, fa[(s + 1) & 1]);
-        frb.read(cur + A_BYTES, s + 1, fb[(s + 1) & 1]);
-        wait_lgkm<R>();
-      } else {
-        wait_lgkm<0>();
-      }
-      if (rown) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint32_t u = (uint32_t)fa[s & 1][i][q];
-            const float lo = __uint_as_float(u << 16), hi = __uint_as_float(u & 0xffff0000u);
-            sq[i] = fmaf(lo, lo, fmaf(hi, hi, sq[i]));
-          }
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          // swapped operands: D = B^T-tile x A^T-tile, so a lane owns one output ROW and
-          // 4 consecutive output COLUMNS per register group (vectorised epilogue)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, fb[s & 1][j]),
-                                                              __builtin_bit_cast(bf16x8_t, fa[s & 1][i]),
-                                                              acc[i][j], 0, 0, 0);
-    }
-  }
-
-  if (S > 1) {
-    // Split-K hand-off (cdna_hip_programming.md Guideline 16, R1 form): every slice
-    // stores its partials WRITE-THROUGH (sc1 buffer stores, 1 KiB contiguous per wave
-    // store, fragment order), every storing wave drains, then one lane counts the
-    // arrival with a relaxed agent-scope atomic.  The slice that arrives last reads
-    // the other slices' partials with sc1 loads (no release/acquire fences needed)
-    // and sums all slices IN SLICE ORDER, its own from registers -- the result does
-    // not depend on arrival order.  No workgroup waits on another (nothing can
-    // hang); the reducer resets the counter for the next launch.
-    typedef __attribute__((address_space(1))) unsigned gu32;
-    constexpr int FR = TM * TN * 1024;                  // floats per wave
-    const long tlin = (long)z * ntile + tile;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(P.slab + tlin * S * (long)(BM * BN), (short)0, S * BM * BN * 4, 0x00020000);
-    const int wof = w * FR + l * 4;                     // this lane's float offset inside a slice
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const i32x4_t v = {__float_as_int(acc[i][j][4 * g]), __float_as_int(acc[i][j][4 * g + 1]),
-                             __float_as_int(acc[i][j][4 * g + 2]), __float_as_int(acc[i][j][4 * g + 3])};
-          __builtin_amdgcn_raw_buffer_store_b128(v, rs, (slice * (BM * BN) + wof + (i * TN + j) * 1024 + g * 256) * 4,
-                                                 0, 16);
-        }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // EVERY storing wave drains its sc1 stores
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);           // the ring is idle (the K loop drained every DMA)
-    if (tid == 0) {
-      gu32* c = (gu32*)(P.cnt + tlin);
-      const unsigned prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = prev == (unsigned)(S - 1);
-      if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = last;
-    }
-    __syncthreads();
-    if (!*flag) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        f32x16_t t;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) t[e] = 0.f;
-        for (int s = 0; s < S; ++s) {
-          if (s == slice) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) t[e] += acc[i][j][e];
-          } else {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const i32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(
-                  rs, (s * (BM * BN) + wof + (i * TN + j) * 1024 + g * 256) * 4, 0, 16);
-              t[4 * g] += __int_as_float(v[0]);
-              t[4 * g + 1] += __int_as_float(v[1]);
-              t[4 * g + 2] += __int_as_float(v[2]);
-              t[4 * g + 3] += __int_as_float(v[3]);
-            }
-          }
-        }
-        acc[i][j] = t;
-      }
-  }
-
-  if (rown) {                                          // the RMSNorm row scale (no split-K: host check)
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float t = sq[i] + __shfl_xor(sq[i], 32);
-      const float r = rsqrtf(t / (float)P.k + P.rn_eps);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] *= r;
-    }
-  }
-  VQA_GEMM_STAMP(3);
-  tile_epilogue<BM, BN, STAGES, NWM, NWN, EXT, BKT>(P, acc, z, m0, n0, P.m, smem);
-  VQA_GEMM_STAMP(4);
-}
-
-template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, int BKT = BK>
-__global__ __launch_bounds__(64 * NWM * NWN) void gemm_kernel(GemmParams P) {
-  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<BM, BN, STAGES, BKT>::LDS];
-  gemm_body<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB, false, BKT>(P, blockIdx.x, smem);
-}
 
 // GELU / tanh epilogues (vqa_gemm_desc.relu 2 / 3: the ViT intermediate and pooler of
 // config 4) in ONE tile config (64x128, 2 stages, k-contiguous A and B = X W^T), so the
@@ -271,33 +51,6 @@ __global__ __launch_bounds__(256) void gemm_pair_kernel(GemmParams P1, GemmParam
   } else if (bid >= t1pad) {
     gemm_body<BM2, BN2, S2, 2, 2, false, false, false, false>(P2, bid - t1pad, smem);   // dW: both m/n-contig
   }
-}
-
-// split-K workspace: a fixed 64 KiB counter block first (so any sequence of calls
-// sharing a workspace only ever finds zeros there), then the slabs
-constexpr long long SPLITK_CNT_BYTES = 65536;
-constexpr long long SPLITK_MAX_TILES = SPLITK_CNT_BYTES / 4;
-long long splitk_bytes(int bm, int bn, int m, int n, int batch, int S) {
-  if (S <= 1) return 0;
-  const long long tiles = (long long)vqa::cdiv(m, bm) * vqa::cdiv(n, bn) * batch;
-  return SPLITK_CNT_BYTES + tiles * S * bm * bn * 4;
-}
-
-template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, int BKT = BK>
-int launch(GemmParams& P, int batch, hipStream_t s) {
-  if (BKT != BK && P.splitk > 1)                        // split-K slices are counted in 64-deep k-tiles
-    return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: 128-deep k-tile configs take no split-K");
-  P.tiles_m = vqa::cdiv(P.m, BM);
-  P.tiles_n = vqa::cdiv(P.n, BN);
-  if (P.splitk > 1) {                                   // workspace = [counters | slabs]
-    const long long tiles = (long long)P.tiles_m * P.tiles_n * batch;
-    if (tiles > SPLITK_MAX_TILES) return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: split-K needs <= %lld tiles", SPLITK_MAX_TILES);
-    P.cnt = reinterpret_cast<unsigned*>(P.slab);
-    P.slab = reinterpret_cast<float*>(reinterpret_cast<char*>(P.slab) + SPLITK_CNT_BYTES);
-  }
-  dim3 grid(P.tiles_m * P.tiles_n * (P.splitk > 1 ? P.splitk : 1), 1, batch);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB, BKT>), grid, dim3(64 * NWM * NWN), 0, s, P);
-  return vqa::check_launch("vqa_gemm");
 }
 
 // config: 0 = auto; 1 = 128x128 (3 stages); 2 = 128x64 (4); 3 = 64x64 (4); 4 = 64x64 (2);
@@ -409,7 +162,7 @@ extern "C" long long vqa_gemm_workspace_bytes(const vqa_gemm_desc* d) {
   if (!d || d->splitk <= 1 || d->a_conv == 2) return 0;
   int bm, bn, kper;
   tile_of(vqa_gemm_select(d), bm, bn);
-  const int S = effective_splitk(d->k, d->splitk, &kper);
+  const int S = effective_splitk(d->fp8 ? d->k / 2 : d->k, d->splitk, &kper);   // fp8: k in 2-byte units
   return splitk_bytes(bm, bn, d->m, d->n, d->batch < 1 ? 1 : d->batch, S);
 }
 
@@ -452,6 +205,27 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
               "vqa_gemm: rownorm needs a k-contiguous plain A, no split-K, batch 1 and eps > 0");
   P.rownorm = d->rownorm;
   P.rn_eps = d->rownorm_eps;
+  P.qsa = P.qsb = nullptr;
+  P.sqa = P.sqb = 0;
+  if (d->fp8) {
+    // e4m3 operands: bytes, staged by the bf16 loaders as 2-byte units (128 fp8 per 64-unit k-tile)
+    VQA_REQUIRE(!d->a_trans && !d->b_trans && !d->a_conv && !d->b_conv && !d->rownorm && d->relu <= 1,
+                "vqa_gemm(fp8): k-contiguous A and B, no conv operand, no rownorm, ReLU at most");
+    VQA_REQUIRE(d->k % 16 == 0 && d->lda % 16 == 0 && d->ldb % 16 == 0 && d->stride_a % 2 == 0 &&
+                    d->stride_b % 2 == 0 && d->n % 4 == 0,
+                "vqa_gemm(fp8): k, lda, ldb multiples of 16 bytes, even strides, n %% 4 == 0");
+    VQA_REQUIRE(d->scale_a && d->scale_b && aligned16(d->scale_b) && d->stride_scale_b % 4 == 0,
+                "vqa_gemm(fp8): row scales of A and B (scale_b 16-byte aligned)");
+    P.k = d->k / 2;
+    P.lda = d->lda / 2;
+    P.ldb = d->ldb / 2;
+    P.sa = d->stride_a / 2;
+    P.sb = d->stride_b / 2;
+    P.qsa = d->scale_a;
+    P.qsb = d->scale_b;
+    P.sqa = d->stride_scale_a;
+    P.sqb = d->stride_scale_b;
+  }
   P.splitk = 1;
   P.kper = 0;
   P.slab = nullptr;
@@ -459,7 +233,7 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
   VQA_REQUIRE(d->splitk >= 0 && d->splitk <= 64, "vqa_gemm: splitk must be 0..64");
   if (d->splitk > 1) {
     int kper;
-    const int S = effective_splitk(d->k, d->splitk, &kper);
+    const int S = effective_splitk(P.k, d->splitk, &kper);
     if (S > 1) {
       const long long need = vqa_gemm_workspace_bytes(d);
       VQA_REQUIRE(d->workspace && aligned16(d->workspace), "vqa_gemm: splitk needs a 16-byte aligned workspace");
@@ -481,10 +255,13 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
 }
 
 #ifndef VQA_GEMM_MICRO
+int vqa_gemm_fp8_dispatch(void* P, int batch, int config, hipStream_t s);   // gemm_fp8.hip
+
 extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   GemmParams P;
   if (int rc = prepare(d, P)) return rc;
   const int batch = d->batch, cfg = d->config;
+  if (d->fp8) return vqa_gemm_fp8_dispatch(&P, batch, cfg, stream);
   const bool akc = !d->a_trans, bkc = !d->b_trans;
   const bool patch_cfg = cfg >= VQA_GEMM_PATCH_FIRST && cfg <= VQA_GEMM_PATCH_LAST;
   if (d->a_conv == 2) {                                   // LDS-patch 3x3 convolution (conv_patch.inl)

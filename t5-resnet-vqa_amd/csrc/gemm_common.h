@@ -35,6 +35,10 @@ struct GemmParams {
   int dsite;               // != 0: batch z uses dropout site + z*dsite, element indices from 0
   int rownorm;             // scale output rows by rsqrt(mean_k(A^2) + rn_eps) (vqa_gemm_desc.rownorm)
   float rn_eps;
+  // fp8 (e4m3) operands (vqa_gemm_desc.fp8): a / b hold bytes (lda, ldb, k, sa, sb in units of
+  // 2 bytes, so the bf16 loaders stage them unchanged); acc(m, n) is scaled by qsa[m] * qsb[n]
+  const float* qsa; const float* qsb;
+  long sqa, sqb;           // scale strides per batch element
 };
 
 // byte offset of 16-B chunk `ch` of row `row` in a k-contig image ([rows][BKT bf16]):
@@ -264,6 +268,35 @@ struct FragAddr {
     }
   }
   static constexpr int READS = KC ? T : 2 * T;
+};
+
+// Per-lane LDS byte offsets of one e4m3 operand's fragments for the 64-deep scaled MFMA
+// (v_mfma_scale_f32_32x32x64_f8f6f4): a 128-B k-contig image row holds 128 fp8 = two steps;
+// lane l reads row l&31, 32 contiguous bytes = chunks 4t + 2(l>>5) and +1 of step t.  Both
+// operands use the same lane -> k map, so the products are summed over the same k whatever
+// order the instruction assigns inside a step.
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+template <int T, int BKT = BK>
+struct FragAddr8 {
+  static constexpr int STEPS = BKT / 32;                  // 64-deep fp8 steps per k-tile
+  uint32_t o[STEPS][2];
+  __device__ __forceinline__ void init(int row_base) {
+    const int l = threadIdx.x & 63;
+    const int row = row_base + (l & 31);
+#pragma unroll
+    for (int t = 0; t < STEPS; ++t)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) o[t][c] = kc_off_t<BKT>(row, 4 * t + 2 * (l >> 5) + c);
+  }
+  __device__ __forceinline__ void read(uint32_t base, int t, i32x8_t (&f)[T]) const {
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+      const i32x4_t lo = ds_b128(base + o[t][0] + i * 32 * (BKT * 2));
+      const i32x4_t hi = ds_b128(base + o[t][1] + i * 32 * (BKT * 2));
+      f[i] = i32x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  }
+  static constexpr int READS = 2 * T;
 };
 
 template <int N>

@@ -34,6 +34,15 @@ from .engine import no_gc_capture
 DP_T5_DW_GROUPS = (4, 4, 3, 1)
 
 
+def dp_t5_dw_groups(layers=12):
+    """The DP grouping for a T5 stack of `layers` (t5-large: 24 -> (8, 8, 6, 2)): the same
+    shape, scaled, with a short last group so the exposed bucket stays small."""
+    if layers == 12:
+        return DP_T5_DW_GROUPS
+    g = [layers // 3, layers // 3, layers // 4]
+    return tuple(g + [layers - sum(g)])
+
+
 def plan_buckets(ready_marks, end, min_bytes=24 << 20):
     """Group the engine's ready marks (call index, prefix end) into buckets of
     at least `min_bytes` of fp32 gradient.  Returns [(call_index, start, stop)]."""

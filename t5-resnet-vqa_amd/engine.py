@@ -84,7 +84,18 @@ def _gemm_key(d):
     return (d.m, d.n, d.k, d.batch, d.a_trans, d.b_trans, d.a_conv, d.b_conv,
             geo(d.ga) if d.a_conv else None, geo(d.gb) if d.b_conv else None,
             bool(d.c32), bool(d.c16), bool(d.bias), bool(d.res32), bool(d.res16), bool(d.mask16), d.relu,
-            d.beta != 0.0, d.drop.p > 0.0) + (("rownorm",) if d.rownorm else ())
+            d.beta != 0.0, d.drop.p > 0.0) + (("rownorm",) if d.rownorm else ()) + (("fp8",) if d.fp8 else ())
+
+
+class _Seq:
+    """Several prepared calls issued as one (a deferred AdamW range and the e4m3 weight
+    copies that follow it)."""
+    def __init__(self, calls):
+        self.calls = calls
+
+    def __call__(self, stream):
+        for c in self.calls:
+            c(stream)
 
 
 @contextlib.contextmanager
@@ -135,7 +146,7 @@ class VQAEngine:
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0, pipeline=False,
                  t5_dw_group=None, defer_optimizer=True, dw_stream=None, sga_dw_batch=True, pair_bwd=True,
-                 language_model="t5-base"):
+                 language_model="t5-base", fp8=False):
         L.load()
         # pipeline: the frozen ResNet (no trainable input) of the NEXT batch runs on its own
         # stream beside this step's T5 / SGA / backward / optimizer (see train_step)
@@ -151,6 +162,10 @@ class VQAEngine:
         self.D, self.nl, self.h5, self.dkv, self.dff = dm.d_model, dm.t5_layers, dm.t5_heads, dm.t5_dkv, dm.t5_dff
         self.sga_heads, self.sga_dh = dm.sga_heads, dm.sga_dhead
         assert self.h5 * self.dkv == self.D and self.sga_heads * self.sga_dh == self.D
+        # fp8: the forward weight GEMMs of the T5 layers and SGA blocks on e4m3 operands (BASELINE
+        # configs[4] "fp8 MFMA weights"): weights and their input activations quantised row-wise
+        # (vqa_quant_rows_fp8), the backward on the bf16 shadows / saved bf16 activations
+        self.fp8 = bool(fp8)
         # the answer head's log-softmax keeps one sample's answer logits in registers (head.hip:
         # A <= 1024; DAQUAR has 170) and the pooler one sample's tokens (L <= 64)
         if not 1 <= answer_spaces <= 1024:
@@ -201,6 +216,7 @@ class VQAEngine:
             self._plan_forward()
             self._plan_backward()
             self._plan_optimizer()
+            self._run(self.quant_all)                     # e4m3 weights of the initial parameters
         self.graph = None
         self.allreduce = None            # set by the DP trainer: fn(G32 tensor) on the current stream
         self._side = torch.cuda.Stream(self.dev)
@@ -223,6 +239,13 @@ class VQAEngine:
         self.P32 = torch.from_numpy(flat).to(self.dev)
         self.P16 = self.P32.to(BF16)
         self.G32 = self._t(lay.total, zero=True)
+        if self.fp8:
+            # e4m3 weight shadow and its row scales, at the fp32 arena's element offsets: row r of
+            # segment s is W8[s.offset + r*K :] with scale WSC[s.offset + r] (constant strides
+            # between the blocks' segments, as the batched launches need)
+            self.W8 = torch.empty(lay.total, dtype=torch.uint8, device=self.dev)
+            self.WSC = torch.ones(lay.total, dtype=F32, device=self.dev)
+            self._xq = {}
         self.M = self._t(lay.total, zero=True)
         self.V = self._t(lay.total, zero=True)
         self.VMAX = self._t(lay.total, zero=True)
@@ -291,12 +314,13 @@ class VQAEngine:
         # stem: conv7x7/2 + BN + ReLU, then maxpool 3x3/2
         # (as a 4x4 stride-1 conv over the space-to-depth image: K 256 instead of 7*7*8 = 392)
         w16, b32 = conv_w("conv1", "bn1", s2d=True)
-        self.res_calls.append(ops.Call("vqa_image_to_s2d16", self.IMG.data_ptr(), self.IMG8.data_ptr(), B, H, H))
+        self.res_calls.append(ops.Call("vqa_image_to_s2d16", self.IMG.data_ptr(), self.IMG8.data_ptr(), B, H, H,
+                                       keep=(self.IMG, self.IMG8)))
         g = ops.conv_geom(B, hz, hz, 16, h1, h1, 4, 4, 1, 1)
         self._gemm(self.res_calls, self.IMG8, w16, B * h1 * h1, 64, 256, lda=256, ldb=256, ga=g,
                    c16=bufs[0], ldc16=64, bias=b32, relu=True)
         self.res_calls.append(ops.Call("vqa_maxpool3x3s2_nhwc", bufs[0].data_ptr(), bufs[1].data_ptr(), B, h1, h1,
-                                       64, h2, h2))
+                                       64, h2, h2, keep=(bufs[0], bufs[1])))
         x = bufs[1]
         free = [bufs[0], bufs[2], bufs[3], bufs[4]]
         nblocks_total = len(plan)
@@ -481,7 +505,50 @@ class VQAEngine:
         p = np.float32(self.p_drop)
         return float(np.float32(1.0) / (np.float32(1.0) - p))
 
+    # ------------------------------------------------------------------ fp8 (config 5)
+    FP8_T5 = ("qkv_w", "o_w", "wi", "wo")
+    FP8_SGA = ("qkv1_w", "m1_w", "q2_w", "kv2_w", "m2_w", "fc1_w", "fc2_w")
+
+    def _is_fp8(self, wname):
+        return self.fp8 and wname.rsplit(".", 1)[-1] in (self.FP8_T5 + self.FP8_SGA)
+
+    def _w8(self, wname):
+        """(e4m3 weight view [n, k], its row scales [n]) of segment `wname` in the fp8 arenas."""
+        sg = self.lay[wname]
+        n, k = sg.shape
+        return self.W8[sg.offset:sg.offset + n * k].view(n, k), self.WSC[sg.offset:sg.offset + n]
+
+    def _quant_weight(self, lst, wname, rows=None):
+        """Row-wise e4m3 copy of weight `wname` (its fp32 master, `rows` rows from its offset:
+        several side-by-side segments quantised as one matrix)."""
+        sg = self.lay[wname]
+        k = sg.shape[1]
+        rows = sg.shape[0] if rows is None else rows
+        self._call(lst, "vqa_quant_rows_fp8", ops.addr(self.P32, sg.offset), 0, k, rows, k, ops.addr(self.W8, sg.offset),
+                   k, ops.addr(self.WSC, sg.offset), extra=(self.P32, self.W8, self.WSC))
+
+    def _quant_act(self, lst, key, x16, rows):
+        """e4m3 copy (+ row scales) of a bf16 GEMM input, into a buffer private to call site `key`."""
+        k = x16.shape[-1]
+        if key not in self._xq:
+            self._xq[key] = (torch.empty(rows, k, dtype=torch.uint8, device=self.dev), self._t(rows))
+        x8, xs = self._xq[key]
+        self._call(lst, "vqa_quant_rows_fp8", x16, 1, k, rows, k, x8, k, xs)
+        return x8, xs
+
     def _linear(self, lst, x16, wname, m, out32=None, out16=None, bias=True, relu=False, res32=None, drop=None):
+        if self._is_fp8(wname):
+            x8, xs = self._quant_act(lst, (wname, "x"), x16, m)
+            w8, ws = self._w8(wname)
+            n, k = w8.shape
+            self._gemm(lst, x8, w8, m, n, k, lda=k, ldb=k, c32=out32, ldc32=n, c16=out16, ldc16=n,
+                       bias=self.p32[wname[:-1] + "b"] if bias else None, relu=relu, res32=res32, ldres=n, fp8=True,
+                       scale_a=xs, scale_b=ws, keep=(self.W8, self.WSC))
+            d = self._drop(drop) if drop is not None else None
+            if d is not None:
+                lst[-1].desc.drop = d
+                lst[-1].keep = lst[-1].keep + (self.RNG,)
+            return
         w = self.p16[wname]
         n, k = w.shape
         self._gemm(lst, x16, w, m, n, k, lda=k, ldb=k, c32=out32, ldc32=n, c16=out16, ldc16=n,
@@ -621,8 +688,16 @@ class VQAEngine:
         # self-attention halves of all blocks first (they only read the T5 output): one q|k|v
         # projection with N = 3 * 2304, the blocks' attentions, one batched merge
         NB, W3 = self.NB, 3 * D
-        self._gemm(f, self.TXT16, self.p16["sga0.qkv1_w"], T, NB * W3, D, lda=D, ldb=D, c16=self.QKV1A,
-                   ldc16=NB * W3, bias=self.p32["sga0.qkv1_b"], keep=self._sga_self_keep())
+        if self.fp8:                                          # the blocks' q|k|v weights as one [NB*2304, D] matrix
+            x8, xs = self._quant_act(f, ("sga.qkv1", "x"), self.TXT16, T)
+            w8 = self.W8[self.lay["sga0.qkv1_w"].offset:]
+            self._gemm(f, x8, w8, T, NB * W3, D, lda=D, ldb=D, c16=self.QKV1A, ldc16=NB * W3,
+                       bias=self.p32["sga0.qkv1_b"], fp8=True, scale_a=xs,
+                       scale_b=ops.addr(self.WSC, self.lay["sga0.qkv1_w"].offset),
+                       keep=self._sga_self_keep() + (self.W8, self.WSC))
+        else:
+            self._gemm(f, self.TXT16, self.p16["sga0.qkv1_w"], T, NB * W3, D, lda=D, ldb=D, c16=self.QKV1A,
+                       ldc16=NB * W3, bias=self.p32["sga0.qkv1_b"], keep=self._sga_self_keep())
         for n in range(NB):
             s, c0 = self.sga[n], n * W3
             q = self.QKV1A
@@ -630,10 +705,17 @@ class VQAEngine:
                        v=ops.addr(q, c0 + 2 * D), ldv=NB * W3, o=s["O1"], ldo=D, p=s["P1"], batch=B,
                        heads=self.sga_heads, lq=Lq, lk=Lq, dh=self.sga_dh, scale=sc, drop=sga_site(n, 0),
                        keep=(q,))
-        self._gemm(f, self.O1A, self.p16["sga0.m1_w"], T, D, D, lda=D, ldb=D, c32=self.S1A, ldc32=D,
-                   bias=self.p32["sga0.m1_b"], res32=self.TXT32, ldres=D, batch=NB, stride_a=T * D,
-                   stride_b=D * D, stride_c32=T * D, stride_res=0, stride_bias=D,
-                   drop_site_stride=sga_site(1, 1) - sga_site(0, 1), keep=self._sga_self_keep())
+        m1kw = dict(c32=self.S1A, ldc32=D, bias=self.p32["sga0.m1_b"], res32=self.TXT32, ldres=D, batch=NB,
+                    stride_a=T * D, stride_b=D * D, stride_c32=T * D, stride_res=0, stride_bias=D,
+                    drop_site_stride=sga_site(1, 1) - sga_site(0, 1))
+        if self.fp8:
+            x8, xs = self._quant_act(f, ("sga.m1", "x"), self.O1A.view(NB * T, D), NB * T)
+            o0 = self.lay["sga0.m1_w"].offset
+            self._gemm(f, x8, self.W8[o0:], T, D, D, lda=D, ldb=D, fp8=True, scale_a=xs, stride_scale_a=T,
+                       scale_b=ops.addr(self.WSC, o0), stride_scale_b=D * D,
+                       keep=self._sga_self_keep() + (self.W8, self.WSC), **m1kw)
+        else:
+            self._gemm(f, self.O1A, self.p16["sga0.m1_w"], T, D, D, lda=D, ldb=D, keep=self._sga_self_keep(), **m1kw)
         self._set_drop(f[-1], sga_site(0, 1))
         for n in range(NB):
             s, p = self.sga[n], f"sga{n}."
@@ -646,9 +728,17 @@ class VQAEngine:
         wst = segs[1].offset - segs[0].offset if NB > 1 else 0
         assert all(b_.offset - a_.offset == wst for a_, b_ in zip(segs, segs[1:]))
         assert all(b_.offset - a_.offset == wst for a_, b_ in zip(bsegs, bsegs[1:]))
-        self._gemm(f, self.X1hS, self.p16[f"sga{NB - 1}.q2_w"], T, D, D, lda=D, ldb=D, c16=self.Q2S, ldc16=D,
-                   bias=self.p32[f"sga{NB - 1}.q2_b"], batch=NB, stride_a=T * D, stride_b=wst, stride_c16=T * D,
-                   stride_bias=wst, keep=(self.P16, self.P32))
+        q2kw = dict(c16=self.Q2S, ldc16=D, bias=self.p32[f"sga{NB - 1}.q2_b"], batch=NB, stride_a=T * D,
+                    stride_b=wst, stride_c16=T * D, stride_bias=wst)
+        if self.fp8:
+            x8, xs = self._quant_act(f, ("sga.q2", "x"), self.X1hS.view(NB * T, D), NB * T)
+            o0 = self.lay[f"sga{NB - 1}.q2_w"].offset
+            self._gemm(f, x8, self.W8[o0:], T, D, D, lda=D, ldb=D, fp8=True, scale_a=xs, stride_scale_a=T,
+                       scale_b=ops.addr(self.WSC, o0), stride_scale_b=wst, keep=(self.P16, self.P32, self.W8, self.WSC),
+                       **q2kw)
+        else:
+            self._gemm(f, self.X1hS, self.p16[f"sga{NB - 1}.q2_w"], T, D, D, lda=D, ldb=D, keep=(self.P16, self.P32),
+                       **q2kw)
         for n in range(NB):
             s, p = self.sga[n], f"sga{n}."
             if n > 0:
@@ -962,6 +1052,19 @@ class VQAEngine:
         cuts.append(("scaler", lay["scaler_w"].offset, lay["t5.final_ln"].offset))
         cuts.append(("head", 0, lay["scaler_w"].offset))     # classifier, pooler, SGA
         assert sum(hi - lo for _, lo, hi in cuts) == n
+        # fp8: the e4m3 copies of the range's weights follow every AdamW range (and the whole
+        # update when it is not deferred)
+        quant = {name: [] for name, _, _ in cuts}
+        self.quant_all = []
+        if self.fp8:
+            jobs = [(f"t5.{i}.{w}", None) for i in range(self.nl) for w in self.FP8_T5]
+            jobs.append(("sga0.qkv1_w", self.NB * 3 * self.D))          # the blocks' side-by-side q|k|v
+            jobs += [(f"sga{n}.{w}", None) for n in range(self.NB) for w in self.FP8_SGA if w != "qkv1_w"]
+            for wname, rows in jobs:
+                off = self.lay[wname].offset
+                nm = next(name for name, lo, hi in cuts if lo <= off < hi)
+                self._quant_weight(quant[nm], wname, rows)
+                self.quant_all += quant[nm][-1:]
         self.adam_segs = []
         self.adam_embed = None
         for name, lo, hi in cuts:
@@ -974,6 +1077,8 @@ class VQAEngine:
             for i, e in enumerate(ends):
                 ds.group_end[i] = e - lo
             c = ops.Call("vqa_adamw_amsgrad", ctypes.byref(ds), desc=ds, keep=keep)
+            if quant[name]:
+                c = _Seq([c] + quant[name])
             if name == "embed":
                 self.adam_embed = c
             else:
@@ -983,6 +1088,7 @@ class VQAEngine:
         self.clear_pending = lst[0]
         if not self.defer_opt:
             o.append(self.adam_full)
+            o += self.quant_all
         elif self.adam_embed is not None:
             o.append(self.adam_embed)
 
@@ -1419,6 +1525,8 @@ class VQAEngine:
                 for cfg in range(1, lib_gemm_configs() + 1):
                     if (cfg in L.GEMM_KC_B_ONLY and d.b_trans) or ((cfg in L.GEMM_PATCH_ONLY) != (d.a_conv == 2)):
                         continue
+                    if d.fp8 and cfg not in L.GEMM_FP8:
+                        continue
                     bm, bn, _ = L.GEMM_TILES[cfg]
                     tiles = -(-d.m // bm) * -(-d.n // bn) * max(1, d.batch)
                     if cfg in L.GEMM_BK128 and (d.a_conv or d.b_conv):
@@ -1513,6 +1621,7 @@ class VQAEngine:
         """Re-derive the bf16 GEMM shadow from the fp32 masters (after writing weights through
         param_view / ParameterGroup views)."""
         self.P16.copy_(self.P32)
+        self._run(self.quant_all)
 
     def layer4_features(self):
         """The frozen ResNet's layer4 map of the current batch as NCHW fp32 (the kernels keep

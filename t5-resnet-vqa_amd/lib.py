@@ -49,6 +49,8 @@ class GemmDesc(ctypes.Structure):
         ("splitk", c_int), ("workspace", c_void_p), ("workspace_bytes", c_ll),
         ("stride_bias", c_ll), ("drop_site_stride", c_int),
         ("rownorm", c_int), ("rownorm_eps", c_float),
+        ("fp8", c_int), ("scale_a", c_void_p), ("scale_b", c_void_p),
+        ("stride_scale_a", c_ll), ("stride_scale_b", c_ll),
     ]
 
 
@@ -88,6 +90,7 @@ GEMM_TILES = {1: (128, 128, 3), 2: (128, 64, 4), 3: (64, 64, 4), 4: (64, 64, 2),
 GEMM_PATCH_ONLY = (17, 18, 19, 20)       # the LDS-patch 3x3 convolution (a_conv = 2) and nothing else
 GEMM_KC_B_ONLY = (13, 14, 15, 16)        # tile configs that need a k-contiguous B operand (b_trans = 0)
 GEMM_BK128 = (21, 22, 23)                # 128-deep k-tiles: no implicit im2col operand, no split-K
+GEMM_FP8 = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 21, 22, 23)   # tile configs with an e4m3 form (gemm_fp8.hip)
 GEMM_WAVES = {c: ((4, 2) if c in (9, 12) else (2, 4) if c in (10, 11) else (2, 2)) for c in GEMM_TILES}
 
 ATTN_MFMA, ATTN_LONG, ATTN_VALU = 0, 1, 2          # vqa_attn_path
@@ -187,6 +190,7 @@ register("vqa_batch_sum", P, c_int, c_ll, P, c_float)
 register("vqa_cast_f32_bf16", P, P, c_ll)
 register("vqa_zero", P, c_ll)
 register("vqa_copy", P, P, c_ll)
+register("vqa_quant_rows_fp8", P, c_int, c_ll, c_int, c_int, P, c_ll, P)
 register("vqa_head_fwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_head_bwd", P, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_grad_sqnorm", P, c_ll, P, c_int)

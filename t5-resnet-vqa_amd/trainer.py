@@ -63,10 +63,11 @@ class VQATrainer:
                              "the ViT configuration (configs[3]) is a single-GPU one")
         self.process_group, self.bucket_mb = process_group, int(bucket_mb)
         self._dp = None
-        if self.data_parallel and model.engine.t5_dw_groups != list(dp.DP_T5_DW_GROUPS):
+        groups = dp.dp_t5_dw_groups(model.engine.nl) if self.data_parallel else None
+        if self.data_parallel and model.engine.t5_dw_groups != list(groups):
             # DP layout: T5 weight gradients in groups that let the buckets become final (and be
             # all-reduced) while the backward runs; rebuilt before the optimizer is configured
-            model._build(model.state_dict(), t5_dw_group=dp.DP_T5_DW_GROUPS)
+            model._build(model.state_dict(), t5_dw_group=groups)
         self.num_training_steps = int(num_training_steps)
         warm = lr_scheduler_kwargs.get("num_warmup_steps", -1)
         warm = self.num_training_steps // 10 if warm == -1 else int(warm)

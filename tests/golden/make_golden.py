@@ -269,13 +269,14 @@ def t5_large_case():
     return {"ids": nb["question_input_ids"], "mask": nb["question_attention_masks"], "hidden": h.detach().numpy()}
 
 
-def main_c5():
-    np.savez_compressed(os.path.join(HERE, "sga1024_block.npz"), **sga1024_case())
-    print("sga1024 done", flush=True)
-    np.savez_compressed(os.path.join(HERE, "t5_large_encoder.npz"), **t5_large_case())
-    print("t5-large done", flush=True)
+def main_c5(model_only=False):
+    if not model_only:
+        np.savez_compressed(os.path.join(HERE, "sga1024_block.npz"), **sga1024_case())
+        print("sga1024 done", flush=True)
+        np.savez_compressed(os.path.join(HERE, "t5_large_encoder.npz"), **t5_large_case())
+        print("t5-large done", flush=True)
     np.savez_compressed(os.path.join(HERE, "model_c5_r50_384_l32.npz"),
-                        **full_model_case("resnet50", 2, 32, 384, builder=build_model_c5, blocks=6,
+                        **full_model_case("resnet50", 4, 32, 384, builder=build_model_c5, blocks=6,
                                           lm="t5-large"))
     print("config-5 model done", flush=True)
 
@@ -295,7 +296,7 @@ def main():
 
 
 if __name__ == "__main__":
-    if sys.argv[1:] == ["c5"]:
-        main_c5()
+    if sys.argv[1:2] == ["c5"]:
+        main_c5(model_only=sys.argv[2:] == ["model"])
     else:
         main()

@@ -446,3 +446,85 @@ def test_rmsnorm_fwd_batched_matches_single(ops, pkg):
                      ctypes.c_float(1e-6), None)
         torch.cuda.synchronize()
         assert torch.equal(y, y1) and torch.equal(r, r1)
+
+
+def _fp8_deq(q, scale):
+    """e4m3 bytes [rows, cols] + row scales -> fp64 values."""
+    return q.view(torch.float8_e4m3fn).double() * scale.double()[:, None]
+
+
+def test_quant_rows_fp8_matches_torch_e4m3(ops, pkg):
+    """vqa_quant_rows_fp8 == torch: scale = amax / 448 per row, q = (x / scale) rounded to
+    float8_e4m3fn (nearest even), bit for bit, from fp32 and from bf16 rows; an all-zero row
+    gets scale 1."""
+    rows, cols = 37, 1040
+    x = torch.randn(rows, cols, device="cuda") * torch.logspace(-3, 2, rows, device="cuda")[:, None]
+    x[5] = 0.0
+    for src in (x, x.bfloat16()):
+        q = torch.empty(rows, cols, dtype=torch.uint8, device="cuda")
+        sc = torch.empty(rows, device="cuda")
+        pkg.lib.call("vqa_quant_rows_fp8", src.data_ptr(), int(src.dtype == torch.bfloat16), cols, rows, cols,
+                     q.data_ptr(), cols, sc.data_ptr())
+        torch.cuda.synchronize()
+        xf = src.float()
+        amax = xf.abs().amax(1)
+        ref_s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+        assert torch.equal(sc, ref_s)
+        ref_q = (xf / ref_s[:, None]).to(torch.float8_e4m3fn).view(torch.uint8)
+        assert torch.equal(q, ref_q), (q != ref_q).sum()
+
+
+@pytest.mark.parametrize("M,N,K,cfg,splitk", [(2048, 1024, 1024, 0, 1), (300, 136, 512, 4, 1), (2048, 3072, 1024, 7, 1),
+                                             (2048, 1024, 4096, 6, 4), (512, 512, 2048, 21, 1), (1000, 256, 1024, 9, 1),
+                                             (2048, 1024, 1024, 23, 1), (256, 512, 256, 12, 1), (640, 384, 768, 1, 2)])
+def test_fp8_gemm_matches_dequantised_fp64(ops, pkg, M, N, K, cfg, splitk):
+    """vqa_gemm_desc.fp8: Y = (X8 W8^T) * sx[m] * sw[n] + bias, ReLU, fp32 residual, bf16 copy;
+    against the fp64 product of the dequantised operands (the e4m3 products are exact in fp32,
+    so only the fp32 accumulation order differs)."""
+    x = torch.randn(M, K, device="cuda")
+    w = torch.randn(N, K, device="cuda") * 0.05
+    x8, w8 = torch.empty(M, K, dtype=torch.uint8, device="cuda"), torch.empty(N, K, dtype=torch.uint8, device="cuda")
+    sx, sw = torch.empty(M, device="cuda"), torch.empty(N, device="cuda")
+    pkg.lib.call("vqa_quant_rows_fp8", x.data_ptr(), 0, K, M, K, x8.data_ptr(), K, sx.data_ptr())
+    pkg.lib.call("vqa_quant_rows_fp8", w.data_ptr(), 0, K, N, K, w8.data_ptr(), K, sw.data_ptr())
+    bias = torch.randn(N, device="cuda")
+    res = torch.randn(M, N, device="cuda")
+    out, out16 = torch.full((M, N), float("nan"), device="cuda"), torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    d = ops.gemm_desc(x8.view(torch.bfloat16), w8.view(torch.bfloat16), M, N, K, lda=K, ldb=K, c32=out, ldc32=N,
+                      c16=out16, ldc16=N, bias=bias, res32=res, ldres=N, relu=True)
+    d.fp8, d.scale_a, d.scale_b = 1, sx.data_ptr(), sw.data_ptr()
+    d.config = cfg
+    ws = None
+    if splitk > 1:
+        ops.set_splitk(d, splitk)
+        ws = ops.splitk_workspace(d)
+        ops.set_splitk(d, splitk, ws)
+    ops.run(d)
+    torch.cuda.synchronize()
+    ref = torch.relu(_fp8_deq(x8, sx) @ _fp8_deq(w8, sw).T + bias.double() + res.double())
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item() + 1e-5, err
+    torch.testing.assert_close(out16.float(), out.bfloat16().float())
+
+
+def test_fp8_gemm_batched_strides(ops, pkg):
+    """Batched fp8 launch (the SGA blocks' batched merge): batch z reads A, B at their byte
+    strides and its scales at stride_scale_a / stride_scale_b."""
+    Z, M, N, K = 3, 256, 384, 512
+    x = torch.randn(Z * M, K, device="cuda")
+    w = torch.randn(Z * N, K, device="cuda") * 0.05
+    x8, w8 = torch.empty(Z * M, K, dtype=torch.uint8, device="cuda"), torch.empty(Z * N, K, dtype=torch.uint8,
+                                                                                   device="cuda")
+    sx, sw = torch.empty(Z * M, device="cuda"), torch.empty(Z * N, device="cuda")
+    pkg.lib.call("vqa_quant_rows_fp8", x.data_ptr(), 0, K, Z * M, K, x8.data_ptr(), K, sx.data_ptr())
+    pkg.lib.call("vqa_quant_rows_fp8", w.data_ptr(), 0, K, Z * N, K, w8.data_ptr(), K, sw.data_ptr())
+    out = torch.empty(Z, M, N, device="cuda")
+    d = ops.gemm_desc(x8.view(torch.bfloat16), w8.view(torch.bfloat16), M, N, K, lda=K, ldb=K, c32=out, ldc32=N,
+                      batch=Z, stride_a=M * K, stride_b=N * K, stride_c32=M * N)
+    d.fp8, d.scale_a, d.scale_b, d.stride_scale_a, d.stride_scale_b = 1, sx.data_ptr(), sw.data_ptr(), M, N
+    ops.run(d)
+    torch.cuda.synchronize()
+    for z in range(Z):
+        ref = _fp8_deq(x8[z * M:(z + 1) * M], sx[z * M:(z + 1) * M]) @ _fp8_deq(w8[z * N:(z + 1) * N],
+                                                                                  sw[z * N:(z + 1) * N]).T
+        assert (out[z].double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-6
