@@ -1591,6 +1591,31 @@ class VQAEngine:
         specs = S.model_specs(self.vision, self.A, self.NB, self.dims)
         return {k: sd[k] for k in specs}
 
+    def optimizer_state(self):
+        """AdamW(amsgrad) state in reference layout: ({key: exp_avg}, {key: exp_avg_sq},
+        {key: max_exp_avg_sq}, step, dropout RNG {seed, counter, training}).  The pending
+        deferred update is applied first, as state_dict() does."""
+        self.flush_optimizer()
+        torch.cuda.synchronize(self.dev)
+        unpack = lambda t: self.lay.unpack(t.cpu().numpy())
+        return (unpack(self.M), unpack(self.V), unpack(self.VMAX), float(self.opt_state[L.ST_STEP].item()),
+                self.RNG.cpu().numpy().copy())
+
+    def load_optimizer_state(self, exp_avg, exp_avg_sq, max_exp_avg_sq, step, rng=None):
+        """Restore what optimizer_state() returned (keys missing from the dicts: zero state)."""
+        self.flush_optimizer()
+        zeros = {k: np.zeros(sg, np.float32) for k, sg in S.model_specs(self.vision, self.A, self.NB, self.dims).items()
+                 if k in set(self.lay.trainable_keys)}
+        for arena, st in ((self.M, exp_avg), (self.V, exp_avg_sq), (self.VMAX, max_exp_avg_sq)):
+            full = dict(zeros)
+            full.update({k: np.asarray(v, np.float32) for k, v in st.items() if k in full})
+            arena.copy_(torch.from_numpy(self.lay.pack(full)))
+        self.opt_state.zero_()
+        self.opt_state[L.ST_STEP] = float(step)
+        if rng is not None:
+            self.RNG.copy_(torch.as_tensor(np.asarray(rng).astype(np.uint32).view(np.int32)))
+        torch.cuda.synchronize(self.dev)
+
     def segment_grad(self, name):
         return self.g32[name]
 

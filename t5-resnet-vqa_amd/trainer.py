@@ -35,9 +35,11 @@ from __future__ import annotations
 import inspect
 import time
 
+import numpy as np
 import torch
 
 from . import dp
+from . import synthetic as S
 from .model import ResnetVQAModel
 
 HARD_CODED_LR = 5e-4          # faster_rcnn_vqa_trainer.py:244-261
@@ -79,6 +81,10 @@ class VQATrainer:
             group_lr = {"lang_model": float(optimizer_kwargs.get("lm_encoder_lr", 5e-3)),
                         "scaler": HARD_CODED_LR, "sga_modules": HARD_CODED_LR, "attention_pooler": HARD_CODED_LR,
                         "classification_layer": float(optimizer_kwargs.get("classifier_lr", 1e-5))}
+        self.group_lr = dict(group_lr)
+        self.vision_lr = float(optimizer_kwargs.get("vision_lr", 8e-3))
+        self.adam_kwargs = {"betas": tuple(kw.get("betas", (0.9, 0.999))), "eps": float(kw.get("eps", 1e-8)),
+                            "weight_decay": float(kw.get("weight_decay", 1e-2)), "amsgrad": True}
         model.configure_optimizer(group_lr=group_lr, warmup=warm, total=self.num_training_steps,
                                          max_norm=float(gradient_clipping or 0.0),
                                          weight_decay=float(kw.get("weight_decay", 1e-2)),
@@ -161,6 +167,96 @@ class VQATrainer:
         t = torch.cat([x.cpu() for x in targets]) if targets else torch.zeros(0, dtype=torch.long)
         acc = float((p == t).float().mean()) if len(t) else 0.0
         return {"avg_loss": total / max(1, n), "predictions": p.tolist(), "targets": t.tolist(), "accuracy": acc}
+
+    # ------------------------------------------------------------------ optimizer checkpoints
+    # The reference saves {'epoch', 'scheduler', 'optimizer'} with torch.save (callbacks.py:118-125)
+    # and reloads the optimizer from state_dict_checkpoint.pt (faster_rcnn_vqa_trainer.py:269-277).
+    # Here the same dict, with the optimizer and scheduler state in torch's own AdamW / LambdaLR
+    # state_dict formats over the reference's parameter order (its six groups, :231-263), so a
+    # checkpoint written here loads into the reference's optimizer and back.
+    def _param_groups(self):
+        m = self.model
+        scaler = "downscale_layer" if m.vision_model_name == "resnet50" else "upscale_layer"
+        names = [("vision_model", "Vision Model"), ("lang_model", "Language Model"),
+                 (scaler, "DownScaler Layer" if scaler == "downscale_layer" else "UpScaler Layer"),
+                 ("sga_modules", "Self-Guided Attention Module"), ("attention_pooler", "Attention Pooler"),
+                 ("classification_layer", "Classifier Layer")]
+        specs = S.model_specs(m.vision_model_name, m.answer_spaces, m.num_attention_blocks, m.language_model_name)
+        params = [k for k in specs if not k.endswith(("running_mean", "running_var", "num_batches_tracked"))]
+        groups = []
+        for top, label in names:
+            keys = [k for k in params if k.split(".", 1)[0] == top]
+            lr = self.vision_lr if top == "vision_model" else \
+                self.group_lr.get("scaler" if top == scaler else top, HARD_CODED_LR)
+            groups.append((label, lr, keys))
+        return groups
+
+    def optimizer_state_dict(self):
+        """torch.optim.AdamW(amsgrad=True).state_dict() of the reference's parameter groups."""
+        e = self.model.engine
+        m, v, vm, step, _ = e.optimizer_state()
+        state, pgroups, idx = {}, [], 0
+        for label, lr, keys in self._param_groups():
+            ids = []
+            for k in keys:
+                if k in m and step > 0:                     # the frozen ResNet / unused scaler: no state
+                    state[idx] = {"step": torch.tensor(step), "exp_avg": torch.from_numpy(m[k]),
+                                  "exp_avg_sq": torch.from_numpy(v[k]), "max_exp_avg_sq": torch.from_numpy(vm[k])}
+                ids.append(idx)
+                idx += 1
+            pgroups.append({"lr": lr * self._lr_factor(step), "initial_lr": lr, "model_name": label,
+                            "betas": self.adam_kwargs["betas"], "eps": self.adam_kwargs["eps"],
+                            "weight_decay": self.adam_kwargs["weight_decay"], "amsgrad": True, "maximize": False,
+                            "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+                            "decoupled_weight_decay": True, "params": ids})
+        return {"state": state, "param_groups": pgroups}
+
+    def _lr_factor(self, step):
+        """get_linear_schedule_with_warmup's multiplier at `step` (TF/optimization.py:101-107)."""
+        w, t = self.num_warmup_steps, self.num_training_steps
+        return step / max(1, w) if step < w else max(0.0, (t - step) / max(1, t - w))
+
+    def scheduler_state_dict(self):
+        """LambdaLR.state_dict() of the reference's schedule (last_epoch = optimizer steps taken)."""
+        step = int(self.model.engine.opt_state[0].item())
+        base = [lr for _, lr, _ in self._param_groups()]
+        return {"base_lrs": base, "last_epoch": step, "_step_count": step + 1, "_is_initial": False,
+                "_get_lr_called_within_step": False, "_last_lr": [b * self._lr_factor(step) for b in base],
+                "lr_lambdas": [None] * len(base)}
+
+    def save_state_dict_checkpoint(self, path, epoch):
+        """callbacks.py:118-125: torch.save({'epoch', 'scheduler', 'optimizer'}) (+ this engine's
+        dropout RNG counter, so a resumed run draws the same masks)."""
+        e = self.model.engine
+        rng = e.optimizer_state()[4]
+        torch.save({"epoch": int(epoch), "scheduler": self.scheduler_state_dict(),
+                    "optimizer": self.optimizer_state_dict(), "vqa_rng": torch.from_numpy(rng.astype(np.int64))}, path)
+
+    def load_state_dict_checkpoint(self, path):
+        """faster_rcnn_vqa_trainer.py:269-277: resume the optimizer (and the schedule position) from
+        a checkpoint in the format above; loaded with weights_only=True.  Returns the epoch."""
+        ck = torch.load(path, weights_only=True)
+        opt = ck["optimizer"]
+        groups = self._param_groups()
+        if len(opt["param_groups"]) != len(groups):
+            raise ValueError("optimizer checkpoint has another parameter-group structure")
+        m, v, vm, step = {}, {}, {}, 0.0
+        for (label, _, keys), pg in zip(groups, opt["param_groups"]):
+            if len(pg["params"]) != len(keys):
+                raise ValueError(f"optimizer checkpoint group {label!r}: {len(pg['params'])} parameters, expected "
+                                 f"{len(keys)}")
+            for k, i in zip(keys, pg["params"]):
+                st = opt["state"].get(i)
+                if st is None:
+                    continue
+                m[k], v[k], vm[k] = (st[n].numpy() for n in ("exp_avg", "exp_avg_sq", "max_exp_avg_sq"))
+                step = float(st["step"])
+        sched = ck.get("scheduler", {})
+        if "last_epoch" in sched and not m:
+            step = float(sched["last_epoch"])
+        rng = ck["vqa_rng"].numpy() if "vqa_rng" in ck else None
+        self.model.engine.load_optimizer_state(m, v, vm, step, rng)
+        return int(ck.get("epoch", 0))
 
     @staticmethod
     def convert_logits_to_predictions(lm_logits):

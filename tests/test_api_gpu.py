@@ -159,3 +159,48 @@ def test_trainer_epochs_and_resnet18(cuda, pkg):
     v = tr.valid_one_epoch(batches)
     assert len(v["predictions"]) == 3 * B and 0.0 <= v["accuracy"] <= 1.0 and np.isfinite(v["avg_loss"])
     assert torch.equal(m.state_dict()["classification_layer.weight"], before)
+
+
+def test_optimizer_checkpoint_resumes_bit_identically(cuda, pkg, tmp_path):
+    """callbacks.py:118-125 / faster_rcnn_vqa_trainer.py:269-277: save the weights
+    (best-model.pt style) and {'epoch', 'scheduler', 'optimizer'} after two steps, rebuild a
+    model + trainer from the two files (torch.load weights_only=True) and continue: the next
+    two steps equal the uninterrupted run's bit for bit (losses, parameters, AdamW moments).
+    The optimizer entry is torch's AdamW(amsgrad) state_dict over the reference's six groups:
+    it loads into a torch.optim.AdamW built over reference-shaped parameters."""
+    import torch
+    B, L, H = 2, 16, 64
+    batches = [{k: (torch.as_tensor(v).cuda() if v is not None else None)
+                for k, v in pkg.synthetic.make_batch(B, L, H, seed=50 + i).items()} for i in range(4)]
+    okw = {"type": "AdamW", "lm_encoder_lr": 5e-3, "classifier_lr": 1e-5, "vision_lr": 8e-3,
+           "kwargs": {"weight_decay": 0.1, "amsgrad": True}}
+
+    def fresh(sd=None):
+        m = pkg.model.ResnetVQAModel("resnet50", "t5-base", 170, device="cuda", batch_size=B, seq_len=L,
+                                     image_size=H, dropout=0.1, state_dict=sd)
+        return m, pkg.trainer.VQATrainer(m, okw, {"num_warmup_steps": 2}, num_training_steps=20, logger=None)
+    m, tr = fresh()
+    for b in batches[:2]:
+        tr.train_one_step(b)
+    torch.save(m.state_dict(), tmp_path / "best-model.pt")
+    tr.save_state_dict_checkpoint(tmp_path / "state_dict_checkpoint.pt", epoch=3)
+    ref_losses = [tr.train_one_step(b)[0] for b in batches[2:]]
+    ref_m = m.engine.optimizer_state()[0]
+    ref_p = m.state_dict()
+    m2, tr2 = fresh(torch.load(tmp_path / "best-model.pt", weights_only=True))
+    assert tr2.load_state_dict_checkpoint(tmp_path / "state_dict_checkpoint.pt") == 3
+    losses = [tr2.train_one_step(b)[0] for b in batches[2:]]
+    assert losses == ref_losses, (losses, ref_losses)
+    p2, m2m = m2.state_dict(), m2.engine.optimizer_state()[0]
+    for k in ref_p:
+        assert torch.equal(p2[k], ref_p[k]), k
+    for k in ref_m:
+        assert np.array_equal(m2m[k], ref_m[k]), k
+    # the reference's optimizer accepts the saved state
+    ck = torch.load(tmp_path / "state_dict_checkpoint.pt", weights_only=True)
+    groups = [{"params": [torch.zeros(pkg.synthetic.model_specs("resnet50")[k]) for k in keys], "lr": lr}
+              for _, lr, keys in tr._param_groups()]
+    opt = torch.optim.AdamW(groups, weight_decay=0.1, amsgrad=True)
+    opt.load_state_dict(ck["optimizer"])
+    st = opt.state_dict()["state"]
+    assert len(st) == len(ck["optimizer"]["state"]) > 0 and ck["scheduler"]["last_epoch"] == 2
