@@ -295,6 +295,8 @@ def main():
     for i in range(args.warmup):
         step(i)
     stream = torch.cuda.current_stream(dev)
+    if world > 1:                          # per-collective exposed wait (HIP events around each wait)
+        dps.timing = True
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if dist:
@@ -366,6 +368,9 @@ def main():
         "roofline": roofline,
         "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
     }
+    if world > 1:
+        out["dp"] = dps.timing_report()
+        out["dp"]["backend"] = dist.get_backend()
     if args.rehearse:                               # the N-rank path's results: lockstep across ranks
         eng.flush_optimizer()
         p = eng.P32[:: max(1, eng.P32.numel() // 65536)].cpu()

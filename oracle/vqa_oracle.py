@@ -105,10 +105,12 @@ def _nodrop(site, x):
 # fp8, so this is the restatement of that arithmetic the fp8 engine is checked against, and
 # the fp32 oracle (fp8=False) measures what the quantisation costs.
 def fp8_rows(x):
-    """Row-wise e4m3 quantise-dequantise (torch.float8_e4m3fn rounds to nearest even)."""
-    amax = x.abs().amax(-1, keepdim=True)
-    s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
-    return (x / s).to(torch.float8_e4m3fn).float() * s
+    """Row-wise e4m3 quantise-dequantise: scale = amax / 448 and x / scale as correctly rounded
+    fp32 divisions (computed in fp64, then rounded), then torch.float8_e4m3fn (nearest even)."""
+    amax = x.detach().abs().amax(-1, keepdim=True).double()
+    s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax)).float()
+    q = (x.double() / s.double()).float().to(torch.float8_e4m3fn).float()
+    return q * s
 
 
 class _Fp8Matmul(torch.autograd.Function):

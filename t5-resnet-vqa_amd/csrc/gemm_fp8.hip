@@ -57,14 +57,16 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const void* __restrict_
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
-  const float s = amax > 0.f ? amax / 448.f : 1.f;
+  // correctly rounded divisions (__fdiv_rn): the compiler may not turn them into reciprocal
+  // multiplies, so the scale and the quantised bytes are exactly torch's amax / 448, x / scale
+  const float s = amax > 0.f ? __fdiv_rn(amax, 448.f) : 1.f;
   if (l == 0) scale[row] = s;
   for (int c = l * 8; c < cols; c += 512) {
     float v[8];
     load8(c, v);
     uint2 o;
-    o.x = pack4_fp8(v[0] / s, v[1] / s, v[2] / s, v[3] / s);
-    o.y = pack4_fp8(v[4] / s, v[5] / s, v[6] / s, v[7] / s);
+    o.x = pack4_fp8(__fdiv_rn(v[0], s), __fdiv_rn(v[1], s), __fdiv_rn(v[2], s), __fdiv_rn(v[3], s));
+    o.y = pack4_fp8(__fdiv_rn(v[4], s), __fdiv_rn(v[5], s), __fdiv_rn(v[6], s), __fdiv_rn(v[7], s));
     *reinterpret_cast<uint2*>(q + (long)row * ldq + c) = o;
   }
 }

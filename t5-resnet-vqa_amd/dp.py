@@ -20,6 +20,7 @@ parameters after every step.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import lib as L
@@ -132,6 +133,10 @@ class DataParallelStep:
                                  e.g32["t5.embed"].data_ptr(), self.world * T, D, S.T5_VOCAB, self.WS.data_ptr(),
                                  keep=(self.GIDS, self.GDH, self.WS, e.g32["t5.embed"]))
         self.graphs = None
+        # exposed-communication timing (bench at N > 1): HIP events on the compute stream right
+        # before and after each collective's wait, i.e. how long the step's stream stalls on it
+        self.timing = False
+        self._ev = []
         if use_graph:
             self.capture()
         # the dense embedding gradient must be zero outside the rows the scatter writes: the
@@ -229,10 +234,39 @@ class DataParallelStep:
             seg.replay()
             works += allreduce_buckets(e.G32, [bk], self.group)
         works += gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
-        for w in works[-2:]:
-            w.wait()
+        evs = []
+        self._wait(works[-2:], evs)                         # the embedding rows: needed by the tail
         g["tail"][0].replay()
         for w in works[:-2]:
-            w.wait()
+            self._wait([w], evs)
         g["opt"][0].replay()
         self._res_end()
+        if self.timing:
+            self._ev.append(evs)
+
+    def _wait(self, works, evs):
+        if not self.timing:
+            for w in works:
+                w.wait()
+            return
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for w in works:
+            w.wait()
+        b.record()
+        evs.append((a, b))
+
+    def timing_report(self):
+        """Mean exposed wait per collective over the steps run with `timing` on: the row gather,
+        then each gradient bucket (its bytes, the slice of G32 it covers)."""
+        torch.cuda.synchronize()
+        if not self._ev:
+            return None
+        waits = np.array([[a.elapsed_time(b) * 1e3 for a, b in evs] for evs in self._ev]).mean(0)
+        e = self.eng
+        return {"world_size": self.world, "steps": len(self._ev),
+                "embedding_rows_gather": {"bytes": int(self.world * e.T * (e.D * 4 + 8)),
+                                          "exposed_wait_us": round(float(waits[0]), 1)},
+                "buckets": [{"start": int(a), "stop": int(b), "bytes": int(4 * (b - a)),
+                             "exposed_wait_us": round(float(w), 1)} for (_, a, b), w in zip(self.buckets, waits[1:])],
+                "exposed_wait_us_total": round(float(waits.sum()), 1)}

@@ -537,7 +537,7 @@ class VQAEngine:
         return x8, xs
 
     def _linear(self, lst, x16, wname, m, out32=None, out16=None, bias=True, relu=False, res32=None, drop=None):
-        if self._is_fp8(wname):
+        if getattr(self, "fp8", False) and self._is_fp8(wname):          # (borrowed by VitVQAEngine: no fp8)
             x8, xs = self._quant_act(lst, (wname, "x"), x16, m)
             w8, ws = self._w8(wname)
             n, k = w8.shape

