@@ -34,7 +34,26 @@ FLOP_PER_PAIR = 30.95e9        # fwd+bwd algorithmic FLOPs
 MFMA_PEAK_TFLOPS = 2517.0      # bf16 dense: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md)
 FP8_PEAK_TFLOPS = 5034.0       # e4m3 dense, block-scaled MFMA (2x the bf16 rate per clock, MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
-PMC_FILE = "r02_pmc.json"               # rocprofv3 PMC summary this bench quotes (tools/pmc_step.py)
+PMC_FILE = "r03_pmc.json"               # rocprofv3 PMC summary this bench quotes (tools/pmc_step.py)
+DIGEST_SUFFIXES = (".py", ".hip", ".h", ".inl", ".json", "Makefile")
+
+
+def tree_digest():
+    """sha256 over the sources that decide which kernels one step launches and what they
+    touch: the package (kernels, host code, tile table), bench.py and __graft_entry__.py.
+    tools/pmc_step.py stamps it into the PMC summary; main() quotes the summary's counters
+    only when the stamp equals this tree's digest (a PMC file from another tree is ignored)."""
+    import hashlib
+    h = hashlib.sha256()
+    files = [os.path.join(ROOT, f) for f in ("bench.py", "__graft_entry__.py")]
+    for d, dirs, fs in os.walk(os.path.join(ROOT, "t5-resnet-vqa_amd")):
+        dirs[:] = sorted(x for x in dirs if x != "__pycache__" and not x.startswith("_build"))
+        files += [os.path.join(d, f) for f in sorted(fs) if f.endswith(DIGEST_SUFFIXES)]
+    for f in files:
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
 def cpu_baseline(pkg, batch=64, steps=5, warm=2):
@@ -321,10 +340,15 @@ def main():
     gnorm = eng.last_grad_norm()
     pairs = world * B * args.steps
     value = pairs / dt
-    pmc = {}
+    pmc, pmc_note = {}, f"profiles/{PMC_FILE} absent"
     pmc_path = os.path.join(ROOT, "profiles", PMC_FILE)
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
+        if pmc.get("tree_digest") != tree_digest():      # counters of another tree: not quoted
+            pmc, pmc_note = {}, f"profiles/{PMC_FILE} was measured on another tree (digest mismatch): not quoted"
+        else:
+            pmc_note = (f"profiles/{PMC_FILE} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, all dispatches of one step; "
+                        f"measured on this tree, commit {pmc.get('commit')})")
 
     # Headline roofline (the step is > 97 % GEMM FLOPs, so it is MFMA-bound): the whole
     # captured train step as one unit of work.  Algorithmic work per step = 30.95 GFLOP per
@@ -349,7 +373,7 @@ def main():
                 "traffic": round(st["traffic_bytes"]) if "traffic_bytes" in st else None,
                 "flop_per_step": step_flop, "flop_per_step_calls": calls_flop(eng),
                 "step_gpu_ms": round(gpu_step * 1e3, 4),
-                "traffic_source": f"profiles/{PMC_FILE} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, all dispatches of one step)"}
+                "traffic_source": pmc_note}
     out = {
         "metric": ("question-image pairs/sec, ResNet50+T5-large+6xSGA 384x384 fp8-weight train step (BASELINE configs[4])"
                    if args.config5 else "question-image pairs/sec, ResNet50+T5-base+SGA train step, 1/2/4/8 MI355X"),

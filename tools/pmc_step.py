@@ -49,7 +49,11 @@ def total(span, counter):
 
 def main():
     out, sf, sw, sm, rf, rw, rm, man = sys.argv[1:9]
-    res = {"correction": "fetch = 2 x 1024 x FETCH_SIZE (gfx950 half-count); write = 1024 x WRITE_SIZE"}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import tree_digest
+    # the tree the passes ran on: bench.py quotes these counters only while its digest matches
+    res = {"tree_digest": tree_digest(), "commit": os.environ.get("PMC_COMMIT"),
+           "correction": "fetch = 2 x 1024 x FETCH_SIZE (gfx950 half-count); write = 1024 x WRITE_SIZE"}
     F, W, M = steps(load(sf)), steps(load(sw)), steps(load(sm))
     n = [len(s) for s in F + W + M]
     fetch = sum(2048.0 * total(s, "FETCH_SIZE") for s in F) / len(F)
