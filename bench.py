@@ -341,8 +341,11 @@ def main():
     pairs = world * B * args.steps
     value = pairs / dt
     pmc, pmc_note = {}, f"profiles/{PMC_FILE} absent"
+    survey_cfg = (args.image_size, args.seq_len, NB) == (224, 32, 3) and not args.config5
     pmc_path = os.path.join(ROOT, "profiles", PMC_FILE)
-    if os.path.exists(pmc_path):
+    if not survey_cfg:
+        pmc_note = f"profiles/{PMC_FILE} covers the config-2 step only (B=64, 224x224, L=32, 3 blocks)"
+    elif os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
         if pmc.get("tree_digest") != tree_digest():      # counters of another tree: not quoted
             pmc, pmc_note = {}, f"profiles/{PMC_FILE} was measured on another tree (digest mismatch): not quoted"
@@ -356,7 +359,6 @@ def main():
     # the replay stream over the timed region; traffic = HBM bytes per step from the
     # committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes over every dispatch of one step.
     # Other shapes (--image-size / --seq-len): the MFMA work of the prepared calls.
-    survey_cfg = (args.image_size, args.seq_len, NB) == (224, 32, 3) and not args.config5
     step_flop = FLOP_PER_PAIR * B if survey_cfg else calls_flop(eng)
     step_tflops = step_flop / gpu_step / 1e12
     st = pmc.get("step", {}) if survey_cfg else {}

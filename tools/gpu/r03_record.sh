@@ -16,9 +16,9 @@ fi
 timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_smoke.log 2>&1 || { echo SMOKEFAIL; tail -20 gpurun_out/r03_smoke.log; exit 1; }
 tail -1 gpurun_out/r03_smoke.log
 rm -rf gpurun_out/r03_stats gpurun_out/r03_stats_c5
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r03_stats -o run -- python3 bench.py --no-cpu-baseline \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/r03_stats -o run -- python3 bench.py --no-cpu-baseline \
    > gpurun_out/r03_stats_bench.json 2> gpurun_out/r03_stats_bench.err || { echo STATSFAIL; tail -20 gpurun_out/r03_stats_bench.err; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r03_stats_c5 -o run -- python3 bench.py --config5 --no-cpu-baseline \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/r03_stats_c5 -o run -- python3 bench.py --config5 --no-cpu-baseline \
    > gpurun_out/r03_stats_c5.json 2> gpurun_out/r03_stats_c5.err || { echo STATSC5FAIL; tail -20 gpurun_out/r03_stats_c5.err; exit 1; }
 cd /tmp
 run() {  # tag counters... -- cmd   (each counter group in a run of its own)
