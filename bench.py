@@ -95,9 +95,6 @@ def calls_flop(eng, fp8_only=False):
         elif c.name in ("vqa_attn_fwd", "vqa_attn_bwd"):
             d = c.desc
             tot += (4.0 if c.name == "vqa_attn_fwd" else 8.0) * d.batch * d.heads * d.lq * d.lk * d.dh
-        elif c.name == "vqa_gemm_attn":                          # GEMM + attention, one launch
-            g, d = c.desc
-            tot += 2.0 * g.m * g.n * g.k + (8.0 if c.args[2] else 4.0) * d.batch * d.heads * d.lq * d.lk * d.dh
     return tot
 
 

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 14
+#define VQA_ABI_VERSION 13
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -212,15 +212,6 @@ int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t stream);
 #define VQA_ATTN_LONG 1
 #define VQA_ATTN_VALU 2
 int vqa_attn_path(const vqa_attn_desc* d, int backward);
-/* vqa_gemm_attn: a projection GEMM and the attention that consumes it in ONE launch (T5
- * self-attention, TF modeling_t5.py:498-560; fused.hip), bit-identical to vqa_gemm followed by
- * vqa_attn_fwd / vqa_attn_bwd on the same descriptors.  T5 shapes only: dh 64, lq = lk = 32,
- * g->m = batch * 32 a multiple of 64, bf16 output, no split-K.
- *   backward = 0: g = the q|k|v projection (k-contiguous [3D, D] weight, c16 = [T, 3D]) and
- *     a = the forward attention reading q, k, v at c16, c16 + D, c16 + 2D (ld 3D);
- *   backward = 1: g = the o projection's input gradient dContext = dY Wo (b_trans = 1, c16 =
- *     [T, D]) and a = the attention backward reading it as dout. */
-int vqa_gemm_attn(const vqa_gemm_desc* g, const vqa_attn_desc* a, int backward, hipStream_t stream);
 
 /* ----------------------------------------------------------------- norms ---
  * Rows of width d (d % 256 == 0, d <= 1024), fp32 in, fp32 and/or bf16 out.

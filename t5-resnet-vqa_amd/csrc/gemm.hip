@@ -207,7 +207,6 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
   P.rn_eps = d->rownorm_eps;
   P.qsa = P.qsb = nullptr;
   P.sqa = P.sqb = 0;
-  P.hd = 0;
   if (d->fp8) {
     // e4m3 operands: bytes, staged by the bf16 loaders as 2-byte units (128 fp8 per 64-unit k-tile)
     VQA_REQUIRE(!d->a_trans && !d->b_trans && !d->a_conv && !d->b_conv && !d->rownorm && d->relu <= 1,
@@ -257,9 +256,6 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
 
 #ifndef VQA_GEMM_MICRO
 int vqa_gemm_fp8_dispatch(void* P, int batch, int config, hipStream_t s);   // gemm_fp8.hip
-
-// the descriptor checks + kernel parameters of vqa_gemm, for the fused launches (fused.hip)
-int vqa_gemm_prepare(const vqa_gemm_desc* d, void* P) { return prepare(d, *static_cast<GemmParams*>(P)); }
 
 extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   GemmParams P;

@@ -11,21 +11,26 @@
 
 namespace {
 
-// Tile of linear block id `bid`: XCD-aware bijective remap of the id (with split-K the slices
-// of one tile are consecutive ids, i.e. (mostly) on one XCD, next to their reducer), then the
-// tile's (row, column) indices.  fused.hip recomputes a tile's coordinates with it.
-template <int BN, bool GB>
-__device__ __forceinline__ void tile_coords(const GemmParams& P, const int bid, int& tile, int& slice, int& tm,
-                                            int& tn) {
+template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, bool EXT = false,
+          int BKT = BK, bool F8 = false>
+__device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, char* smem) {
+  constexpr int NW = NWM * NWN, NT = 64 * NW;
+  constexpr int WM = BM / NWM, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
+  static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "wave sub-tile must be whole 32x32 blocks");
+  constexpr int A_BYTES = BM * BKT * 2, B_BYTES = BN * BKT * 2, ST_BYTES = A_BYTES + B_BYTES;
+  using LA = Loader<BM, AKC, GA, NW, BKT>;
+  using LB = Loader<BN, BKC, GB, NW, BKT>;
+  constexpr int NL = LA::NI + LB::NI;                 // glds instructions per thread per K-tile
+
+  // XCD-aware bijective remap of the linear block id; with split-K the slices of
+  // one tile are consecutive ids, i.e. (mostly) on one XCD, next to their reducer
   const int S = P.splitk > 1 ? P.splitk : 1;
   const int ntile = P.tiles_m * P.tiles_n;
   const int nwg = ntile * S;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  tile = wg / S;
-  slice = wg - tile * S;
-  tm = tile / P.tiles_n;
-  tn = tile - tm * P.tiles_n;
+  const int tile = wg / S, slice = wg - tile * S;
+  int tm = tile / P.tiles_n, tn = tile - tm * P.tiles_n;
   if constexpr (GB) {
     // implicit-im2col B (ConvTranspose2d dW: column = tap * C + c): order the tiles channel
     // block first, so the consecutive tiles an XCD gets are every tap and row tile of ONE
@@ -39,23 +44,6 @@ __device__ __forceinline__ void tile_coords(const GemmParams& P, const int bid, 
       tn = (r - tm * taps) * cb + cblk;
     }
   }
-}
-
-template <int BM, int BN, int STAGES, int NWM, int NWN, bool AKC, bool BKC, bool GA, bool GB, bool EXT = false,
-          int BKT = BK, bool F8 = false>
-__device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, char* smem) {
-  constexpr int NW = NWM * NWN, NT = 64 * NW;
-  constexpr int WM = BM / NWM, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
-  static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "wave sub-tile must be whole 32x32 blocks");
-  constexpr int A_BYTES = BM * BKT * 2, B_BYTES = BN * BKT * 2, ST_BYTES = A_BYTES + B_BYTES;
-  using LA = Loader<BM, AKC, GA, NW, BKT>;
-  using LB = Loader<BN, BKC, GB, NW, BKT>;
-  constexpr int NL = LA::NI + LB::NI;                 // glds instructions per thread per K-tile
-
-  const int S = P.splitk > 1 ? P.splitk : 1;
-  const int ntile = P.tiles_m * P.tiles_n;
-  int tile, slice, tm, tn;
-  tile_coords<BN, GB>(P, bid, tile, slice, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int z = blockIdx.z;
@@ -69,7 +57,7 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
   LA la;
   LB lb;
   la.init(m0, P.m, P.lda, P.ga);
-  lb.init(n0, P.n, P.ldb, P.gb, BKC && !GB ? P.hd : 0, tn);
+  lb.init(n0, P.n, P.ldb, P.gb);
   using FA = FragAddr<BM, AKC, TM, BKT>;
   using FB = FragAddr<BN, BKC, TN, BKT>;
   static_assert(!F8 || (AKC && BKC && !GA && !GB), "fp8 operands: k-contiguous A and B, no implicit im2col");

@@ -39,10 +39,6 @@ struct GemmParams {
   // 2 bytes, so the bf16 loaders stage them unchanged); acc(m, n) is scaled by qsa[m] * qsb[n]
   const float* qsa; const float* qsb;
   long sqa, sqb;           // scale strides per batch element
-  // hd > 0: head-interleaved output columns (the q|k|v projection feeding a fused attention,
-  // fused.hip): B holds 3 blocks of n/3 rows (q, k, v); tile column c of tile tn is column
-  // (c / hd) * (n / 3) + tn * hd + c % hd, i.e. tile tn = head tn's q, k and v (BN = 3 hd)
-  int hd;
 };
 
 // byte offset of 16-B chunk `ch` of row `row` in a k-contig image ([rows][BKT bf16]):
@@ -98,10 +94,7 @@ struct Loader {
   int g0[NI], g1[NI], g2[NI];
   bool ok[NI];
 
-  // hd > 0 (k-contig B of a head-interleaved tile, GemmParams.hd): image row r is matrix row
-  // (r / hd) * (nrows / 3) + hsel * hd + r % hd
-  __device__ __forceinline__ void init(int row0, int nrows, long ld, const vqa_conv_geom& g, int hd = 0,
-                                       int hsel = 0) {
+  __device__ __forceinline__ void init(int row0, int nrows, long ld, const vqa_conv_geom& g) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -109,7 +102,7 @@ struct Loader {
       if constexpr (KC) {
         const int row = ins * RPI + l / KCPR;
         const int ch = (l % KCPR) ^ kc_swz_t<BKT>(row);
-        const int grow = hd > 0 ? (row / hd) * (nrows / 3) + hsel * hd + row % hd : row0 + row;
+        const int grow = row0 + row;
         ok[j] = grow < nrows;
         kof[j] = ch * 8;
         off[j] = (long)grow * ld + ch * 8;
@@ -421,8 +414,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
             }
       }
       __syncthreads();                                  // the fragment writes have landed
-      const int c = (tid % TPR) * 8;
-      const int col = P.hd > 0 ? (c / P.hd) * (P.n / 3) + (n0 / BN) * P.hd + c % P.hd : n0 + c;
+      const int c = (tid % TPR) * 8, col = n0 + c;
 #pragma unroll
       for (int r0 = 0; r0 < HALF; r0 += RPP) {
         const int r = r0 + tid / TPR, row = m0 + pw * WM + pg * HALF + r;
@@ -503,8 +495,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int row = m0 + wm * WM + i * 32 + rl;
-          const int c = wn * WN + j * 32 + 8 * (e >> 2) + 4 * ch + (e & 3);
-          const int col = P.hd > 0 ? (c / P.hd) * (P.n / 3) + (n0 / BN) * P.hd + c % P.hd : n0 + c;
+          const int col = n0 + wn * WN + j * 32 + 8 * (e >> 2) + 4 * ch + (e & 3);
           if (row >= mlim || col >= P.n) continue;
           float kf = 1.f;
           if (MK && !(bf2f(MK[(long)row * P.ldmask + col]) > 0.f)) kf = 0.f;

@@ -146,7 +146,7 @@ class VQAEngine:
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0, pipeline=False,
                  t5_dw_group=None, defer_optimizer=True, dw_stream=None, sga_dw_batch=True, pair_bwd=True,
-                 language_model="t5-base", fp8=False, fuse_attention=True):
+                 language_model="t5-base", fp8=False):
         L.load()
         # pipeline: the frozen ResNet (no trainable input) of the NEXT batch runs on its own
         # stream beside this step's T5 / SGA / backward / optimizer (see train_step)
@@ -166,10 +166,6 @@ class VQAEngine:
         # configs[4] "fp8 MFMA weights"): weights and their input activations quantised row-wise
         # (vqa_quant_rows_fp8), the backward on the bf16 shadows / saved bf16 activations
         self.fp8 = bool(fp8)
-        # T5 self-attention fused with its producing GEMM (vqa_gemm_attn: the q|k|v projection +
-        # attention forward, the o projection's input gradient + attention backward) where the
-        # fused kernel's shapes hold: 32 tokens, head dim 64, an even batch, bf16 weights
-        self.fuse_attn = bool(fuse_attention) and seq_len == 32 and batch % 2 == 0 and not self.fp8
         # the answer head's log-softmax keeps one sample's answer logits in registers (head.hip:
         # A <= 1024; DAQUAR has 170) and the pooler one sample's tokens (L <= 64)
         if not 1 <= answer_spaces <= 1024:
@@ -489,17 +485,6 @@ class VQAEngine:
         _check_attn_path(d, fn)
         lst.append(ops.Call(fn, ctypes.byref(d), keep=ts, desc=d))
 
-    def _gemm_attn(self, lst, calls, backward):
-        """calls = [the GEMM producing the attention's operand, the attention]: ONE fused
-        vqa_gemm_attn launch when the engine fuses (bit-identical), else the two calls.  A
-        (dX, dW) pair (vqa_gemm_pair, the per-layer weight gradients) is never fused."""
-        if not self.fuse_attn or len(calls) != 2 or calls[0].name != "vqa_gemm":
-            lst.extend(calls)
-            return
-        g, a = calls
-        lst.append(ops.Call("vqa_gemm_attn", ctypes.byref(g.desc), ctypes.byref(a.desc), int(backward),
-                            keep=tuple(g.keep) + tuple(a.keep), desc=(g.desc, a.desc)))
-
     def _drop(self, site):
         """vqa_dropout for `site` (None when dropout is off)."""
         if self.p_drop <= 0.0:
@@ -678,13 +663,11 @@ class VQAEngine:
             self._t5_layer_start.append(len(f))
             self._call(f, "vqa_rmsnorm_fwd", self.HS[i], self.p32[f"t5.{i}.ln0"], None, self.N0[i], self.R0[i], T,
                        D, 1e-6, None)
-            tmp = []
-            self._linear(tmp, self.N0[i], f"t5.{i}.qkv_w", T, out16=self.QKV[i], bias=False)
+            self._linear(f, self.N0[i], f"t5.{i}.qkv_w", T, out16=self.QKV[i], bias=False)
             q = self.QKV[i]
-            self._attn(tmp, "vqa_attn_fwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
+            self._attn(f, "vqa_attn_fwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, o=self.O[i], ldo=D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B,
                        heads=self.h5, lq=Lq, lk=Lq, dh=self.dkv, scale=1.0, drop=t5_site(i, 0))
-            self._gemm_attn(f, tmp, backward=False)
             # h + dropout(attention output)   (T5LayerSelfAttention :400)
             self._linear(f, self.O[i], f"t5.{i}.o_w", T, out32=self.HM[i], bias=False, res32=self.HS[i],
                          drop=t5_site(i, 1))
@@ -957,16 +940,14 @@ class VQAEngine:
                        self.dHM32, dHM, None, 0.0, ws, T, D,
                        None, None, self._dptr(t5_site(i, 1), kp), extra=kp + [self.RNG])
             self._defer(ws, nparts, D, D, self.g32[f"t5.{i}.ln1"])
-            tmp = []
-            dxdw(tmp, dHM, self.O[i], f"t5.{i}.o_w", T, out16=self.dO16)
+            dxdw(b, dHM, self.O[i], f"t5.{i}.o_w", T, out16=self.dO16)
             q = self.QKV[i]
             dq = dQKV
-            self._attn(tmp, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
+            self._attn(b, "vqa_attn_bwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, p=self.PT[i], bias=self.PB, key_mask=self.MASK, batch=B, heads=self.h5, lq=Lq,
                        lk=Lq, dh=self.dkv, scale=1.0, dout=self.dO16, lddo=D, dq=dq, lddq=3 * D,
                        dk=ops.addr(dq, D), lddk=3 * D, dv=ops.addr(dq, 2 * D), lddv=3 * D, dbias=self.dSB[i],
                        drop=t5_site(i, 0))
-            self._gemm_attn(b, tmp, backward=True)
             dxdw(b, dq, self.N0[i], f"t5.{i}.qkv_w", T, out32=self.dC32)
             # layer 0: dH32 becomes the embedding gradient (masked by the embedding dropout :725);
             # otherwise dH16 is the FF branch gradient of layer i-1

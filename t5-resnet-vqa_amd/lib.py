@@ -144,7 +144,6 @@ def load():
     lib.vqa_attn_fwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_attn_bwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_attn_path.argtypes = [ctypes.POINTER(AttnDesc), c_int]
-    lib.vqa_gemm_attn.argtypes = [ctypes.POINTER(GemmDesc), ctypes.POINTER(AttnDesc), c_int, c_void_p]
     lib.vqa_adamw_amsgrad.argtypes = [ctypes.POINTER(AdamWDesc), c_void_p]
     for name in ("vqa_norm_bwd_workspace_floats", "vqa_colsum_workspace_floats"):
         getattr(lib, name).argtypes = [c_int, c_int]

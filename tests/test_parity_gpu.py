@@ -293,40 +293,6 @@ def test_dw_stream_matches_single_stream_bitwise(cuda, pkg):
         assert torch.equal(a, b)
 
 
-def test_fused_gemm_attention_matches_unfused_bitwise(cuda, pkg):
-    """vqa_gemm_attn (the T5 q|k|v projection + attention forward, and the o projection's input
-    gradient + attention backward, each ONE launch; the engine's default at 32 tokens) gives the
-    unfused launches' results bit for bit: losses, log-probs, gradients, parameters and optimizer
-    state over three train-mode steps (dropout on, key padding in the batches, captured graph)."""
-    import torch
-    B, L, H = 4, 32, 64
-    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
-    batches = [pkg.synthetic.make_batch(B, L, H, seed=60 + i) for i in range(4)]
-    assert any(int(np.asarray(b["question_attention_masks"]).min()) == 0 for b in batches)
-    res = []
-    for fuse in (True, False):
-        eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.1, seed=5,
-                                   pipeline=True, fuse_attention=fuse)
-        names = [c.name for c in eng.fwd_calls + eng.bwd_calls]
-        assert (names.count("vqa_gemm_attn") == 2 * eng.nl) == fuse
-        imgs = [torch.as_tensor(b["image_tensors"]).cuda() for b in batches]
-        eng.prime(imgs[0])
-        eng.load_batch(batches[0], next_images=imgs[1])
-        eng.capture()
-        eng.prime(imgs[0])
-        losses = []
-        for i in range(3):
-            eng.load_batch(batches[i], next_images=imgs[i + 1])
-            eng.train_step()
-            losses.append(float(eng.LOSS.item()))
-        eng.flush_optimizer()
-        torch.cuda.synchronize()
-        res.append((losses, eng.LOGP.clone(), eng.G32.clone(), eng.P32.clone(), eng.M.clone(), eng.VMAX.clone()))
-    assert res[0][0] == res[1][0]
-    for a, b in zip(res[0][1:], res[1][1:]):
-        assert torch.equal(a, b)
-
-
 def test_engine_matches_oracle_at_384(cuda, pkg, parity_report):
     """The step at 384 x 384 images (R50: a 12 x 12 layer4 map, so SGA block 0 attends over
     144 vision tokens -- the 5-key-tile attention kernels) against the fp32 oracle, one
