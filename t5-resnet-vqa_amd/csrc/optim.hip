@@ -9,7 +9,7 @@
 //   3. vqa_adamw_amsgrad  one fused HBM pass over p, g, m, v, vmax -> p, m, v,
 //                         vmax and the bf16 shadow copy used by the GEMMs.
 // The DP average (1/world) enters as grad_scale in steps 2 and 3.
-#include "common.h"
+#include "adamw.h"
 
 namespace {
 
@@ -68,14 +68,6 @@ __global__ void finalize_kernel(const double* __restrict__ ws, int parts, float 
   st[VQA_ST_PENDING] = 1.f;
 }
 
-struct AdamArgs {
-  float* p; const float* g; float* m; float* v; float* vm; bf16_t* p16;
-  long n4;
-  int ngroups; long gend4[VQA_MAX_GROUPS]; float glr[VQA_MAX_GROUPS];
-  float b1, b2, eps, wd, gscale;
-  const float* st;
-};
-
 // One float4 of every stream per thread, no grid-stride loop: 138k blocks of
 // 256 keep ~2k threads x 5 x 16 B of loads in flight per CU.  Every stream is
 // touched once per step (5.4 GB >> the 256 MiB Infinity Cache), so loads and
@@ -83,30 +75,12 @@ struct AdamArgs {
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs A) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= A.n4 || A.st[VQA_ST_PENDING] == 0.f) return;   // nothing to apply (see VQA_ST_PENDING)
-  const float coef = A.st[VQA_ST_CLIP_COEF], lam = A.st[VQA_ST_LR_SCALE];
-  const float bc1 = A.st[VQA_ST_BC1], bc2s = A.st[VQA_ST_BC2_SQRT];
-  const float gmul = A.gscale * coef;
-  const float omb1 = 1.f - A.b1, omb2 = 1.f - A.b2;
-  int gi = 0;
-#pragma unroll
-  for (int k = 0; k < VQA_MAX_GROUPS - 1; ++k) gi += (k < A.ngroups - 1 && i >= A.gend4[k]) ? 1 : 0;
-  const float lr = A.glr[gi] * lam;
-  const float decay = 1.f - lr * A.wd, step_size = lr / bc1;
   f32x4_t p = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.p) + i);
   const f32x4_t g4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.g) + i);
   f32x4_t m = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.m) + i);
   f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.v) + i);
   f32x4_t vm = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.vm) + i);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float gr = g4[j] * gmul;
-    p[j] *= decay;                                      // decoupled weight decay
-    m[j] = m[j] + omb1 * (gr - m[j]);                   // exp_avg.lerp_(grad, 1-beta1)
-    v[j] = v[j] * A.b2 + omb2 * gr * gr;                // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-    vm[j] = fmaxf(vm[j], v[j]);                         // amsgrad running max
-    const float denom = sqrtf(vm[j]) / bc2s + A.eps;
-    p[j] = p[j] - step_size * (m[j] / denom);
-  }
+  adamw_update4(A, i, p, g4, m, v, vm);
   __builtin_nontemporal_store(p, reinterpret_cast<f32x4_t*>(A.p) + i);
   __builtin_nontemporal_store(m, reinterpret_cast<f32x4_t*>(A.m) + i);
   __builtin_nontemporal_store(v, reinterpret_cast<f32x4_t*>(A.v) + i);
@@ -141,21 +115,8 @@ extern "C" int vqa_optim_finalize(const double* ws, int parts, float grad_scale,
 }
 
 extern "C" int vqa_adamw_amsgrad(const vqa_adamw_desc* d, hipStream_t s) {
-  VQA_REQUIRE(d && d->param && d->grad && d->exp_avg && d->exp_avg_sq && d->max_exp_avg_sq && d->state,
-              "vqa_adamw_amsgrad: null argument");
-  VQA_REQUIRE(d->n % 4 == 0 && d->ngroups >= 1 && d->ngroups <= VQA_MAX_GROUPS, "vqa_adamw_amsgrad: bad sizes");
   AdamArgs A;
-  A.p = d->param; A.g = d->grad; A.m = d->exp_avg; A.v = d->exp_avg_sq; A.vm = d->max_exp_avg_sq;
-  A.p16 = (bf16_t*)d->param16;
-  A.n4 = d->n / 4;
-  A.ngroups = d->ngroups;
-  for (int i = 0; i < VQA_MAX_GROUPS; ++i) {
-    VQA_REQUIRE(i >= d->ngroups || d->group_end[i] % 4 == 0, "vqa_adamw_amsgrad: group ends must be multiples of 4");
-    A.gend4[i] = i < d->ngroups ? d->group_end[i] / 4 : A.n4;
-    A.glr[i] = i < d->ngroups ? d->group_lr[i] : 0.f;
-  }
-  A.b1 = d->beta1; A.b2 = d->beta2; A.eps = d->eps; A.wd = d->weight_decay; A.gscale = d->grad_scale;
-  A.st = d->state;
+  if (int rc = adam_args(d, A)) return rc;
   hipLaunchKernelGGL(adamw_kernel, dim3(vqa::cdiv(A.n4, 256)), dim3(256), 0, s, A);
   return vqa::check_launch("vqa_adamw_amsgrad");
 }
