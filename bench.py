@@ -90,7 +90,7 @@ def calls_flop(eng, fp8_only=False):
         if c.name == "vqa_gemm":
             d = c.desc
             tot += 2.0 * d.m * d.n * d.k * max(1, d.batch)
-        elif c.name in ("vqa_gemm_pair", "vqa_conv_pair"):
+        elif c.name == "vqa_gemm_pair":
             tot += sum(2.0 * d.m * d.n * d.k for d in c.desc)
         elif c.name in ("vqa_attn_fwd", "vqa_attn_bwd"):
             d = c.desc

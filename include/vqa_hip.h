@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 14
+#define VQA_ABI_VERSION 13
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -164,13 +164,6 @@ long long vqa_gemm_workspace_bytes(const vqa_gemm_desc* d);
  * conv.  Each keeps its own epilogue and tile config (configs 3, 4, 6, 7; others
  * map to 4).  Any other pair of descriptors runs as two vqa_gemm calls. */
 int vqa_gemm_pair(const vqa_gemm_desc* dx, const vqa_gemm_desc* dw, hipStream_t stream);
-/* The frozen ResNet's bottleneck seam as ONE launch (resnet_vqa_model.py:126-132, torchvision
- * Bottleneck): `ex` = block i's 1x1 expansion (bias, bf16 residual, ReLU; c16 = Y, block i+1's
- * residual), `rd` = block i+1's 1x1 reduction reading rd->a == ex->c16 (Y).  Both plain
- * k-contiguous GEMMs, batch 1; ex->n a multiple of 64, rd->n 64 or 128.  Y is still written;
- * the reduction reads each 64-channel chunk of it back from L2 right after computing it
- * instead of re-reading all of Y from HBM.  Bit-identical to vqa_gemm(ex); vqa_gemm(rd). */
-int vqa_conv_pair(const vqa_gemm_desc* ex, const vqa_gemm_desc* rd, hipStream_t stream);
 
 /* ------------------------------------------------------------- attention ---
  * Multi-head attention core for Lq, Lk <= 64 (one workgroup per (b, head)):

@@ -53,34 +53,6 @@ __global__ __launch_bounds__(256) void gemm_pair_kernel(GemmParams P1, GemmParam
   }
 }
 
-// Bottleneck seam of the frozen ResNet in ONE launch (resnet_vqa_model.py:126-132, torchvision
-// Bottleneck.forward): block i's 1x1 expansion + bias + residual + ReLU (Y = relu(A W3^T + b3 +
-// res), which block i+1 keeps as its residual) and block i+1's 1x1 reduction (Z = relu(Y W1^T +
-// b1)).  One workgroup = 64 rows: the expansion tile spans ALL of Y's columns (stored by its
-// epilogue), then the reduction tile of the same rows streams those rows of Y back from L2
-// (this workgroup just wrote them) instead of re-reading Y from HBM in a second launch.  Two
-// gemm_body passes over the same row tile (both grids are one tile wide, so the XCD remap
-// gives both the same rows); same K order as the two separate GEMMs: bit-identical.
-template <int NOUT, int NWN1, int NP>
-struct PairCfg {
-  static constexpr int L1 = TileCfg<64, NOUT, 2>::LDS, L2 = TileCfg<64, NP, 2>::LDS;
-  static constexpr int LDS = L1 > L2 ? L1 : L2;
-  static constexpr int NT = 64 * 2 * NWN1;                 // threads (the expansion's 2 x NWN1 waves)
-};
-
-template <int NOUT, int NWN1, int NP>
-__global__ __launch_bounds__(128 * NWN1) void conv_pair_kernel(GemmParams P3, GemmParams P1) {
-  __shared__ __attribute__((aligned(1024))) char smem[PairCfg<NOUT, NWN1, NP>::LDS];
-  gemm_body<64, NOUT, 2, 2, NWN1, true, true, false, false>(P3, blockIdx.x, smem);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's Y stores have left
-  __syncthreads();                                        // ... every wave's; the ring is free
-  if constexpr (2 * NWN1 == 4) {
-    gemm_body<64, NP, 2, 2, 2, true, true, false, false>(P1, blockIdx.x, smem);
-  } else {                                                // 8 waves: the reduction tile as 2 x 4 waves
-    gemm_body<64, NP, 2, 2, 4, true, true, false, false>(P1, blockIdx.x, smem);
-  }
-}
-
 // config: 0 = auto; 1 = 128x128 (3 stages); 2 = 128x64 (4); 3 = 64x64 (4); 4 = 64x64 (2);
 //         5 = 64x64 (3); 6 = 128x64 (2); 7 = 64x128 (2); 8 = 128x128 (2)  -- 4 waves (2x2);
 //         9 = 256x128 (2, 8 waves 4x2); 10 = 128x256 (2, 8 waves 2x4); 11 = 256x256 (2, 8 waves 2x4);
@@ -315,29 +287,6 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   if (!akc && !bkc && d->b_conv) return dispatch_tile<false, false, false, true>(P, batch, cfg, stream);
   if (!akc && bkc) return dispatch_tile<false, true, false, false>(P, batch, cfg, stream);
   return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: unsupported layout combination");
-}
-
-extern "C" int vqa_conv_pair(const vqa_gemm_desc* ex, const vqa_gemm_desc* rd, hipStream_t stream) {
-  GemmParams P3, P1;
-  if (int rc = prepare(ex, P3)) return rc;
-  if (int rc = prepare(rd, P1)) return rc;
-  auto plain = [](const vqa_gemm_desc* d) {
-    return !d->a_trans && !d->b_trans && !d->a_conv && !d->b_conv && d->batch == 1 && d->splitk <= 1 && !d->fp8 &&
-           !d->rownorm;
-  };
-  VQA_REQUIRE(plain(ex) && plain(rd) && ex->m == rd->m && ex->c16 && rd->a == ex->c16 && rd->lda == ex->ldc16 &&
-                  rd->k == ex->n && P3.vec && P1.vec && rd->c16,
-              "vqa_conv_pair: the reduction must read the expansion's bf16 output (plain k-contiguous 1x1 GEMMs)");
-  const bool l1 = ex->n == 256 && rd->n == 64, l1b = ex->n == 256 && rd->n == 128, l2 = ex->n == 512 && rd->n == 128;
-  VQA_REQUIRE(l1 || l1b || l2, "vqa_conv_pair: expansion / reduction widths %d / %d (256 / 64, 256 / 128, 512 / 128)",
-              ex->n, rd->n);
-  P3.tiles_m = P1.tiles_m = vqa::cdiv(ex->m, 64);
-  P3.tiles_n = P1.tiles_n = 1;
-  const dim3 grid(P3.tiles_m);
-  if (l1) hipLaunchKernelGGL((conv_pair_kernel<256, 2, 64>), grid, dim3(256), 0, stream, P3, P1);
-  else if (l1b) hipLaunchKernelGGL((conv_pair_kernel<256, 2, 128>), grid, dim3(256), 0, stream, P3, P1);
-  else hipLaunchKernelGGL((conv_pair_kernel<512, 4, 128>), grid, dim3(512), 0, stream, P3, P1);
-  return vqa::check_launch("vqa_conv_pair");
 }
 
 namespace {

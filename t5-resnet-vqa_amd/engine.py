@@ -146,7 +146,7 @@ class VQAEngine:
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0, pipeline=False,
                  t5_dw_group=None, defer_optimizer=True, dw_stream=None, sga_dw_batch=True, pair_bwd=True,
-                 language_model="t5-base", fp8=False, conv_pair=True):
+                 language_model="t5-base", fp8=False):
         L.load()
         # pipeline: the frozen ResNet (no trainable input) of the NEXT batch runs on its own
         # stream beside this step's T5 / SGA / backward / optimizer (see train_step)
@@ -166,9 +166,6 @@ class VQAEngine:
         # configs[4] "fp8 MFMA weights"): weights and their input activations quantised row-wise
         # (vqa_quant_rows_fp8), the backward on the bf16 shadows / saved bf16 activations
         self.fp8 = bool(fp8)
-        # frozen ResNet: each bottleneck's 1x1 expansion and the next block's 1x1 reduction as ONE
-        # launch (vqa_conv_pair: the reduction reads the expansion's output chunk by chunk from L2)
-        self.conv_pair = bool(conv_pair)
         # the answer head's log-softmax keeps one sample's answer logits in registers (head.hip:
         # A <= 1024; DAQUAR has 170) and the pooler one sample's tokens (L <= 64)
         if not 1 <= answer_spaces <= 1024:
@@ -353,32 +350,8 @@ class VQAEngine:
             self._conv(last_in, (B, last_h, last_h, last_c), w3, b3, 1, 1 if k3 == 3 else 0, y, relu=True,
                        res16=res)
             if y is not self.F4N:
-                # next block: t1 <- this block's t1 (not x: vqa_conv_pair writes the next block's
-                # conv1 output while other tiles still read this block's x as their residual,
-                # and a [M, planes] buffer over a [M, 4 planes] one overlaps other tiles' rows)
-                free = [t1, x, t2, ds]
+                free = [x, t1, t2, ds]
                 x = y
-        if self.conv_pair:
-            self.res_calls = self._pair_bottleneck_seams(self.res_calls)
-
-    @staticmethod
-    def _pair_bottleneck_seams(calls):
-        """Fuse every (1x1 expansion with a residual, next block's 1x1 reduction of its output)
-        pair of adjacent ResNet calls into one vqa_conv_pair launch (bit-identical)."""
-        out, i = [], 0
-        while i < len(calls):
-            a = calls[i]
-            b = calls[i + 1] if i + 1 < len(calls) else None
-            if (b is not None and a.name == b.name == "vqa_gemm" and a.desc.res16 and not a.desc.a_conv
-                    and not b.desc.a_conv and b.desc.a == a.desc.c16 and b.desc.k == a.desc.n
-                    and (a.desc.n, b.desc.n) in ((256, 64), (256, 128), (512, 128))):
-                out.append(ops.Call("vqa_conv_pair", ctypes.byref(a.desc), ctypes.byref(b.desc),
-                                    keep=tuple(a.keep) + tuple(b.keep), desc=(a.desc, b.desc)))
-                i += 2
-            else:
-                out.append(a)
-                i += 1
-        return out
 
     def _conv(self, x, shape, w16, b32, stride, pad, out, relu, res16=None):
         n, h, w, c = shape

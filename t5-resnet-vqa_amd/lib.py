@@ -141,7 +141,6 @@ def load():
     lib.vqa_gemm_workspace_bytes.argtypes = [ctypes.POINTER(GemmDesc)]
     lib.vqa_gemm_workspace_bytes.restype = c_ll
     lib.vqa_gemm_pair.argtypes = [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc), c_void_p]
-    lib.vqa_conv_pair.argtypes = [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc), c_void_p]
     lib.vqa_attn_fwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_attn_bwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_attn_path.argtypes = [ctypes.POINTER(AttnDesc), c_int]

@@ -293,26 +293,6 @@ def test_dw_stream_matches_single_stream_bitwise(cuda, pkg):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("H", [64, 224])
-def test_resnet_conv_pair_is_bit_identical(cuda, pkg, H):
-    """The frozen ResNet with each bottleneck seam (1x1 expansion + residual + ReLU, the next
-    block's 1x1 reduction) as one vqa_conv_pair launch (the default) gives the layer4 map of the
-    separate launches bit for bit."""
-    import torch
-    B = 2
-    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
-    img = torch.as_tensor(pkg.synthetic.make_batch(B, 32, H, seed=3)["image_tensors"]).cuda()
-    maps = []
-    for pair in (True, False):
-        eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=32, image_size=H, pipeline=True, conv_pair=pair)
-        n = sum(c.name == "vqa_conv_pair" for c in eng.res_calls)
-        assert n == (6 if pair else 0), n                  # layer1: 3 seams, layer2: 3 (+1 into layer3 at n 256: no)
-        eng.prime(img)
-        torch.cuda.synchronize()
-        maps.append(eng.F4N.clone())
-    assert torch.equal(maps[0], maps[1])
-
-
 def test_engine_matches_oracle_at_384(cuda, pkg, parity_report):
     """The step at 384 x 384 images (R50: a 12 x 12 layer4 map, so SGA block 0 attends over
     144 vision tokens -- the 5-key-tile attention kernels) against the fp32 oracle, one
