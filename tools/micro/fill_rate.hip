@@ -81,6 +81,63 @@ __global__ __launch_bounds__(64 * NW) void fill_reg(const char* __restrict__ src
   if (acc == 12345.f) out[blockIdx.x] = acc;
 }
 
+// no workgroup barrier: every wave streams its OWN slice of each tile into its own ring and
+// waits only for its own LDS-DMA (vmcnt) -- what the per-slot barrier of the GEMM ring costs
+template <int BYTES, int NW, int STAGES>
+__global__ __launch_bounds__(64 * NW) void fill_glds_nobar(const char* __restrict__ src, long span, int tiles, float* out) {
+  __shared__ __attribute__((aligned(1024))) char ring[STAGES * BYTES];
+  constexpr int NI = BYTES / (1024 * NW);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const long base = ((long)blockIdx.x * 7919 * BYTES) % span;
+  auto issue = [&](int t) {
+    char* st = ring + (t % STAGES) * BYTES;
+    const long off = (base + (long)t * BYTES) % span;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const char* g = src + off + (long)((w * NI + j) * 1024 + l * 16);
+      __builtin_amdgcn_global_load_lds(g, (lds_void_t*)(st + (w * NI + j) * 1024), 16, 0, 0);
+    }
+  };
+  for (int s = 0; s < STAGES - 1; ++s) issue(s);
+  float acc = 0.f;
+  for (int t = 0; t < tiles; ++t) {
+    if constexpr (STAGES >= 3) {
+      if (t + 1 < tiles) wait_vm<(STAGES - 2) * NI>(); else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    acc += *reinterpret_cast<volatile float*>(ring + (t % STAGES) * BYTES + (w * NI) * 1024 + l * 4);
+    if (t + STAGES - 1 < tiles) issue(t + STAGES - 1);
+  }
+  if (acc == 12345.f) out[blockIdx.x] = acc;
+}
+
+// register loads with many in flight per lane (no LDS): NI 16-B loads per lane per tile, one
+// tile ahead, summed so nothing is dead
+template <int BYTES, int NW>
+__global__ __launch_bounds__(64 * NW) void fill_reg_deep(const char* __restrict__ src, long span, int tiles, float* out) {
+  constexpr int NI = BYTES / (1024 * NW);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const long base = ((long)blockIdx.x * 7919 * BYTES) % span;
+  float acc = 0.f;
+  uint4 r[2][NI];
+  auto load = [&](int t, uint4 (&d)[NI]) {
+    const long off = (base + (long)t * BYTES) % span;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) d[j] = *reinterpret_cast<const uint4*>(src + off + (long)((w * NI + j) * 1024 + l * 16));
+  };
+  load(0, r[0]);
+  for (int t = 0; t < tiles; t += 2) {
+    if (t + 1 < tiles) load(t + 1, r[1]);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc += __uint_as_float(r[0][j].x);
+    if (t + 2 < tiles) load(t + 2, r[0]);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc += __uint_as_float(r[1][j].x);
+  }
+  if (acc == 12345.f) out[blockIdx.x] = acc;
+}
+
 template <typename K>
 float timeit(K k, int grid, int block, const char* src, long span, int tiles, float* out) {
   hipEvent_t a, b;
@@ -109,6 +166,14 @@ int main() {
     printf("%-34s grid %4d  %7.1f us  %6.1f GB/s per WG  %6.2f TB/s chip\n", tag, grid, ms * 1e3, tot / grid / (ms * 1e-3) / 1e9,
            tot / (ms * 1e-3) / 1e12);
   };
+  for (int grid : {256, 512}) {
+    rep("glds-nobar 16K 4 waves 2 stages", timeit(fill_glds_nobar<16384, 4, 2>, grid, 256, src, span, tiles, out), grid, 16384);
+    rep("glds-nobar 16K 4 waves 4 stages", timeit(fill_glds_nobar<16384, 4, 4>, grid, 256, src, span, tiles, out), grid, 16384);
+    rep("glds-nobar 32K 4 waves 4 stages", timeit(fill_glds_nobar<32768, 4, 4>, grid, 256, src, span, tiles, out), grid, 32768);
+    rep("reg-deep 16K 4 waves (4/lane x2)", timeit(fill_reg_deep<16384, 4>, grid, 256, src, span, tiles, out), grid, 16384);
+    rep("reg-deep 32K 4 waves (8/lane x2)", timeit(fill_reg_deep<32768, 4>, grid, 256, src, span, tiles, out), grid, 32768);
+    rep("reg-deep 32K 8 waves (4/lane x2)", timeit(fill_reg_deep<32768, 8>, grid, 512, src, span, tiles, out), grid, 32768);
+  }
   for (int grid : {256, 384, 512}) {
     rep("glds 32K 4 waves 2 stages", timeit(fill_glds<32768, 4, 2>, grid, 256, src, span, tiles, out), grid, 32768);
     rep("glds 48K 4 waves 2 stages", timeit(fill_glds<49152, 4, 2>, grid, 256, src, span, tiles, out), grid, 49152);
