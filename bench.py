@@ -223,6 +223,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-kernel-rooflines", action="store_true", help="skip the per-kernel replays after the timed region")
+    ap.add_argument("--shard-optimizer", action="store_true",
+                    help="N > 1: reduce-scatter + sharded AdamW + all-gather instead of the bucketed all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run the frozen ResNet inside each step instead of beside the previous one")
     ap.add_argument("--tune-table", default=os.path.join(ROOT, "t5-resnet-vqa_amd", "tuning", "gemm_gfx950.json"),
@@ -291,7 +293,7 @@ def main():
     eng.backward()
     eng.autotune(table=args.tune_table, save=args.tune_save if rank == 0 else None)   # tile choice: speed only
     if world > 1:
-        dps = pkg.dp.DataParallelStep(eng, use_graph=not args.no_graph)
+        dps = pkg.dp.DataParallelStep(eng, use_graph=not args.no_graph, shard_optimizer=args.shard_optimizer)
         run_step = dps.step
     else:
         if not args.no_graph:

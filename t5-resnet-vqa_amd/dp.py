@@ -57,9 +57,33 @@ def plan_buckets(ready_marks, end, min_bytes=24 << 20):
     return out
 
 
+def plan_shards(buckets, world, align=64):
+    """Sharded optimizer (DataParallelStep(shard_optimizer=True)): each bucket [a, b) is cut
+    into `world` equal chunks of a multiple of `align` elements, chunk r owned by rank r (its
+    reduce-scatter target and the slice of the AdamW update it runs), plus a remainder
+    [a + world*chunk, b) shorter than world*align that every rank all-reduces and updates.
+    Returns [(a, chunk, b)] (chunk may be 0: the whole bucket is remainder)."""
+    out = []
+    for _, a, b in buckets:
+        chunk = (b - a) // (world * align) * align
+        out.append((a, chunk, b))
+    return out
+
+
 class _Done:
     """A completed collective (host-staged gloo path): wait() is a no-op."""
     def wait(self):
+        return True
+
+
+class _All:
+    """Several collectives of one bucket waited on as one (the sharded exchange)."""
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
         return True
 
 
@@ -103,10 +127,12 @@ def gather_rows(ids, rows, out_ids, out_rows, group=None):
 
 
 class DataParallelStep:
-    def __init__(self, engine, group=None, bucket_mb=24, use_graph=True):
+    def __init__(self, engine, group=None, bucket_mb=24, use_graph=True, shard_optimizer=False):
         import torch.distributed as dist
         self.eng, self.group = engine, group
         self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.shard = bool(shard_optimizer)
         e = engine
         e.set_grad_scale(1.0 / self.world)
         emb = e.lay["t5.embed"]
@@ -132,6 +158,8 @@ class DataParallelStep:
         self.emb_call = ops.Call("vqa_embedding_bwd", self.GIDS.data_ptr(), self.GDH.data_ptr(),
                                  e.g32["t5.embed"].data_ptr(), self.world * T, D, S.T5_VOCAB, self.WS.data_ptr(),
                                  keep=(self.GIDS, self.GDH, self.WS, e.g32["t5.embed"]))
+        if self.shard:
+            self._plan_sharded_optimizer()
         self.graphs = None
         # exposed-communication timing (bench at N > 1): HIP events on the compute stream right
         # before and after each collective's wait, i.e. how long the step's stream stalls on it
@@ -143,6 +171,110 @@ class DataParallelStep:
         # zero-rows call only clears the PREVIOUS step's gathered ids (GIDS), so clear rows that
         # local backward passes (warm-ups, a train_step before this object) left behind
         e.g32["t5.embed"].zero_()
+
+    def _plan_sharded_optimizer(self):
+        """Reduce-scatter + sharded AdamW + all-gather (ZeRO stage 1):
+        the buckets' gradients are reduce-scattered instead of all-reduced, rank r runs the
+        clip-scaled AdamW-amsgrad on its chunk of every bucket only (m, v, vmax of other chunks
+        are never touched here), and the updated fp32 masters and bf16 shadows of the chunks are
+        all-gathered.  The remainders of the buckets and the embedding table (whose gradient rows
+        every rank rebuilds identically) are updated by every rank.  The clip norm is the sum
+        of per-range squared-norm partials, all-reduced (each owned chunk counted by its owner,
+        the replicated ranges by rank 0 only), then finalized as usual."""
+        e = self.eng
+        self.shards = plan_shards(self.buckets, self.world)
+        n, emb = e.lay.total, e.lay["t5.embed"].offset
+        r, N = self.rank, self.world
+        own = [(a + r * c, a + (r + 1) * c) for a, c, b in self.shards if c > 0]
+        rep = [(a + N * c, b) for a, c, b in self.shards if b > a + N * c] + [(emb, n)]
+        K = e.SQ_PARTS
+        ranges = own + rep
+        self.WS_SQN = torch.zeros(len(ranges) * K, dtype=torch.float64, device=e.dev)
+        sq = []
+        for i, (lo, hi) in enumerate(ranges):
+            if i < len(own) or r == 0:                      # a replicated range is counted once
+                sq.append(ops.Call("vqa_grad_sqnorm", ops.addr(e.G32, lo), hi - lo, ops.addr(self.WS_SQN, i * K), K,
+                                   keep=(e.G32, self.WS_SQN)))
+        self.sq_calls = sq
+        fin = []
+        e._call(fin, "vqa_optim_finalize", self.WS_SQN, len(ranges) * K, float(e.grad_scale), float(e.max_norm),
+                int(e.warmup), int(e.total), float(e.betas[0]), float(e.betas[1]), e.opt_state)
+        self.finalize_call = fin[0]
+        self.adam_calls = [e.adam_range_call(lo, hi) for lo, hi in ranges]
+
+    def _sharded_collectives_after(self, bk_index):
+        """Reduce-scatter of bucket `bk_index`'s chunks (owner r receives the sum of chunk r)
+        and all-reduce of its remainder; returns the works."""
+        import torch.distributed as dist
+        e = self.eng
+        a, c, b = self.shards[bk_index]
+        N, r = self.world, self.rank
+        works = []
+        if c > 0:
+            full, mine = e.G32[a:a + N * c], e.G32[a + r * c:a + (r + 1) * c]
+            if _staged(full, self.group) or dist.get_backend(self.group) == "gloo":
+                h = full.cpu()                              # gloo: all-reduce, keep the own chunk
+                dist.all_reduce(h, group=self.group)
+                mine.copy_(h[r * c:(r + 1) * c])
+                works.append(_Done())
+            else:
+                works.append(dist.reduce_scatter_tensor(mine, full, group=self.group, async_op=True))
+        if b > a + N * c:
+            works += allreduce_buckets(e.G32, [(None, a + N * c, b)], self.group)
+        return [_All(works)]
+
+    def _sharded_optimizer(self):
+        """sqnorm partials -> all-reduce -> finalize -> AdamW on the own chunks + the replicated
+        ranges -> clear the pending flag (the forward's deferred ranges then do nothing) ->
+        all-gather the chunks' fp32 masters and bf16 shadows."""
+        import torch.distributed as dist
+        e = self.eng
+        s = L.stream_handle()
+        self.WS_SQN.zero_()
+        for c in self.sq_calls:
+            c(s)
+        if _staged(self.WS_SQN, self.group):
+            h = self.WS_SQN.cpu()
+            dist.all_reduce(h, group=self.group)
+            self.WS_SQN.copy_(h)
+        else:
+            dist.all_reduce(self.WS_SQN, group=self.group)
+        self.finalize_call(s)
+        for c in self.adam_calls:
+            c(s)
+        e.clear_pending(s)
+        N, r = self.world, self.rank
+        for a, c, b in self.shards:
+            if c == 0:
+                continue
+            for t in (e.P32, e.P16):
+                full, mine = t[a:a + N * c], t[a + r * c:a + (r + 1) * c]
+                if _staged(full, self.group):
+                    parts = [torch.empty(c, dtype=t.dtype) for _ in range(N)]
+                    dist.all_gather(parts, mine.cpu(), group=self.group)
+                    full.copy_(torch.cat(parts))
+                else:
+                    dist.all_gather_into_tensor(full, mine.clone(), group=self.group)
+
+    def sync_optimizer_state(self):
+        """Sharded optimizer: all-gather the AdamW moments of every chunk (each rank holds only
+        its own chunks' up-to-date m, v, vmax) so optimizer_state() / checkpoints see them."""
+        import torch.distributed as dist
+        if not self.shard:
+            return
+        e = self.eng
+        N, r = self.world, self.rank
+        for a, c, b in self.shards:
+            if c == 0:
+                continue
+            for t in (e.M, e.V, e.VMAX):
+                full, mine = t[a:a + N * c], t[a + r * c:a + (r + 1) * c]
+                if _staged(full, self.group):
+                    parts = [torch.empty(c, dtype=t.dtype) for _ in range(N)]
+                    dist.all_gather(parts, mine.cpu(), group=self.group)
+                    full.copy_(torch.cat(parts))
+                else:
+                    dist.all_gather_into_tensor(full, mine.clone(), group=self.group)
 
     def _run(self, calls):
         s = L.stream_handle()
@@ -212,34 +344,42 @@ class DataParallelStep:
     def step(self):
         e = self.eng
         self._res_begin()
+        exchange = (lambda i, bk: self._sharded_collectives_after(i)) if self.shard else \
+            (lambda i, bk: allreduce_buckets(e.G32, [bk], self.group))
         if self.graphs is None:
             e.forward()
             works = []
-            for seg, bk in zip(self.segments, self.buckets):
+            for i, (seg, bk) in enumerate(zip(self.segments, self.buckets)):
                 self._run(seg)
-                works += allreduce_buckets(e.G32, [bk], self.group)
+                works += exchange(i, bk)
             works += gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
             for w in works[-2:]:
                 w.wait()
             self._run(self.tail + [self.emb_call])
             for w in works[:-2]:
                 w.wait()
-            self._run(e.opt_calls)
+            if self.shard:
+                self._sharded_optimizer()
+            else:
+                self._run(e.opt_calls)
             self._res_end()
             return
         g = self.graphs
         g["fwd"][0].replay()
         works = []
-        for seg, bk in zip(g["seg"], self.buckets):
+        for i, (seg, bk) in enumerate(zip(g["seg"], self.buckets)):
             seg.replay()
-            works += allreduce_buckets(e.G32, [bk], self.group)
+            works += exchange(i, bk)
         works += gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
         evs = []
         self._wait(works[-2:], evs)                         # the embedding rows: needed by the tail
         g["tail"][0].replay()
         for w in works[:-2]:
             self._wait([w], evs)
-        g["opt"][0].replay()
+        if self.shard:
+            self._sharded_optimizer()
+        else:
+            g["opt"][0].replay()
         self._res_end()
         if self.timing:
             self._ev.append(evs)

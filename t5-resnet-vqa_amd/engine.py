@@ -1092,6 +1092,21 @@ class VQAEngine:
         elif self.adam_embed is not None:
             o.append(self.adam_embed)
 
+    def adam_range_call(self, lo, hi):
+        """The fused AdamW-amsgrad pass over flat parameters [lo, hi) only (the step's device
+        state: clip coefficient, schedule, bias corrections; no-op unless an update is pending)."""
+        d = self._adam_desc
+        ds = L.AdamWDesc()
+        ctypes.memmove(ctypes.addressof(ds), ctypes.addressof(d), ctypes.sizeof(d))
+        ds.param, ds.grad = ops.addr(self.P32, lo), ops.addr(self.G32, lo)
+        ds.exp_avg, ds.exp_avg_sq = ops.addr(self.M, lo), ops.addr(self.V, lo)
+        ds.max_exp_avg_sq, ds.param16 = ops.addr(self.VMAX, lo), ops.addr(self.P16, lo)
+        ds.n = hi - lo
+        for i in range(d.ngroups):
+            ds.group_end[i] = d.group_end[i] - lo
+        return ops.Call("vqa_adamw_amsgrad", ctypes.byref(ds), desc=ds,
+                        keep=(self.P32, self.G32, self.M, self.V, self.VMAX, self.P16, self.opt_state))
+
     def flush_optimizer(self):
         """Apply a deferred AdamW update now (before reading the parameters outside a step)."""
         if self.defer_opt:

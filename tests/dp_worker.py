@@ -2,10 +2,11 @@
 the gloo backend (several ranks share the one GPU of the test box; RCCL refuses two ranks
 on one device).  Rank r trains on samples [r*B, (r+1)*B) of each global batch.
 
-  python tests/dp_worker.py RANK WORLD PORT OUT.npz STEPS PIPELINE GRAPH [trainer]
+  python tests/dp_worker.py RANK WORLD PORT OUT.npz STEPS PIPELINE GRAPH [trainer|shard]
 
 `trainer`: drive the step through model.ResnetVQAModel + trainer.VQATrainer (data_parallel
-picked up from the initialised process group) instead of the engine directly."""
+picked up from the initialised process group) instead of the engine directly; `shard`: the
+engine step with the sharded optimizer (reduce-scatter, AdamW on the own chunks, all-gather)."""
 import os
 import sys
 
@@ -43,7 +44,8 @@ def main():
         eng.load_batch(dev[0], next_images=dev[1]["image_tensors"])
     else:
         eng.load_batch(dev[0])
-    step = pkg.dp.DataParallelStep(eng, bucket_mb=8, use_graph=graph)
+    shard = len(sys.argv) > 8 and sys.argv[8] == "shard"
+    step = pkg.dp.DataParallelStep(eng, bucket_mb=8, use_graph=graph, shard_optimizer=shard)
     if pipe:
         eng.prime(dev[0]["image_tensors"])
     losses, norms = [], []
@@ -58,13 +60,15 @@ def main():
         losses.append(float(eng.LOSS.item()))
         norms.append(eng.last_grad_norm())
     eng.flush_optimizer()
+    step.sync_optimizer_state()                         # sharded: every chunk's moments on every rank
     torch.cuda.synchronize()
     rep = step.timing_report()
     if graph:                                           # one wait per bucket + the row gather
         assert rep["steps"] == steps and len(rep["buckets"]) == len(step.buckets), rep
         assert all(b["exposed_wait_us"] >= 0.0 for b in rep["buckets"]), rep
     np.savez(out, losses=np.array(losses), norms=np.array(norms), p32=eng.P32.cpu().numpy(),
-             g32=eng.G32.cpu().numpy())
+             g32=eng.G32.cpu().numpy(), m=eng.M.cpu().numpy(), vmax=eng.VMAX.cpu().numpy(),
+             p16=eng.P16.float().cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()
 

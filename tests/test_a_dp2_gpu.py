@@ -111,3 +111,25 @@ def test_trainer_data_parallel_two_ranks(gpu, pkg, tmp_path, parity_report):
                 np.linalg.norm(ref["p32"].astype(np.float64) - p0))
     parity_report["dp2_trainer"]["update_rel_l2"] = upd
     assert upd <= 5e-2, upd
+
+
+def test_dp_sharded_optimizer_matches_allreduce(gpu, tmp_path, parity_report):
+    """DataParallelStep(shard_optimizer=True): reduce-scatter of the gradient buckets, AdamW on
+    each rank's chunks only, all-gather of the fp32 masters and bf16 shadows.  The ranks stay
+    bitwise in lockstep (parameters, shadows, gathered moments), and the result equals the
+    all-reduce step's: the gradients are the same sums, only the clip norm's partial sums are
+    grouped differently (fp64), so parameters agree to fp32 rounding."""
+    world, steps = 2, 3
+    ref = _ranks(tmp_path, world, steps, False, True)
+    shd = _ranks(tmp_path, world, steps, False, True, mode="shard")
+    for r in shd[1:]:
+        for k in ("p32", "p16", "m", "vmax", "norms"):
+            assert np.array_equal(r[k], shd[0][k]), f"sharded ranks diverged in {k}"
+    assert np.array_equal(shd[0]["losses"], ref[0]["losses"]) or \
+        np.abs(shd[0]["losses"] - ref[0]["losses"]).max() <= 1e-6 * np.abs(ref[0]["losses"]).max()
+    dn = float(np.abs(shd[0]["norms"] - ref[0]["norms"]).max() / np.abs(ref[0]["norms"]).max())
+    dp = float(np.abs(shd[0]["p32"].astype(np.float64) - ref[0]["p32"]).max() /
+               np.abs(ref[0]["p32"]).max())
+    dm = float(np.abs(shd[0]["m"].astype(np.float64) - ref[0]["m"]).max() / np.abs(ref[0]["m"]).max())
+    parity_report["dp2_sharded_vs_allreduce"] = {"grad_norm_rel": dn, "p32_max_rel": dp, "exp_avg_max_rel": dm}
+    assert dn <= 1e-6 and dp <= 1e-6 and dm <= 1e-5, (dn, dp, dm)

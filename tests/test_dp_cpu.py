@@ -51,6 +51,26 @@ def test_plan_buckets_cover_prefix(pkg):
     assert sum(b - a for _, a, b in bks) == emb
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_plan_shards_partition_the_prefix(pkg, world):
+    """Sharded optimizer plan: per bucket, world equal 64-aligned owned chunks + a remainder
+    shorter than world * 64; the owned chunks of all ranks and the remainders tile [0, emb)."""
+    lay = pkg.layout.ParamLayout("resnet50")
+    emb = lay["t5.embed"].offset
+    names = ["pool_b", "sga2.m1_b", "scaler_b", "t5.final_ln"] + \
+        [f"t5.{i}.ln1" for i in reversed(range(12))] + ["t5.relbias"]
+    marks = [(10 * (i + 1), lay[n].offset + (lay[n].numel + 63) // 64 * 64) for i, n in enumerate(names)]
+    bks = pkg.dp.plan_buckets(marks, emb, 24 << 20)
+    shards = pkg.dp.plan_shards(bks, world)
+    cover = np.zeros(emb, np.int32)
+    for (_, a, b), (a2, c, b2) in zip(bks, shards):
+        assert (a, b) == (a2, b2) and c % 64 == 0 and 0 <= b - a - world * c < world * 64
+        for r in range(world):
+            cover[a + r * c:a + (r + 1) * c] += 1
+        cover[a + world * c:b] += 1
+    assert (cover == 1).all()
+
+
 def _allreduce_worker(rank, world, port, pkg_dir):
     _init(rank, world, port)
     from __graft_entry__ import load_package
