@@ -48,7 +48,7 @@ HARD_CODED_LR = 5e-4          # faster_rcnn_vqa_trainer.py:244-261
 class VQATrainer:
     def __init__(self, model: ResnetVQAModel, optimizer_kwargs: dict, lr_scheduler_kwargs: dict,
                  num_training_steps: int, gradient_clipping=1.0, use_graph=True, logger=print,
-                 data_parallel=None, process_group=None, bucket_mb=24):
+                 data_parallel=None, process_group=None, bucket_mb=24, shard_optimizer=False):
         if optimizer_kwargs.get("type", "AdamW") != "AdamW":
             raise ValueError("only AdamW is on this path (vit_daquar_config.json:41)")
         kw = dict(optimizer_kwargs.get("kwargs", {}))
@@ -64,6 +64,7 @@ class VQATrainer:
             raise ValueError("data parallel training is planned for ResnetVQAModel (BASELINE configs[2]); "
                              "the ViT configuration (configs[3]) is a single-GPU one")
         self.process_group, self.bucket_mb = process_group, int(bucket_mb)
+        self.shard_optimizer = bool(shard_optimizer)      # DP: reduce-scatter + sharded AdamW + all-gather
         self._dp = None
         groups = dp.dp_t5_dw_groups(model.engine.nl) if self.data_parallel else None
         if self.data_parallel and model.engine.t5_dw_groups != list(groups):
@@ -103,7 +104,7 @@ class VQATrainer:
         if self.data_parallel:
             if self._dp is None:
                 self._dp = dp.DataParallelStep(e, group=self.process_group, bucket_mb=self.bucket_mb,
-                                               use_graph=self.use_graph)
+                                               use_graph=self.use_graph, shard_optimizer=self.shard_optimizer)
             self._dp.step()
         else:
             if self.use_graph and e.graph is None:
@@ -194,6 +195,8 @@ class VQATrainer:
     def optimizer_state_dict(self):
         """torch.optim.AdamW(amsgrad=True).state_dict() of the reference's parameter groups."""
         e = self.model.engine
+        if self._dp is not None:
+            self._dp.sync_optimizer_state()                # sharded: every chunk's moments on this rank
         m, v, vm, step, _ = e.optimizer_state()
         state, pgroups, idx = {}, [], 0
         for label, lr, keys in self._param_groups():
