@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 13
+#define VQA_ABI_VERSION 14
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -200,6 +200,14 @@ typedef struct vqa_attn_desc {
   void* dv; long long lddv;
   float* dbias;
   vqa_dropout drop;
+  /* groups > 1 (MFMA path): `groups` independent attentions of the same shape in ONE launch
+   * (the SGA blocks' self-attention halves): group g reads / writes q, k, v, dq, dk, dv at
+   * + g*gstride_qkv, o at + g*gstride_o, p at + g*gstride_p, dout at + g*gstride_dout
+   * (elements), with dropout site drop.site + g*gdrop_site_stride and element indices from 0 --
+   * the results of `groups` separate launches.  0 / 1: one attention (strides unused). */
+  int groups;
+  long long gstride_qkv, gstride_o, gstride_p, gstride_dout;
+  int gdrop_site_stride;
 } vqa_attn_desc;
 
 int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t stream);
@@ -212,6 +220,11 @@ int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t stream);
 #define VQA_ATTN_LONG 1
 #define VQA_ATTN_VALU 2
 int vqa_attn_path(const vqa_attn_desc* d, int backward);
+/* The attention probabilities alone, d->p = [batch, heads, lq, lk] fp32:
+ * softmax_j(scale q_i.k_j (+ bias) (+ finfo.min at masked keys)) for any lq, lk (dh <= 1024):
+ * HF ViTModel(output_attentions=True), the `attentions` that VitVQAModel.generate_answers
+ * returns (model/vit_vqa_model.py:238-240, 285-290).  Eval-time readout; o / v / dropout unused. */
+int vqa_attn_probs(const vqa_attn_desc* d, hipStream_t stream);
 
 /* ----------------------------------------------------------------- norms ---
  * Rows of width d (d % 256 == 0, d <= 1024), fp32 in, fp32 and/or bf16 out.

@@ -54,9 +54,11 @@ def _nodrop(site, x, p=None):
     return x
 
 
-def vit_pooled(sd, pix, prefix="vision_model."):
+def vit_pooled(sd, pix, prefix="vision_model.", attentions=None):
     """ViTModel(pixel_values).pooler_output (transformers ViTEmbeddings / ViTLayer (pre-LN) /
-    ViTPooler): [B, 768].  Dropout probabilities are 0 in the ViT-base config."""
+    ViTPooler): [B, 768].  Dropout probabilities are 0 in the ViT-base config.  attentions: a
+    list that receives each layer's softmax probabilities [B, 12, L, L] (output_attentions=True,
+    vit_vqa_model.py:238-240)."""
     g = lambda k: sd[prefix + k]
     B = pix.shape[0]
     x = F.conv2d(pix, g("embeddings.patch_embeddings.projection.weight"),
@@ -70,6 +72,8 @@ def vit_pooled(sd, pix, prefix="vision_model."):
         qkv = [(n @ g(p + f"attention.attention.{t}.weight").T + g(p + f"attention.attention.{t}.bias"))
                .view(B, L, VIT_HEADS, VIT_DH).transpose(1, 2) for t in ("query", "key", "value")]
         s = qkv[0] @ qkv[1].transpose(2, 3) / math.sqrt(VIT_DH)
+        if attentions is not None:
+            attentions.append(torch.softmax(s, dim=-1))
         ctx = (torch.softmax(s, dim=-1) @ qkv[2]).transpose(1, 2).reshape(B, L, 768)
         x = ctx @ g(p + "attention.output.dense.weight").T + g(p + "attention.output.dense.bias") + x
         n = F.layer_norm(x, (768,), g(p + "layernorm_after.weight"), g(p + "layernorm_after.bias"), VIT_EPS)

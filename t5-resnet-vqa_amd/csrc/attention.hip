@@ -201,6 +201,51 @@ int fill(AttnP& P, const vqa_attn_desc* d) {
   return VQA_OK;
 }
 
+// Attention probabilities only (output_attentions=True of HF ViTModel, vit_vqa_model.py:238-240):
+// P[b, h, i, :] = softmax_j(scale * q_i . k_j (+ bias[h, i, j]) (+ finfo.min where key_mask[b, j] == 0)),
+// fp32, one 256-thread workgroup per (b, h, query i); the q row sits in LDS, each thread takes keys
+// j = tid, tid + 256, ...  An eval-time readout (the heat-map caller), not on the training path.
+__global__ __launch_bounds__(256) void attn_probs_kernel(AttnP P, int pairs) {
+  __shared__ float qs[1024];
+  __shared__ float red[8];
+  const int blk = blockIdx.x, i = blk % P.lq, pair = blk / P.lq;
+  const int b = pair / P.heads, hh = pair - b * P.heads;
+  const bf16_t* q = P.q + ((long)b * P.lq + i) * P.ldq + (long)hh * P.dh;
+  for (int c = threadIdx.x; c < P.dh; c += 256) qs[c] = bf2f(q[c]);
+  __syncthreads();
+  float* prow = P.p + (((long)b * P.heads + hh) * P.lq + i) * P.lk;
+  float mx = -INFINITY;
+  for (int j = threadIdx.x; j < P.lk; j += 256) {
+    const bf16_t* k = P.k + ((long)b * P.lk + j) * P.ldk + (long)hh * P.dh;
+    float acc = 0.f;
+    for (int c = 0; c < P.dh; c += 2) {
+      const float2 kv = unpack(*reinterpret_cast<const uint32_t*>(k + c));
+      acc = fmaf(qs[c], kv.x, fmaf(qs[c + 1], kv.y, acc));
+    }
+    float v = acc * P.scale;
+    if (P.bias) v += P.bias[((long)hh * P.lq + i) * P.lk + j];
+    if (P.mask && P.mask[(long)b * P.lk + j] == 0) v += MASK_MIN;
+    prow[j] = v;
+    mx = fmaxf(mx, v);
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float z = 0.f;
+  for (int j = threadIdx.x; j < P.lk; j += 256) {         // each thread re-reads only its own entries
+    const float e = __expf(prow[j] - mx);
+    prow[j] = e;
+    z += e;
+  }
+  z = wave_sum(z);
+  if ((threadIdx.x & 63) == 0) red[4 + (threadIdx.x >> 6)] = z;
+  __syncthreads();
+  const float iz = 1.f / (red[4] + red[5] + red[6] + red[7]);
+  for (int j = threadIdx.x; j < P.lk; j += 256) prow[j] *= iz;
+}
+
 }  // namespace
 
 bool vqa_attn_mfma_ok(const vqa_attn_desc* d);           // attention_mfma.hip
@@ -212,16 +257,20 @@ int vqa_attn_fwd_long(const vqa_attn_desc* d, hipStream_t s);
 
 extern "C" int vqa_attn_path(const vqa_attn_desc* d, int backward) {
   if (!d) return -1;
-  if (!backward && (d->lq > 32 || d->lk > 64) && vqa_attn_long_ok(d)) return VQA_ATTN_LONG;
+  if (!backward && d->groups <= 1 && (d->lq > 32 || d->lk > 64) && vqa_attn_long_ok(d)) return VQA_ATTN_LONG;
   return vqa_attn_mfma_ok(d) ? VQA_ATTN_MFMA : VQA_ATTN_VALU;
 }
 
 extern "C" int vqa_attn_fwd(const vqa_attn_desc* d, hipStream_t s) {
   VQA_REQUIRE(d && d->q && d->k && d->v, "attention: null q/k/v");
-  if ((d->lq > 32 || d->lk > 64) && vqa_attn_long_ok(d)) return vqa_attn_fwd_long(d, s);   // ViT (config 4)
+  if (d->groups <= 1 && (d->lq > 32 || d->lk > 64) && vqa_attn_long_ok(d))
+    return vqa_attn_fwd_long(d, s);                                // ViT (config 4)
   VQA_REQUIRE(d->o, "vqa_attn_fwd: null output");
   VQA_REQUIRE(d->drop.p >= 0.f && d->drop.p < 1.f, "attention: dropout p must be in [0, 1)");
   VQA_REQUIRE(d->batch > 0 && d->heads > 0, "attention: empty batch");
+  VQA_REQUIRE(d->groups <= 1 || ((long)d->groups * d->batch * d->heads < (1l << 30) && vqa_attn_mfma_ok(d) &&
+                                 !d->bias && !d->dbias && !d->key_mask),
+              "attention: groups > 1 needs the MFMA shapes and no bias / key mask");
   if (vqa_attn_mfma_ok(d)) return vqa_attn_fwd_mfma(d, s);        // the step's shapes (lk <= 160)
   AttnP P;
   if (int rc = fill(P, d)) return rc;
@@ -237,6 +286,9 @@ extern "C" int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t s) {
   VQA_REQUIRE(d->lddo % 8 == 0, "vqa_attn_bwd: dO stride must be a multiple of 8");
   VQA_REQUIRE(d->drop.p >= 0.f && d->drop.p < 1.f, "attention: dropout p must be in [0, 1)");
   VQA_REQUIRE(d->batch > 0 && d->heads > 0, "attention: empty batch");
+  VQA_REQUIRE(d->groups <= 1 || ((long)d->groups * d->batch * d->heads < (1l << 30) && vqa_attn_mfma_ok(d) &&
+                                 !d->bias && !d->dbias && !d->key_mask),
+              "attention: groups > 1 needs the MFMA shapes and no bias / key mask");
   if (vqa_attn_mfma_ok(d)) return vqa_attn_bwd_mfma(d, s);        // lk <= 160
   AttnP P;
   if (int rc = fill(P, d)) return rc;
@@ -244,4 +296,20 @@ extern "C" int vqa_attn_bwd(const vqa_attn_desc* d, hipStream_t s) {
   VQA_REQUIRE(sm <= 65536, "vqa_attn_bwd: shape needs %zu B of LDS (> 64 KiB)", sm);
   hipLaunchKernelGGL(attn_bwd_kernel, dim3(d->batch * d->heads), dim3(256), sm, s, P);
   return vqa::check_launch("vqa_attn_bwd");
+}
+
+extern "C" int vqa_attn_probs(const vqa_attn_desc* d, hipStream_t s) {
+  VQA_REQUIRE(d && d->q && d->k && d->p, "vqa_attn_probs: null q / k / p");
+  VQA_REQUIRE(d->batch > 0 && d->heads > 0 && d->lq > 0 && d->lk > 0 && d->dh > 0 && d->dh <= 1024 && d->dh % 2 == 0,
+              "vqa_attn_probs: bad shape (dh even, <= 1024)");
+  VQA_REQUIRE(d->ldk % 2 == 0 && ((uintptr_t)d->k & 3) == 0, "vqa_attn_probs: k rows must be 4-byte aligned");
+  VQA_REQUIRE(d->groups <= 1, "vqa_attn_probs: one attention per call (groups <= 1)");
+  AttnP P{};                                              // (fill() is for the lq, lk <= 64 kernels)
+  P.q = (const bf16_t*)d->q; P.k = (const bf16_t*)d->k; P.ldq = d->ldq; P.ldk = d->ldk;
+  P.p = d->p; P.bias = d->bias; P.mask = d->key_mask;
+  P.heads = d->heads; P.lq = d->lq; P.lk = d->lk; P.dh = d->dh; P.scale = d->scale;
+  const long grid = (long)d->batch * d->heads * d->lq;
+  VQA_REQUIRE(grid < (1l << 31), "vqa_attn_probs: grid too large");
+  hipLaunchKernelGGL(attn_probs_kernel, dim3((unsigned)grid), dim3(256), 0, s, P, d->batch * d->heads);
+  return vqa::check_launch("vqa_attn_probs");
 }

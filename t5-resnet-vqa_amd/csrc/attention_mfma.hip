@@ -40,7 +40,27 @@ struct AttnM {
   bf16_t *dq, *dk, *dv; long lddq, lddk, lddv;
   float* dbias;
   vqa_dropout drop;
+  int pg;                                               // pairs per group (batch * heads)
+  long gq, go, gp, gdo;                                 // group strides (vqa_attn_desc.gstride_*)
+  int gsite;                                            // dropout site stride per group
 };
+
+// group of `pair` (vqa_attn_desc.groups): its (batch, head) index inside the group, the
+// group's operand offsets applied to a copy of the parameters, its dropout site
+__device__ __forceinline__ int group_pair(AttnM& P, int pair) {
+  if (P.pg <= 0 || pair >= P.pairs) return pair;
+  const int g = pair / P.pg;
+  if (g == 0) return pair;
+  P.q += g * P.gq; P.k += g * P.gq; P.v += g * P.gq;
+  if (P.o) P.o += g * P.go;
+  if (P.p) P.p += g * P.gp;
+  if (P.dout) P.dout += g * P.gdo;
+  if (P.dq) P.dq += g * P.gq;
+  if (P.dk) P.dk += g * P.gq;
+  if (P.dv) P.dv += g * P.gq;
+  P.drop.site += (unsigned)(g * P.gsite);
+  return pair - g * P.pg;
+}
 
 // Every global load below is issued UNconditionally at a clamped (valid) address
 // and zeroed afterwards by an AND mask / multiply: "if (ok) load" or "ok ? load : 0"
@@ -169,8 +189,8 @@ __global__ __launch_bounds__(64 * wpb_for(NT)) void attn_fwd_mfma(AttnM P) {
   constexpr int KR = 32 * NT;                            // key rows of the V image
   __shared__ __attribute__((aligned(16))) char smem[WPB * KR * G::ROWB];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h5 = l >> 5, l31 = l & 31;
-  const int pair = blockIdx.x * WPB + w;
-  const bool live = pair < P.pairs;
+  const bool live = blockIdx.x * WPB + w < P.pairs;
+  const int pair = group_pair(P, blockIdx.x * WPB + w);
   const int b = live ? pair / P.heads : 0, hh = live ? pair - b * P.heads : 0;
   const int lq = P.lq, lk = P.lk;
   lds_char* vimg = (lds_char*)smem + w * KR * G::ROWB;
@@ -289,8 +309,8 @@ __global__ __launch_bounds__(64 * wpb_for(NT)) void attn_bwd_mfma(AttnM P) {
   constexpr int TRB = 2 * 32 * PR * 4;                   // saved P and dropout multipliers, [query][key] fp32
   __shared__ __attribute__((aligned(16))) char smem[WPB * (IMG + 32 * 4 + TRB)];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h5 = l >> 5, l31 = l & 31;
-  const int pair = blockIdx.x * WPB + w;
-  const bool live = pair < P.pairs;
+  const bool live = blockIdx.x * WPB + w < P.pairs;
+  const int pair = group_pair(P, blockIdx.x * WPB + w);
   const int b = live ? pair / P.heads : 0, hh = live ? pair - b * P.heads : 0;
   const int lq = P.lq, lk = P.lk;
   lds_char* kimg = (lds_char*)smem + w * (IMG + 128 + TRB);
@@ -537,6 +557,15 @@ static void fillm(AttnM& M, const vqa_attn_desc* d) {
   M.dq = (bf16_t*)d->dq; M.dk = (bf16_t*)d->dk; M.dv = (bf16_t*)d->dv;
   M.lddq = d->lddq; M.lddk = d->lddk; M.lddv = d->lddv;
   M.dbias = d->dbias; M.drop = d->drop;
+  M.pg = 0;
+  M.gq = M.go = M.gp = M.gdo = 0;
+  M.gsite = 0;
+  if (d->groups > 1) {                                  // groups x (batch, head) pairs in one grid
+    M.pg = M.pairs;
+    M.pairs *= d->groups;
+    M.gq = d->gstride_qkv; M.go = d->gstride_o; M.gp = d->gstride_p; M.gdo = d->gstride_dout;
+    M.gsite = d->gdrop_site_stride;
+  }
 }
 
 template <int DH, int NT>

@@ -146,7 +146,7 @@ class VQAEngine:
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0, pipeline=False,
                  t5_dw_group=None, defer_optimizer=True, dw_stream=None, sga_dw_batch=True, pair_bwd=True,
-                 language_model="t5-base", fp8=False):
+                 language_model="t5-base", fp8=False, sga_attn_group=True):
         L.load()
         # pipeline: the frozen ResNet (no trainable input) of the NEXT batch runs on its own
         # stream beside this step's T5 / SGA / backward / optimizer (see train_step)
@@ -199,6 +199,9 @@ class VQAEngine:
             self.t5_dw_group = int(t5_dw_group)
         # SGA blocks' q2 / m2 / fc1 / fc2 weight gradients batched over the blocks
         self.sga_dw_batch = bool(sga_dw_batch)
+        # the SGA blocks' self-attentions as ONE launch forward and ONE backward
+        # (vqa_attn_desc.groups; False: one launch per block)
+        self.sga_attn_group = bool(sga_attn_group)
         # AdamW of step k applied inside step k+1's forward (see _plan_optimizer)
         self.defer_opt = bool(defer_optimizer)
         # weight-gradient GEMMs (calls tagged `side`) on a stream of their own beside the
@@ -403,6 +406,7 @@ class VQAEngine:
         # q|k|v of block n in columns [n*2304, (n+1)*2304) of QKV1A, merge in/out in [n]
         self.QKV1A = t((T, NB * 3 * D), BF16)
         self.O1A, self.S1A = t((NB, T, D), BF16), t((NB, T, D))
+        self.P1A = t((NB, B, self.sga_heads, Lq, Lq))         # their attention probabilities, stacked
         # inputs of the blocks' q2 / m2 / fc1 / fc2 weight gradients, stacked in backward order
         # (slot NB-1-n) for the batched dW launches
         self.X1hS, self.O2S, self.X2hS, self.FFhS = (t((NB, T, D), BF16) for _ in range(4))
@@ -413,7 +417,7 @@ class VQAEngine:
             lk = self.fh * self.fh if n == 0 else Lq
             self.sga.append(dict(
                 ly=ly, lk=lk,
-                P1=t((B, self.sga_heads, Lq, Lq)), O1=self.O1A[n], S1=self.S1A[n],
+                P1=self.P1A[n], O1=self.O1A[n], S1=self.S1A[n],
                 X1=t((T, D)), X1h=self.X1hS[NB - 1 - n], MU1=t(T), RS1=t(T),
                 Q2=self.Q2S[NB - 1 - n], KV2=t((ly, 2 * D), BF16), P2=t((B, self.sga_heads, Lq, lk)),
                 O2=self.O2S[NB - 1 - n], S2=t((T, D)), X2=t((T, D)), X2h=self.X2hS[NB - 1 - n], MU2=t(T), RS2=t(T),
@@ -462,6 +466,16 @@ class VQAEngine:
             assert all(b.offset == a.offset + a.numel for a, b in zip(segs, segs[1:])), w
         return tuple(self.p16[k] for k in names if k in self.p16) + tuple(self.p32[k] for k in names) + \
             tuple(self.g32[k] for k in names)
+
+    def _sga_groups(self):
+        """vqa_attn_desc group fields of the SGA blocks' self-attentions: all NB blocks in one
+        launch (block n: q|k|v columns n*2304 of QKV1A, O1A[n] / dO1A[n], P1A[n], dropout site
+        sga_site(n, 0)), or one block per launch (sga_attn_group=False)."""
+        T, D = self.B * self.L, self.D
+        if not self.sga_attn_group or self.NB == 1:
+            return dict(groups=1)
+        return dict(groups=self.NB, gstride_qkv=3 * D, gstride_o=T * D, gstride_dout=T * D,
+                    gstride_p=self.P1A[0].numel(), gdrop_site_stride=sga_site(1, 0) - sga_site(0, 0))
 
     def _set_drop(self, call, site):
         d = self._drop(site)
@@ -698,13 +712,14 @@ class VQAEngine:
         else:
             self._gemm(f, self.TXT16, self.p16["sga0.qkv1_w"], T, NB * W3, D, lda=D, ldb=D, c16=self.QKV1A,
                        ldc16=NB * W3, bias=self.p32["sga0.qkv1_b"], keep=self._sga_self_keep())
-        for n in range(NB):
+        grp = self._sga_groups()
+        for n in range(0, NB, grp["groups"]):
             s, c0 = self.sga[n], n * W3
             q = self.QKV1A
             self._attn(f, "vqa_attn_fwd", q=ops.addr(q, c0), ldq=NB * W3, k=ops.addr(q, c0 + D), ldk=NB * W3,
                        v=ops.addr(q, c0 + 2 * D), ldv=NB * W3, o=s["O1"], ldo=D, p=s["P1"], batch=B,
                        heads=self.sga_heads, lq=Lq, lk=Lq, dh=self.sga_dh, scale=sc, drop=sga_site(n, 0),
-                       keep=(q,))
+                       keep=(q, self.O1A, self.P1A), **grp)
         m1kw = dict(c32=self.S1A, ldc32=D, bias=self.p32["sga0.m1_b"], res32=self.TXT32, ldres=D, batch=NB,
                     stride_a=T * D, stride_b=D * D, stride_c32=T * D, stride_res=0, stride_bias=D,
                     drop_site_stride=sga_site(1, 1) - sga_site(0, 1))
@@ -878,14 +893,15 @@ class VQAEngine:
                    stride_c32=D * D, keep=keep)
         b[-1].side = True
         dq = self.dQKV1A
-        for n in reversed(range(NB)):
+        grp = self._sga_groups()
+        for n in reversed(range(0, NB, grp["groups"])):
             s, c0 = self.sga[n], n * W3
             q = self.QKV1A
             self._attn(b, "vqa_attn_bwd", q=ops.addr(q, c0), ldq=NB * W3, k=ops.addr(q, c0 + D), ldk=NB * W3,
                        v=ops.addr(q, c0 + 2 * D), ldv=NB * W3, p=s["P1"], batch=B, heads=self.sga_heads, lq=Lq, lk=Lq,
                        dh=self.sga_dh, scale=sc, dout=self.dO1A[n], lddo=D, dq=ops.addr(dq, c0), lddq=NB * W3,
                        dk=ops.addr(dq, c0 + D), lddk=NB * W3, dv=ops.addr(dq, c0 + 2 * D), lddv=NB * W3,
-                       drop=sga_site(n, 0), keep=(q, dq))
+                       drop=sga_site(n, 0), keep=(q, dq, self.P1A, self.dO1A), **grp)
         tmp = []
         self._gemm(tmp, dq, self.p16["sga0.qkv1_w"], T, D, NB * W3, lda=NB * W3, ldb=D, b_trans=True,
                    c32=self.dTXT, ldc32=D, res32=self.dTA[0], ldres=D, keep=keep)

@@ -77,6 +77,8 @@ class AttnDesc(ctypes.Structure):
         ("dout", c_void_p), ("lddo", c_ll), ("dq", c_void_p), ("lddq", c_ll), ("dk", c_void_p), ("lddk", c_ll),
         ("dv", c_void_p), ("lddv", c_ll), ("dbias", c_void_p),
         ("drop", Dropout),
+        ("groups", c_int), ("gstride_qkv", c_ll), ("gstride_o", c_ll), ("gstride_p", c_ll), ("gstride_dout", c_ll),
+        ("gdrop_site_stride", c_int),
     ]
 
 
@@ -144,6 +146,7 @@ def load():
     lib.vqa_attn_fwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_attn_bwd.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_attn_path.argtypes = [ctypes.POINTER(AttnDesc), c_int]
+    lib.vqa_attn_probs.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_adamw_amsgrad.argtypes = [ctypes.POINTER(AdamWDesc), c_void_p]
     for name in ("vqa_norm_bwd_workspace_floats", "vqa_colsum_workspace_floats"):
         getattr(lib, name).argtypes = [c_int, c_int]

@@ -324,12 +324,17 @@ class VitVQAModel:
                          decoder_question_attention_masks=None, pixel_values=None, image_tensors=None,
                          answer_input_ids=None, answer_attention_masks=None, annotation_ids=None,
                          question_type_ids=None):
-        """:229-290 -> (log_probs, loss or None, attention_tensors).  The ViT's attention
-        probabilities (output_attentions=True, read only by the heat-map script) are never
-        materialised by the online-softmax attention kernel: attention_tensors is None."""
-        lp, loss = self.forward(question_input_ids, decoder_question_input_ids, question_attention_masks,
-                                decoder_question_attention_masks, annotation_ids, pixel_values)
-        return lp, loss, None
+        """:229-290 -> (log_probs, loss or None, attention_tensors): the forward, with the frozen
+        ViT's attention probabilities (output_attentions=True: a tuple of 12 [B, 12, 197, 197]
+        fp32 tensors, written by vqa_attn_probs beside the online-softmax attention)."""
+        e = self.engine
+        self.load_items({"question_input_ids": question_input_ids, "question_attention_masks": question_attention_masks,
+                         "decoder_question_input_ids": decoder_question_input_ids,
+                         "decoder_question_attention_masks": decoder_question_attention_masks,
+                         "pixel_values": pixel_values, "annotation_ids": annotation_ids})
+        atts = e.forward_with_attentions()
+        loss = e.LOSS[0].clone() if annotation_ids is not None else None
+        return e.LOGP.clone(), loss, tuple(a.clone() for a in atts)
 
     @staticmethod
     def convert_logits_to_predictions(lm_logits):

@@ -235,6 +235,7 @@ class VitVQAEngine:
     # ------------------------------------------------------------------ forward
     def _plan_forward(self):
         f = self.fwd_calls
+        self._vit_attn_at, self.ATT_MAPS, self._probs_calls = [], None, None
         B, Lq, Ld, T, TD, TV, NV = self.B, self.L, self.Ld, self.T, self.TD, self.TV, self.NV
         vw = self.vw
         if self.p_drop > 0.0:
@@ -255,6 +256,7 @@ class VitVQAEngine:
             self._attn(f, "vqa_attn_fwd", q=q, ldq=3 * D, k=ops.addr(q, D), ldk=3 * D, v=ops.addr(q, 2 * D),
                        ldv=3 * D, o=self.VO16, ldo=D, batch=B, heads=VM.VIT_HEADS, lq=NV, lk=NV, dh=VM.VIT_DH,
                        scale=VM.VIT_DH ** -0.5, keep=(q,))
+            self._vit_attn_at.append(len(f))               # where forward_with_attentions reads layer i's P
             self._gemm(f, self.VO16, vw[f"{i}.o_w"], TV, D, D, lda=D, ldb=D, c32=self.VH32, ldc32=D,
                        bias=vw[f"{i}.o_b"], res32=self.VH32, ldres=D)
             self._call(f, "vqa_layernorm_fwd", self.VH32, vw[f"{i}.ln2_g"], vw[f"{i}.ln2_b"], None, self.VLN16,
@@ -530,6 +532,30 @@ class VitVQAEngine:
 
     def forward(self):
         self._run(self.fwd_calls)
+
+    def forward_with_attentions(self):
+        """forward() that also writes the frozen ViT's attention probabilities, HF
+        ViTModel(output_attentions=True) (vit_vqa_model.py:238-240): a tuple of 12
+        [B, 12, NV, NV] fp32 tensors (vqa_attn_probs after each layer's q|k|v projection; the
+        buffer is allocated on the first call).  Eval readout for generate_answers."""
+        B, NV = self.B, self.NV
+        if self.ATT_MAPS is None:
+            self.ATT_MAPS = torch.empty((VM.VIT_LAYERS, B, VM.VIT_HEADS, NV, NV), dtype=F32, device=self.dev)
+            q = self.VQKV16
+            self._probs_calls = []
+            for i in range(VM.VIT_LAYERS):
+                d = L.AttnDesc()
+                d.q, d.ldq, d.k, d.ldk = ops.addr(q), 3 * D, ops.addr(q, D), 3 * D
+                d.p = ops.addr(self.ATT_MAPS[i])
+                d.batch, d.heads, d.lq, d.lk, d.dh, d.scale = B, VM.VIT_HEADS, NV, NV, VM.VIT_DH, VM.VIT_DH ** -0.5
+                self._probs_calls.append(ops.Call("vqa_attn_probs", ctypes.byref(d), desc=d, keep=(q, self.ATT_MAPS)))
+        s = L.stream_handle()
+        at = {k: i for i, k in enumerate(self._vit_attn_at)}
+        for idx, c in enumerate(self.fwd_calls):
+            c(s)
+            if idx + 1 in at:
+                self._probs_calls[at[idx + 1]](s)
+        return tuple(self.ATT_MAPS[i] for i in range(VM.VIT_LAYERS))
 
     def backward(self):
         self._run(self.bwd_calls)

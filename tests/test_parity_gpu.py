@@ -225,6 +225,28 @@ def test_t5_weight_gradient_grouping_is_bit_identical(cuda, pkg):
     assert all(torch.equal(grads[0], x) for x in grads[1:])
 
 
+def test_grouped_sga_self_attention_is_bit_identical(cuda, pkg):
+    """The SGA blocks' self-attentions as one grouped launch (vqa_attn_desc.groups = blocks,
+    the default) == one launch per block: same probabilities, loss and gradients, dropout
+    on (each group keeps its block's dropout site)."""
+    import torch
+    B, L, H = 2, 32, 64
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    nb = pkg.synthetic.make_batch(B, L, H, seed=5)
+    res = []
+    for grouped in (False, True):
+        eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=2, total=20, dropout=0.1, seed=4,
+                                   sga_attn_group=grouped)
+        n_attn = sum(1 for c in eng.fwd_calls if getattr(c, "name", "") == "vqa_attn_fwd")
+        eng.forward_backward(nb)
+        torch.cuda.synchronize()
+        res.append((n_attn, float(eng.LOSS.item()), eng.P1A.clone(), eng.O1A.clone(), eng.G32.clone()))
+    assert res[0][0] - res[1][0] == eng.NB - 1                  # NB launches became one
+    assert res[0][1] == res[1][1]
+    for a, b in zip(res[0][2:], res[1][2:]):
+        assert torch.equal(a, b)
+
+
 def test_deferred_optimizer_update_is_bit_identical(cuda, pkg):
     """AdamW applied inside the next forward (parameter ranges on their own stream, the
     default) == AdamW at the end of the step: same losses, and the same parameters and
