@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 14
+#define VQA_ABI_VERSION 15
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -344,6 +344,13 @@ int vqa_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t stream);
 int vqa_zero(void* p, long long bytes, hipStream_t stream);
 /* dst <- src, 16-byte aligned (a kernel, so a captured step holds no runtime memcpy node) */
 int vqa_copy(void* dst, const void* src, long long bytes, hipStream_t stream);
+/* Tap-shifted copies of an NHWC bf16 map [n, h, w, c] (c % 8 == 0, 16-byte aligned):
+ * out[t][(b*h + y)*w + x][:] = in[b][y - ky + pad][x - kx + pad][:] (0 outside), t = ky*kw + kx.
+ * The ConvTranspose2d scaler's weight gradient (resnet_vqa_model.py:72-78, 135) as ONE GEMM
+ * batched over the 9 taps: dW[:, t*C:(t+1)*C] = shift_t(dVIS)^T @ F4 -- plain operands in
+ * place of the implicit im2col gather (127 -> 100 us at B=64, tools/convt_micro.py). */
+int vqa_tap_shift(const void* in, void* out, int n, int h, int w, int c, int kh, int kw, int pad,
+                  hipStream_t stream);
 
 /* ------------------------------------------------ config 4: ViT + T5 enc-dec ---
  * VitVQAModel (model/vit_vqa_model.py:127-227) data movement (vit.hip):

@@ -437,6 +437,7 @@ class VQAEngine:
         self.dO16 = t((T, D), BF16)
         self.dTXT = t((T, D))
         self.dVIS32, self.dVIS16 = t((V, D)), t((V, D), BF16)
+        self.dVIS9 = t((9, V, D), BF16)                 # its 3x3 tap-shifted copies (scaler dW)
         self.dH32 = t((T, D))
         self.dHM32 = t((T, D))
         self.dPB = t((self.h5, Lq, Lq), zero=True)
@@ -915,13 +916,17 @@ class VQAEngine:
         self._defer(ws, lib.vqa_colsum_parts(T), NB * W3, NB * W3, self.g32["sga0.qkv1_b"])
         self._jobs[-1] = self._jobs[-1][:-1] + (self._jobs[-1][-1] + keep,)
         mark(f"sga{NB - 1}.m1_b")
-        # ConvTranspose2d scaler weight/bias gradient: implicit im2col of layer4 as the B operand
-        # (vision branch: independent of the T5 backward below; its own colsum workspace)
+        # ConvTranspose2d scaler weight/bias gradient (vision branch: independent of the T5
+        # backward below; its own colsum workspace).  The flipped-conv weight column t*C + c
+        # (tap t = ky*3 + kx) is sum_pos dVIS[pos] * F4[pos shifted by tap t]; shifting dVIS
+        # the other way instead makes the 9 taps ONE batched GEMM over plain operands:
+        # dW[:, t*C:(t+1)*C] = shift_t(dVIS)^T @ F4 (vqa_tap_shift; no implicit im2col gather)
         self._bsplit = [len(b)]
         cin, fh = self.fc, self.fh
-        g = ops.conv_geom(B, fh, fh, cin, fh, fh, 3, 3, 1, 1)
-        self._gemm(b, self.dVIS16, self.F4, D, 9 * cin, self.V_TOK, lda=D, ldb=9 * cin, a_trans=True, b_trans=True,
-                   c32=self.g32["scaler_w"], ldc32=9 * cin, gb=g)
+        self._call(b, "vqa_tap_shift", self.dVIS16, self.dVIS9, B, fh, fh, D, 3, 3, 1)
+        self._gemm(b, self.dVIS9, self.F4, D, cin, self.V_TOK, lda=D, ldb=cin, a_trans=True, b_trans=True,
+                   c32=self.g32["scaler_w"], ldc32=9 * cin, batch=9, stride_a=self.V_TOK * D, stride_b=0,
+                   stride_c32=cin, keep=(self.G32,))
         self._call(b, "vqa_colsum", self.dVIS32, 0, self.V_TOK, D, D, self.g32["scaler_b"], 0.0, self.WS_COL2)
         mark("scaler_b")
         self._bsplit.append(len(b))

@@ -193,6 +193,7 @@ register("vqa_batch_sum", P, c_int, c_ll, P, c_float)
 register("vqa_cast_f32_bf16", P, P, c_ll)
 register("vqa_zero", P, c_ll)
 register("vqa_copy", P, P, c_ll)
+register("vqa_tap_shift", P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int)
 register("vqa_quant_rows_fp8", P, c_int, c_ll, c_int, c_int, P, c_ll, P)
 register("vqa_head_fwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_head_bwd", P, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)

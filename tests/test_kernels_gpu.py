@@ -304,6 +304,44 @@ def test_image_and_maxpool(k):
     assert torch.equal(y.float(), ref)
 
 
+@pytest.mark.parametrize("n,h,w,c", [(3, 7, 7, 768), (2, 5, 9, 24)])
+def test_tap_shift_and_tap_batched_conv_transpose_dw(k, n, h, w, c):
+    """vqa_tap_shift's 3x3 shifted copies (exact), and the scaler weight gradient as the
+    engine plans it -- one GEMM batched over the taps -- against the implicit-im2col GEMM and
+    torch's ConvTranspose2d weight gradient."""
+    ops = k.ops
+    x = rnd((n, h, w, c), 41, dtype=torch.bfloat16)
+    out = torch.empty(9, n * h * w, c, device="cuda", dtype=torch.bfloat16)
+    run(k, "vqa_tap_shift", x, out, n, h, w, c, 3, 3, 1)
+    xp = F.pad(x, (0, 0, 1, 1, 1, 1))
+    ref = torch.stack([xp[:, 2 - ky:2 - ky + h, 2 - kx:2 - kx + w].reshape(-1, c) for ky in range(3) for kx in range(3)])
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    # dW [c, 9*cin] of a 3x3/1/1 ConvTranspose2d cin -> c (the flipped-conv weight layout)
+    cin, K = 64, n * h * w
+    f4 = rnd((K, cin), 42, dtype=torch.bfloat16)
+    g32 = torch.zeros(c, 9 * cin, device="cuda")
+    d = ops.gemm_desc(out, f4, c, cin, K, lda=c, ldb=cin, a_trans=True, b_trans=True, c32=g32, ldc32=9 * cin,
+                      batch=9, stride_a=K * c, stride_b=0, stride_c32=cin)
+    ops.gemm_call(d, [out, f4, g32])(k.lib.stream_handle())
+    gi = torch.zeros(c, 9 * cin, device="cuda")
+    geo = ops.conv_geom(n, h, w, cin, h, w, 3, 3, 1, 1)
+    d2 = ops.gemm_desc(x.view(K, c), f4, c, 9 * cin, K, lda=c, ldb=9 * cin, a_trans=True, b_trans=True, c32=gi,
+                       ldc32=9 * cin, gb=geo)
+    ops.gemm_call(d2, [x, f4, gi])(k.lib.stream_handle())
+    torch.cuda.synchronize()
+    # torch: y = conv_transpose2d(f, W) with W [cin, c, 3, 3]; dW = autograd of <y, dy>, dy = x
+    fm = f4.float().view(n, h, w, cin).permute(0, 3, 1, 2).double().cpu()
+    dy = x.float().permute(0, 3, 1, 2).double().cpu()
+    wt = torch.zeros(cin, c, 3, 3, dtype=torch.float64, requires_grad=True)
+    (F.conv_transpose2d(fm, wt, padding=1) * dy).sum().backward()
+    # flipped-conv layout: column (ky*3 + kx)*cin + ci holds W[ci, o, 2-ky, 2-kx]
+    want = wt.grad.flip(2, 3).permute(1, 2, 3, 0).reshape(c, 9 * cin)
+    scale = float(want.abs().max())
+    assert float((g32.double().cpu() - want).abs().max()) <= 1e-5 * scale
+    assert float((gi.double().cpu() - want).abs().max()) <= 1e-5 * scale
+
+
 def test_adamw_amsgrad_matches_torch(k):
     n = 4096 + 64
     torch.manual_seed(0)
