@@ -434,16 +434,18 @@ def kernel_rooflines(eng, stream, pmc):
                            "frac": round(adam_gbs / HBM_PEAK_GBS, 4),
                            "traffic": (round(pmc["adamw_kernel"]["traffic_bytes"]) if "adamw_kernel" in pmc else None),
                            "algorithmic_bytes": adam_bytes, "kernel_avg_us": round(adam_dur * 1e6, 2)}
-    # MFMA: the largest single launch, the ConvTranspose2d weight-gradient implicit GEMM
-    # (M=768, N=9*2048, K=B*49; 2*M*N*K FLOP)
-    wg_call = next(c for c in eng.bwd_calls if c.name == "vqa_gemm" and c.desc.b_conv == 1)
+    # MFMA: the largest single launch, the ConvTranspose2d weight gradient as one GEMM batched
+    # over the 9 taps (M=768, N=2048, K=B*49, batch 9 over vqa_tap_shift copies of dVIS;
+    # 2*M*N*K*9 FLOP, the same work as the implicit-im2col form M=768, N=9*2048)
+    wg_call = eng.scaler_dw_call
+    assert wg_call.name == "vqa_gemm" and wg_call.desc.batch == 9
     cfg = VL.load().vqa_gemm_select(wg_call.desc)
     bm, bn, st = VL.GEMM_TILES[cfg]
     wm, wn = VL.GEMM_WAVES[cfg]
-    kname = (f"gemm_kernel<{bm}, {bn}, {st}, {wm}, {wn}, false, false, false, true> (ConvTranspose2d dW implicit "
-             f"GEMM, splitk={max(1, wg_call.desc.splitk)})")
+    kname = (f"gemm_kernel<{bm}, {bn}, {st}, {wm}, {wn}, false, false, false, false> (ConvTranspose2d dW, tap-batched "
+             f"GEMM, batch 9, splitk={max(1, wg_call.desc.splitk)})")
     kdur = time_kernel(wg_call, 20, stream)
-    kflop = 2.0 * wg_call.desc.m * wg_call.desc.n * wg_call.desc.k
+    kflop = 2.0 * wg_call.desc.m * wg_call.desc.n * wg_call.desc.k * wg_call.desc.batch
     k_tflops = kflop / kdur / 1e12
     out["roofline_gemm"] = {"bound": "mfma", "kernel": kname, "achieved": round(k_tflops, 1), "peak": MFMA_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": round(k_tflops / MFMA_PEAK_TFLOPS, 4),

@@ -927,6 +927,7 @@ class VQAEngine:
         self._gemm(b, self.dVIS9, self.F4, D, cin, self.V_TOK, lda=D, ldb=cin, a_trans=True, b_trans=True,
                    c32=self.g32["scaler_w"], ldc32=9 * cin, batch=9, stride_a=self.V_TOK * D, stride_b=0,
                    stride_c32=cin, keep=(self.G32,))
+        self.scaler_dw_call = b[-1]                       # bench roofline_gemm: the step's largest launch
         self._call(b, "vqa_colsum", self.dVIS32, 0, self.V_TOK, D, D, self.g32["scaler_b"], 0.0, self.WS_COL2)
         mark("scaler_b")
         self._bsplit.append(len(b))

@@ -57,7 +57,7 @@ if MODE == "res":
     t5 = [c for c in eng.fwd_calls[eng._t5_layer_start[0]:eng._t5_layer_start[1]] if c.name == "vqa_gemm"]
     plan += [(f"t5_{i}", c, gemm_flop(c), 0.0) for i, c in enumerate(t5)]
 if MODE != "res":
-    wg = next(c for c in eng.bwd_calls if c.name == "vqa_gemm" and c.desc.b_conv == 1)
+    wg = eng.scaler_dw_call                                  # the tap-batched scaler dW GEMM
     plan.append(("convT_dW", wg, gemm_flop(wg), 0.0))
     sga = [c for c in eng.sga_vision_calls + eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
            if c.name in ("vqa_gemm", "vqa_gemm_pair", "vqa_attn_fwd", "vqa_attn_bwd")]
