@@ -535,24 +535,20 @@ extern "C" int vqa_copy(void* dst, const void* src, long long bytes, hipStream_t
 
 // Tap-shifted copies of an NHWC bf16 map (ConvTranspose2d scaler dW as a tap-batched GEMM):
 // out[t][(b*h + y)*w + x][:] = in[b][y - ky + pad][x - kx + pad][:], t = ky*kw + kx, zero
-// outside the map.  One thread per 16-byte chunk (8 channels), chunks of a row contiguous.
-__global__ void tap_shift_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, int n, int h, int w, int c8,
-                                 int kh, int kw, int pad, long total) {
-  const long rows = (long)n * h * w;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / c8;
-    const int ch = (int)(i - r * c8);
-    const int t = (int)(r / rows);
-    const long pos = r - t * rows;
-    const int ky = t / kw, kx = t - ky * kw;
-    const int b = (int)(pos / ((long)h * w));
-    const int yx = (int)(pos - (long)b * h * w);
-    const int y = yx / w, x = yx - y * w;
-    const int sy = y - ky + pad, sx = x - kx + pad;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (sy >= 0 && sy < h && sx >= 0 && sx < w) v = in[(((long)b * h + sy) * w + sx) * c8 + ch];
-    out[i] = v;
-  }
+// outside the map.  blockIdx.y = tap; one thread per 16-byte chunk (8 channels), 32-bit
+// index math (the host bounds rows * c8 below 2^31).
+__global__ __launch_bounds__(256) void tap_shift_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, int h,
+                                                        int w, int c8, int kw, int pad, int per_tap) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= per_tap) return;
+  const int t = blockIdx.y, ky = t / kw, kx = t - ky * kw;
+  const int pos = i / c8, ch = i - pos * c8;
+  const int hw = h * w, b = pos / hw, yx = pos - b * hw;
+  const int y = yx / w, x = yx - y * w;
+  const int sy = y - ky + pad, sx = x - kx + pad;
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (sy >= 0 && sy < h && sx >= 0 && sx < w) v = in[(b * hw + sy * w + sx) * c8 + ch];
+  out[(long)t * per_tap + i] = v;
 }
 
 extern "C" int vqa_tap_shift(const void* in, void* out, int n, int h, int w, int c, int kh, int kw, int pad,
@@ -560,9 +556,9 @@ extern "C" int vqa_tap_shift(const void* in, void* out, int n, int h, int w, int
   VQA_REQUIRE(in && out && n > 0 && h > 0 && w > 0 && c > 0 && kh > 0 && kw > 0 && pad >= 0 && c % 8 == 0 &&
                   ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0,
               "vqa_tap_shift: bad arguments (c a multiple of 8, 16-byte aligned maps)");
-  const long total = (long)kh * kw * n * h * w * (c / 8);
-  const long blocks = (total + 255) / 256;
-  hipLaunchKernelGGL(tap_shift_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s,
-                     (const uint4*)in, (uint4*)out, n, h, w, c / 8, kh, kw, pad, total);
+  const long per_tap = (long)n * h * w * (c / 8);
+  VQA_REQUIRE(per_tap < (1l << 31) && kh * kw <= 65535, "vqa_tap_shift: map too large");
+  hipLaunchKernelGGL(tap_shift_kernel, dim3((unsigned)((per_tap + 255) / 256), (unsigned)(kh * kw)), dim3(256), 0, s,
+                     (const uint4*)in, (uint4*)out, h, w, c / 8, kw, pad, (int)per_tap);
   return vqa::check_launch("vqa_tap_shift");
 }
