@@ -146,3 +146,18 @@ rf = best_of(make_f, tiles(K, D), -(-9 * cin // 64))
 t, cfg, sk = rf[0]
 print(f"convT fwd implicit-A best {t:7.1f} us cfg {cfg:2d} sk {sk}  {fl / t / 1e6:6.0f} TF/s; next: "
       + ", ".join(f"{x[0]:.1f}/c{x[1]}s{x[2]}" for x in rf[1:5]))
+# scaler forward from an explicit im2col of the layer4 map (A [pos, tap*C + c], plain k-contiguous)
+col = torch.stack([torch.nn.functional.pad(f4.view(B, fh, fh, cin), (0, 0, 1, 1, 1, 1))[:, ky:ky + fh, kx:kx + fh]
+                   .reshape(K, cin) for ky in range(3) for kx in range(3)], 1).reshape(K, 9 * cin).contiguous()
+o32b, o16b = torch.zeros(K, D, device="cuda"), torch.zeros(K, D, dtype=torch.bfloat16, device="cuda")
+
+
+def make_fx():
+    return ops.gemm_desc(col, w, K, D, 9 * cin, lda=9 * cin, ldb=9 * cin, c32=o32b, ldc32=D, c16=o16b, ldc16=D), \
+        (col, w, o32b, o16b)
+
+
+rfx = best_of(make_fx, tiles(K, D), -(-9 * cin // 64))
+t, cfg, sk = rfx[0]
+print(f"convT fwd explicit im2col GEMM best {t:7.1f} us cfg {cfg:2d} sk {sk}  {fl / t / 1e6:6.0f} TF/s; next: "
+      + ", ".join(f"{x[0]:.1f}/c{x[1]}s{x[2]}" for x in rfx[1:5]) + f"  (+ the im2col: {col.numel() * 2 / 1e6:.0f} MB written)")
