@@ -156,6 +156,49 @@ def test_attention_fwd_bwd(k, B, H, Lq, Lk, dh, t5, pd):
         torch.testing.assert_close(red - 3.0, bf.grad, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("G,Lk,dh", [(3, 32, 96), (2, 49, 96), (4, 40, 64)])
+def test_grouped_attention_equals_separate_launches(k, G, Lk, dh):
+    """vqa_attn_desc.groups: G attentions in one forward and one backward launch give the bits
+    of G separate launches (q|k|v of group g at column g*3D of one row, outputs / P / dO at
+    per-group strides, dropout site + g*stride)."""
+    B, H, Lq = 3, 8, 32
+    D = H * dh
+    L = k.lib
+    A = k.ops.addr
+    qkv = rnd((B * Lq, G * 3 * D), 20, dtype=torch.bfloat16)
+    kv = qkv if Lk == Lq else rnd((B * Lk, G * 3 * D), 21, dtype=torch.bfloat16)
+    do = rnd((G, B * Lq, D), 22, dtype=torch.bfloat16)
+    rng = torch.tensor([5, 2, 1], dtype=torch.int32, device="cuda")
+    outs = []
+    for grouped in (False, True):
+        o = torch.zeros(G, B * Lq, D, device="cuda", dtype=torch.bfloat16)
+        p = torch.zeros(G, B, H, Lq, Lk, device="cuda")
+        dq = torch.zeros(B * Lq, G * 3 * D, device="cuda", dtype=torch.bfloat16)
+        dkv = dq if Lk == Lq else torch.zeros(B * Lk, G * 3 * D, device="cuda", dtype=torch.bfloat16)
+        for g in range(1 if grouped else G):
+            d = L.AttnDesc()
+            c = g * 3 * D
+            d.q, d.ldq, d.k, d.ldk, d.v, d.ldv = A(qkv, c), G * 3 * D, A(kv, c + D), G * 3 * D, A(kv, c + 2 * D), G * 3 * D
+            d.o, d.ldo, d.p = A(o[g]), D, A(p[g])
+            d.batch, d.heads, d.lq, d.lk, d.dh, d.scale = B, H, Lq, Lk, dh, 1.0 / math.sqrt(dh)
+            d.drop = L.Dropout(0.1, 40 + 8 * g, rng.data_ptr())
+            if grouped:
+                d.groups, d.gstride_qkv, d.gstride_o, d.gstride_p, d.gstride_dout = G, 3 * D, B * Lq * D, p[0].numel(), \
+                    B * Lq * D
+                d.gdrop_site_stride = 8
+            assert L.load().vqa_attn_path(ctypes.byref(d), 0) == L.ATTN_MFMA
+            L.check(L.load().vqa_attn_fwd(ctypes.byref(d), L.stream_handle()), "fwd")
+            d.dout, d.lddo = A(do[g]), D
+            d.dq, d.lddq, d.dk, d.lddk, d.dv, d.lddv = A(dq, c), G * 3 * D, A(dkv, c + D), G * 3 * D, \
+                A(dkv, c + 2 * D), G * 3 * D
+            L.check(L.load().vqa_attn_bwd(ctypes.byref(d), L.stream_handle()), "bwd")
+        torch.cuda.synchronize()
+        outs.append((o, p, dq, dkv))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert float(outs[1][1].abs().sum()) > 0
+
+
 @pytest.mark.parametrize("Lq", [20, 40])
 def test_causal_bias_with_key_mask_one_finfo_min(k, Lq):
     """The T5 decoder's causal pairs (bias = finfo.min, vqa_t5_relbias_fwd bucket < 0) under a
