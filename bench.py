@@ -34,7 +34,8 @@ FLOP_PER_PAIR = 30.95e9        # fwd+bwd algorithmic FLOPs
 MFMA_PEAK_TFLOPS = 2517.0      # bf16 dense: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md)
 FP8_PEAK_TFLOPS = 5034.0       # e4m3 dense, block-scaled MFMA (2x the bf16 rate per clock, MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
-PMC_FILE = "r03_pmc.json"               # rocprofv3 PMC summary this bench quotes (tools/pmc_step.py)
+PMC_FILE = "r04_pmc.json"               # rocprofv3 PMC summary this bench quotes (tools/pmc_step.py)
+PMC_FILE_C5 = "r04_pmc_c5.json"         # the same passes over the config-5 step (bench.py --config5)
 DIGEST_SUFFIXES = (".py", ".hip", ".h", ".inl", ".json", "Makefile")
 
 
@@ -172,7 +173,17 @@ def bench_vit(args, pkg, dev):
         out["cpu_baseline"] = {"value": round(cb / t, 3), "unit": "pairs/s", "cores": torch.get_num_threads(),
                                "kind": "port", "sample": f"config-4 oracle fp32 train step, B={cb}, L={L}, Ld={Ld}, "
                                                          f"224x224, median of {steps} after {warm} ({t:.2f} s/step)"}
-    print(json.dumps(out), flush=True)
+    emit(out)
+
+
+_OUT = None
+
+
+def emit(out):
+    """The bench's one JSON line, on the process's original stdout."""
+    f = _OUT or sys.stdout
+    f.write(json.dumps(out) + "\n")
+    f.flush()
 
 
 def spawn_ranks(n):
@@ -232,6 +243,9 @@ def main():
     ap.add_argument("--tune-save", default=None, help="write the tile choices used to this file")
     ap.add_argument("--model", choices=("resnet", "vit"), default="resnet",
                     help="vit: BASELINE configs[3], ViT-base + T5 encoder-decoder (1 GPU)")
+    ap.add_argument("--dp", action="store_true",
+                    help="N = 1: run the N > 1 step (dp.DataParallelStep over a world-1 RCCL group, the DP engine's "
+                         "weight-gradient groups) instead of the single-GPU engine graph")
     ap.add_argument("--rehearse", action="store_true",
                     help="run every rank on cuda:0 over gloo: exercises the N-rank code path (bucketing, "
                          "gathers, capture, lockstep) on a one-GPU box; the timing is not a measurement")
@@ -240,6 +254,11 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))          # one process per GPU, started before any GPU call
 
+    # the one JSON line goes to the original stdout; anything native libraries print there (the
+    # RCCL version banner at communicator creation) is sent to stderr instead
+    global _OUT
+    _OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -255,9 +274,18 @@ def main():
         bench_vit(args, load_package(), dev)
         return
     dist = None
-    if world > 1:
+    use_dp = world > 1 or args.dp
+    if use_dp:
         import torch.distributed as dist
-        if args.rehearse:
+        if world == 1:                                   # --dp: a world-1 RCCL group of this process
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                s = socket.socket()
+                s.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+                s.close()
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        elif args.rehearse:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
@@ -274,7 +302,7 @@ def main():
     dp_groups = pkg.dp.dp_t5_dw_groups(pkg.synthetic.lm_dims(lm).t5_layers)
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev, num_blocks=NB,
                                warmup=10, total=100000, dropout=0.1, seed=rank, pipeline=pipe,
-                               t5_dw_group=None if world == 1 else dp_groups, language_model=lm,
+                               t5_dw_group=None if not use_dp else dp_groups, language_model=lm,
                                fp8=args.config5)
     del sd
     pool = []
@@ -292,7 +320,7 @@ def main():
     eng.forward()
     eng.backward()
     eng.autotune(table=args.tune_table, save=args.tune_save if rank == 0 else None)   # tile choice: speed only
-    if world > 1:
+    if use_dp:
         dps = pkg.dp.DataParallelStep(eng, use_graph=not args.no_graph, shard_optimizer=args.shard_optimizer)
         run_step = dps.step
     else:
@@ -316,7 +344,7 @@ def main():
     for i in range(args.warmup):
         step(i)
     stream = torch.cuda.current_stream(dev)
-    if world > 1:                          # per-collective exposed wait (HIP events around each wait)
+    if use_dp:                             # per-collective exposed wait (HIP events around each wait)
         dps.timing = True
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
@@ -342,17 +370,22 @@ def main():
     gnorm = eng.last_grad_norm()
     pairs = world * B * args.steps
     value = pairs / dt
-    pmc, pmc_note = {}, f"profiles/{PMC_FILE} absent"
     survey_cfg = (args.image_size, args.seq_len, NB) == (224, 32, 3) and not args.config5
-    pmc_path = os.path.join(ROOT, "profiles", PMC_FILE)
-    if not survey_cfg:
-        pmc_note = f"profiles/{PMC_FILE} covers the config-2 step only (B=64, 224x224, L=32, 3 blocks)"
+    c5_cfg = args.config5 and (B, args.seq_len) == (64, 32)
+    pfile = PMC_FILE if survey_cfg else PMC_FILE_C5
+    pmc, pmc_note = {}, f"profiles/{pfile} absent"
+    pmc_path = os.path.join(ROOT, "profiles", pfile)
+    if not (survey_cfg or c5_cfg):
+        pmc_note = (f"profiles/{PMC_FILE} / {PMC_FILE_C5} cover the config-2 and config-5 steps only "
+                    "(B=64, L=32; 224x224 / 3 blocks, 384x384 / 6 blocks)")
     elif os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
-        if pmc.get("tree_digest") != tree_digest():      # counters of another tree: not quoted
-            pmc, pmc_note = {}, f"profiles/{PMC_FILE} was measured on another tree (digest mismatch): not quoted"
+        if args.no_pipeline or args.no_graph:
+            pmc, pmc_note = {}, f"profiles/{pfile} was measured on the pipelined graph step: not quoted"
+        elif pmc.get("tree_digest") != tree_digest():      # counters of another tree: not quoted
+            pmc, pmc_note = {}, f"profiles/{pfile} was measured on another tree (digest mismatch): not quoted"
         else:
-            pmc_note = (f"profiles/{PMC_FILE} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, all dispatches of one step; "
+            pmc_note = (f"profiles/{pfile} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, all dispatches of one step; "
                         f"measured on this tree, commit {pmc.get('commit')})")
 
     # Headline roofline (the step is > 97 % GEMM FLOPs, so it is MFMA-bound): the whole
@@ -363,7 +396,7 @@ def main():
     # Other shapes (--image-size / --seq-len): the MFMA work of the prepared calls.
     step_flop = FLOP_PER_PAIR * B if survey_cfg else calls_flop(eng)
     step_tflops = step_flop / gpu_step / 1e12
-    st = pmc.get("step", {}) if survey_cfg else {}
+    st = pmc.get("step", {})
     # config 5 mixes e4m3 (forward weight GEMMs) and bf16 MFMA work: the peak is the rate at which
     # the step's FLOP mix would run with every launch at its dtype's dense peak
     f8 = calls_flop(eng, fp8_only=True)
@@ -388,7 +421,8 @@ def main():
                                 + (" (BASELINE configs[1]; configs[2] at N=8)" if survey_cfg else "")
                                 + (" (BASELINE configs[4]: e4m3 forward weight GEMMs)" if args.config5 else "")),
                    "model": f"resnet50+{lm}+{NB}xSGA", "global_batch": world * B, "per_gpu_batch": B,
-                   "seq_len": L, "image_size": H, "answers": 170, "parallelism": f"dp{world}",
+                   "seq_len": L, "image_size": H, "answers": 170,
+                   "parallelism": f"dp{world}" + (" (DataParallelStep, RCCL world 1)" if args.dp and world == 1 else ""),
                    "world_size": (dist.get_world_size() if dist else 1), "graph": not args.no_graph,
                    "resnet_pipelined": pipe},
         **({"rehearsal": "all ranks on cuda:0 over gloo: a code-path check, not a measurement"}
@@ -396,7 +430,7 @@ def main():
         "roofline": roofline,
         "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
     }
-    if world > 1:
+    if use_dp:
         out["dp"] = dps.timing_report()
         out["dp"]["backend"] = dist.get_backend()
     if args.rehearse:                               # the N-rank path's results: lockstep across ranks
@@ -406,11 +440,11 @@ def main():
         dist.all_gather(ps, p)
         out["rehearsal_lockstep"] = all(torch.equal(q, ps[0]) for q in ps)
     elif not args.no_kernel_rooflines:
-        out.update(kernel_rooflines(eng, stream, pmc if survey_cfg else {}))   # PMC figures: the committed shape only
+        out.update(kernel_rooflines(eng, stream, pmc))       # PMC figures: the committed shapes only
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pkg)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
@@ -459,6 +493,9 @@ def kernel_rooflines(eng, stream, pmc):
     sga_calls = [c for c in eng.sga_vision_calls + eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
                  if c.name in ("vqa_gemm", "vqa_gemm_pair", "vqa_attn_fwd", "vqa_attn_bwd")]
 
+    def call_peak(c):                       # each launch's dense peak: e4m3 launches at the fp8 rate
+        return FP8_PEAK_TFLOPS if c.name == "vqa_gemm" and c.desc.fp8 else MFMA_PEAK_TFLOPS
+
     def call_flop(c):
         if c.name == "vqa_gemm":
             return 2.0 * c.desc.m * c.desc.n * c.desc.k * max(1, c.desc.batch)
@@ -467,14 +504,34 @@ def kernel_rooflines(eng, stream, pmc):
         d = c.desc
         return (4.0 if c.name == "vqa_attn_fwd" else 8.0) * d.batch * d.heads * d.lq * d.lk * d.dh
     sga = {}
+    times = {id(c): time_kernel(c, 10, stream) for c in sga_calls}
     for tag, names in (("gemm", ("vqa_gemm", "vqa_gemm_pair")), ("all", None)):
         cs = [c for c in sga_calls if names is None or c.name in names]
         fl = sum(call_flop(c) for c in cs)
-        tm = sum(time_kernel(c, 10, stream) for c in cs)
+        tm = sum(times[id(c)] for c in cs)
+        # the peak of this mix: every launch at its own dtype's dense peak (config 5: the e4m3
+        # forward GEMMs at 5,034, the rest at 2,517 TFLOP/s); config 2 is all bf16
+        pk = fl / sum(call_flop(c) / call_peak(c) for c in cs)
         sga[tag] = {"launches": len(cs), "flop_per_step": fl, "kernel_us_per_step": round(tm * 1e6, 1),
-                    "achieved": round(fl / tm / 1e12, 1), "frac": round(fl / tm / 1e12 / MFMA_PEAK_TFLOPS, 4)}
-    out["sga_mfma"] = {"peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "target_frac": 0.40, **sga,
+                    "achieved": round(fl / tm / 1e12, 1), "peak": round(pk, 1), "frac": round(fl / tm / 1e12 / pk, 4)}
+    out["sga_mfma"] = {"peak": sga["gemm"]["peak"], "unit": "TFLOP/s", "target_frac": 0.40, **sga,
                        "pmc_mfma_busy": pmc.get("sga_mfma_busy")}
+    # e4m3 (config 5): the largest fp8 launch of the step against the fp8 dense peak
+    f8 = [c for c in list(eng.res_calls) + eng.fwd_calls + eng.bwd_calls if c.name == "vqa_gemm" and c.desc.fp8]
+    if f8:
+        c = max(f8, key=call_flop)
+        d = c.desc
+        cfg = VL.load().vqa_gemm_select(d)
+        bm, bn, st = VL.GEMM_TILES[cfg]
+        kd = time_kernel(c, 20, stream)
+        kt = call_flop(c) / kd / 1e12
+        out["roofline_fp8"] = {"bound": "mfma", "kernel": f"gemm_kernel<{bm}, {bn}, {st}, ..., fp8> (e4m3 forward "
+                                                          f"GEMM, m={d.m} n={d.n} k={d.k} batch={max(1, d.batch)}, "
+                                                          f"splitk={max(1, d.splitk)})",
+                               "achieved": round(kt, 1), "peak": FP8_PEAK_TFLOPS, "unit": "TFLOP/s",
+                               "frac": round(kt / FP8_PEAK_TFLOPS, 4),
+                               "traffic": (round(pmc["fp8_gemm"]["traffic_bytes"]) if "fp8_gemm" in pmc else None),
+                               "kernel_avg_us": round(kd * 1e6, 2), "flop_per_launch": call_flop(c)}
     return out
 
 

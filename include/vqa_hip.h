@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 15
+#define VQA_ABI_VERSION 16
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -121,19 +121,12 @@ typedef struct vqa_gemm_desc {
    * at 0, i.e. exactly the masks of z separate launches (0: one site, index (z*m+row)*n+col) */
   long long stride_bias;
   int drop_site_stride;
-  /* rownorm != 0: T5 RMSNorm (TF modeling_t5.py:50-72) folded into the GEMM -- A holds the
-   * UNnormalised rows x (bf16), B the weight with the norm weight folded into its columns
-   * (vqa_scale_cols_bf16), and each output row is scaled by rsqrt(mean_k(x^2) + rownorm_eps),
-   * the row's sum of squares accumulated from the A fragments the k-loop stages anyway.
-   * A k-contiguous, no implicit im2col, no split-K, batch 1. */
-  int rownorm;
-  float rownorm_eps;
   /* fp8 != 0: e4m3 (OCP float8_e4m3fn) operands for the forward weight GEMMs of BASELINE
    * configs[4] ("fp8 MFMA weights"): a = X8 [m][k] bytes (lda in bytes), b = W8 [n][k] bytes
    * (a_trans = b_trans = 0), both row-wise quantised by vqa_quant_rows_fp8; the accumulator
    * is scaled by scale_a[z*stride_scale_a + row] * scale_b[z*stride_scale_b + col] before the
    * epilogue (bias / residual / ReLU / dropout as usual).  k and lda / ldb multiples of 16,
-   * n % 4 == 0, no conv operand, no rownorm, no GELU / tanh.  Products of e4m3 values are
+   * n % 4 == 0, no conv operand, no GELU / tanh.  Products of e4m3 values are
    * exact in fp32, so the result differs from an fp32 GEMM of the dequantised operands only
    * by accumulation order. */
   int fp8;
@@ -246,17 +239,6 @@ int vqa_attn_probs(const vqa_attn_desc* d, hipStream_t stream);
  *     i.e. the bias gradient of the Linear feeding the dropout (fused). */
 int vqa_rmsnorm_fwd(const float* x, const float* w, float* y32, void* y16, float* rstd, int rows, int d, float eps,
                     const vqa_dropout* drop, hipStream_t stream);
-/* Several RMSNorm forwards of `rows` x d rows in one launch (bf16 output and rstd only, no
- * dropout): the normalised T5 layer inputs the weight gradients read, computed off the
- * forward chain once its GEMMs take the unnormalised rows (vqa_gemm_desc.rownorm).
- * jobs: device array of njobs descriptors. */
-typedef struct vqa_rmsnorm_job {
-  const float* x; const float* w; void* y16; float* rstd;
-} vqa_rmsnorm_job;
-int vqa_rmsnorm_fwd_batched(const vqa_rmsnorm_job* jobs, int njobs, int rows, int d, float eps, hipStream_t stream);
-/* out16[r][c] = bf16(w[r][c] * g[c]) for an n x k fp32 weight: a Linear's weight with the
- * preceding RMSNorm's weight folded into its input columns (vqa_gemm_desc.rownorm). */
-int vqa_scale_cols_bf16(const float* w, const float* g, void* out16, int n, int k, hipStream_t stream);
 int vqa_rmsnorm_bwd(const float* dy, const float* x, const float* rstd, const float* w, const float* dres,
                     float* dx32, void* dx16, float* dw, float dw_beta, float* ws, int rows, int d,
                     const vqa_dropout* drop_dy, const vqa_dropout* drop_dx32, const vqa_dropout* drop_dx16,

@@ -59,7 +59,24 @@ def dropout_key(seed, counter, site):
 
 
 def dropout_multiplier(p, seed, counter, site, n):
-    """float32 [n]: 1/(1-p) where element e is kept, 0 where dropped."""
+    """float32 [n]: 1/(1-p) where element e is kept, 0 where dropped.  The 32-bit hash runs on
+    int64 torch tensors (multi-threaded; products wrap mod 2^64 and are masked to their low 32
+    bits, so every value equals the uint32 arithmetic of _mix32 -- tests/test_dropout_cpu.py)."""
+    key = dropout_key(seed, counter, site)
+    e = torch.arange(n, dtype=torch.int64)
+    x = ((e * 0x9E3779B9) + key) & _M32
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    h = x ^ (x >> 16)
+    thresh = int(float(np.float32(p)) * 4294967296.0)
+    scale = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p)))
+    return torch.where(h >= thresh, scale, 0.0).to(torch.float32).numpy()
+
+
+def dropout_multiplier_np(p, seed, counter, site, n):
+    """The same multipliers from the numpy uint64 form of the hash (tests compare the two)."""
     key = dropout_key(seed, counter, site)
     e = np.arange(n, dtype=np.uint64)
     h = _mix32(((e * np.uint64(0x9E3779B9)) + np.uint64(key)) & np.uint64(_M32))

@@ -201,16 +201,12 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
   P.drop = d->drop;
   P.sbias = d->stride_bias;
   P.dsite = d->drop_site_stride;
-  VQA_REQUIRE(!d->rownorm || (!d->a_trans && !d->a_conv && d->splitk <= 1 && d->batch == 1 && d->rownorm_eps > 0.f),
-              "vqa_gemm: rownorm needs a k-contiguous plain A, no split-K, batch 1 and eps > 0");
-  P.rownorm = d->rownorm;
-  P.rn_eps = d->rownorm_eps;
   P.qsa = P.qsb = nullptr;
   P.sqa = P.sqb = 0;
   if (d->fp8) {
     // e4m3 operands: bytes, staged by the bf16 loaders as 2-byte units (128 fp8 per 64-unit k-tile)
-    VQA_REQUIRE(!d->a_trans && !d->b_trans && !d->a_conv && !d->b_conv && !d->rownorm && d->relu <= 1,
-                "vqa_gemm(fp8): k-contiguous A and B, no conv operand, no rownorm, ReLU at most");
+    VQA_REQUIRE(!d->a_trans && !d->b_trans && !d->a_conv && !d->b_conv && d->relu <= 1,
+                "vqa_gemm(fp8): k-contiguous A and B, no conv operand, ReLU at most");
     VQA_REQUIRE(d->k % 16 == 0 && d->lda % 16 == 0 && d->ldb % 16 == 0 && d->stride_a % 2 == 0 &&
                     d->stride_b % 2 == 0 && d->n % 4 == 0,
                 "vqa_gemm(fp8): k, lda, ldb multiples of 16 bytes, even strides, n %% 4 == 0");

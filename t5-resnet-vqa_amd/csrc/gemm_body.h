@@ -81,12 +81,6 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  // rownorm: this lane's share of sum_k A[row]^2 for its fragment rows (row l&31 of block i;
-  // lanes l and l^32 see the two 8-wide halves of every 16-deep k-step)
-  float sq[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) sq[i] = 0.f;
-  const bool rown = AKC && !GA && P.rownorm;
 
   const int nk_all = (P.k + BKT - 1) / BKT;
   const int kb = S > 1 ? slice * P.kper : 0;                  // this slice's first k-tile
@@ -149,16 +143,6 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
         wait_lgkm<R>();
       } else {
         wait_lgkm<0>();
-      }
-      if (rown) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint32_t u = (uint32_t)fa[s & 1][i][q];
-            const float lo = __uint_as_float(u << 16), hi = __uint_as_float(u & 0xffff0000u);
-            sq[i] = fmaf(lo, lo, fmaf(hi, hi, sq[i]));
-          }
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -238,17 +222,6 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
       }
   }
 
-  if (rown) {                                          // the RMSNorm row scale (no split-K: host check)
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float t = sq[i] + __shfl_xor(sq[i], 32);
-      const float r = rsqrtf(t / (float)P.k + P.rn_eps);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] *= r;
-    }
-  }
   if constexpr (F8) {                                  // acc(m, n) * scale_a[m] * scale_b[n]
     const float* qa = P.qsa + (long)z * P.sqa;
     const float* qb = P.qsb + (long)z * P.sqb;

@@ -33,8 +33,6 @@ struct GemmParams {
   unsigned* cnt;           // [batch][tile] arrival counters (zero between launches)
   long sbias;              // bias stride per batch element
   int dsite;               // != 0: batch z uses dropout site + z*dsite, element indices from 0
-  int rownorm;             // scale output rows by rsqrt(mean_k(A^2) + rn_eps) (vqa_gemm_desc.rownorm)
-  float rn_eps;
   // fp8 (e4m3) operands (vqa_gemm_desc.fp8): a / b hold bytes (lda, ldb, k, sa, sb in units of
   // 2 bytes, so the bf16 loaders stage them unchanged); acc(m, n) is scaled by qsa[m] * qsb[n]
   const float* qsa; const float* qsb;

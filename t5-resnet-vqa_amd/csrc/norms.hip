@@ -178,44 +178,6 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* __restric
   }
 }
 
-// several RMSNorm forwards in one launch (blockIdx.y = job): bf16 output + rstd, no dropout
-template <int NV>
-__global__ __launch_bounds__(256) void rmsnorm_fwd_batched_kernel(const vqa_rmsnorm_job* __restrict__ jobs, int rows,
-                                                                  float eps) {
-  const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  constexpr int D = NV * 256;
-  const vqa_rmsnorm_job jb = jobs[blockIdx.y];
-  float v[NV][4], g[NV][4];
-  load_row<NV>(jb.x + (long)row * D, v);
-  load_vec<NV>(jb.w, g);
-  float ss = 0.f;
-#pragma unroll
-  for (int i = 0; i < NV; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) ss += v[i][j] * v[i][j];
-  ss = wave_sum(ss);
-  const float r = rsqrtf(ss / D + eps);
-#pragma unroll
-  for (int i = 0; i < NV; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[i][j] = g[i][j] * (v[i][j] * r);
-  store_row16<NV>((bf16_t*)jb.y16 + (long)row * D, v);
-  if (jb.rstd && (threadIdx.x & 63) == 0) jb.rstd[row] = r;
-}
-
-// out16[r][c] = bf16(w[r][c] * g[c]), 4 columns per thread
-__global__ __launch_bounds__(256) void scale_cols_bf16_kernel(const float4* __restrict__ w, const float4* __restrict__ g,
-                                                              uint2* __restrict__ out, long total4, int k4) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total4) return;
-  const float4 a = w[i], b = g[i % k4];
-  uint2 u;
-  u.x = (uint32_t)f2bf(a.x * b.x) | ((uint32_t)f2bf(a.y * b.y) << 16);
-  u.y = (uint32_t)f2bf(a.z * b.z) | ((uint32_t)f2bf(a.w * b.w) << 16);
-  out[i] = u;
-}
-
 // ------------------------------------------------------------------ LayerNorm
 template <int NV>
 __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gam,
@@ -434,24 +396,6 @@ extern "C" int vqa_rmsnorm_fwd(const float* x, const float* w, float* y32, void*
   DISPATCH_NV(d, hipLaunchKernelGGL(rmsnorm_fwd_kernel<NV>, grid, dim3(256), 0, s, x, w, y32, (bf16_t*)y16, rstd,
                                     rows, eps, dr(drop)));
   return vqa::check_launch("vqa_rmsnorm_fwd");
-}
-
-extern "C" int vqa_rmsnorm_fwd_batched(const vqa_rmsnorm_job* jobs, int njobs, int rows, int d, float eps,
-                                       hipStream_t s) {
-  VQA_REQUIRE(jobs && njobs > 0 && njobs <= 65535 && rows > 0 && d % 256 == 0,
-              "vqa_rmsnorm_fwd_batched: bad arguments");
-  dim3 grid(vqa::cdiv(rows, ROWS_PER_BLOCK), njobs);
-  DISPATCH_NV(d, hipLaunchKernelGGL(rmsnorm_fwd_batched_kernel<NV>, grid, dim3(256), 0, s, jobs, rows, eps));
-  return vqa::check_launch("vqa_rmsnorm_fwd_batched");
-}
-
-extern "C" int vqa_scale_cols_bf16(const float* w, const float* g, void* out16, int n, int k, hipStream_t s) {
-  VQA_REQUIRE(w && g && out16 && n > 0 && k > 0 && k % 4 == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)g & 15) == 0 &&
-              ((uintptr_t)out16 & 7) == 0, "vqa_scale_cols_bf16: bad arguments (k %% 4 == 0, aligned pointers)");
-  const long total4 = (long)n * (k / 4);
-  hipLaunchKernelGGL(scale_cols_bf16_kernel, dim3(vqa::cdiv(total4, 256)), dim3(256), 0, s, (const float4*)w,
-                     (const float4*)g, (uint2*)out16, total4, k / 4);
-  return vqa::check_launch("vqa_scale_cols_bf16");
 }
 
 extern "C" int vqa_norm_bwd_parts(int rows) { return vqa::cdiv(rows, NORM_BWD_ROWS); }

@@ -70,9 +70,29 @@ def plan_shards(buckets, world, align=64):
     return out
 
 
+def _after(stream, other):
+    """`stream` waits for everything issued so far on `other` (an event, no host sync)."""
+    if stream is other:
+        return
+    ev = torch.cuda.Event()
+    ev.record(other)
+    stream.wait_event(ev)
+
+
 class _Done:
     """A completed collective (host-staged gloo path): wait() is a no-op."""
     def wait(self):
+        return True
+
+
+class _Then:
+    """A collective followed by a device copy on the waiting stream (issued at wait())."""
+    def __init__(self, work, then):
+        self.work, self.then = work, then
+
+    def wait(self):
+        self.work.wait()
+        self.then()
         return True
 
 
@@ -160,6 +180,7 @@ class DataParallelStep:
                                  keep=(self.GIDS, self.GDH, self.WS, e.g32["t5.embed"]))
         if self.shard:
             self._plan_sharded_optimizer()
+        self._plan_schedule()
         self.graphs = None
         # exposed-communication timing (bench at N > 1): HIP events on the compute stream right
         # before and after each collective's wait, i.e. how long the step's stream stalls on it
@@ -201,6 +222,11 @@ class DataParallelStep:
                 int(e.warmup), int(e.total), float(e.betas[0]), float(e.betas[1]), e.opt_state)
         self.finalize_call = fin[0]
         self.adam_calls = [e.adam_range_call(lo, hi) for lo, hi in ranges]
+        # reduce-scatter outputs, one slice per bucket (several are in flight at once); each is
+        # copied into the rank's chunk of G32 once its collective is done
+        offs = np.concatenate([[0], np.cumsum([c for _, c, _ in self.shards])]).astype(np.int64)
+        self.rs_off = [int(o) for o in offs[:-1]]
+        self.RS_OUT = torch.empty(max(int(offs[-1]), 1), dtype=torch.float32, device=e.dev)
 
     def _sharded_collectives_after(self, bk_index):
         """Reduce-scatter of bucket `bk_index`'s chunks (owner r receives the sum of chunk r)
@@ -218,7 +244,11 @@ class DataParallelStep:
                 mine.copy_(h[r * c:(r + 1) * c])
                 works.append(_Done())
             else:
-                works.append(dist.reduce_scatter_tensor(mine, full, group=self.group, async_op=True))
+                # into a separate buffer (no reliance on RCCL's in-place aliasing rule), then
+                # copied into the own chunk on the NCCL work's completion (the wait below)
+                out = self.RS_OUT[self.rs_off[bk_index]:self.rs_off[bk_index] + c]
+                works.append(_Then(dist.reduce_scatter_tensor(out, full, group=self.group, async_op=True),
+                                   lambda out=out, mine=mine: mine.copy_(out)))
         if b > a + N * c:
             works += allreduce_buckets(e.G32, [(None, a + N * c, b)], self.group)
         return [_All(works)]
@@ -255,6 +285,10 @@ class DataParallelStep:
                     full.copy_(torch.cat(parts))
                 else:
                     dist.all_gather_into_tensor(full, mine.clone(), group=self.group)
+        if e.fp8 and not e.defer_opt:
+            # the e4m3 weight copies follow the gathered masters (a deferred update requantizes
+            # them range by range in the next forward: its _Seq(AdamW range, quant) calls)
+            self._run(e.quant_all)
 
     def sync_optimizer_state(self):
         """Sharded optimizer: all-gather the AdamW moments of every chunk (each rank holds only
@@ -280,6 +314,40 @@ class DataParallelStep:
         s = L.stream_handle()
         for c in calls:
             c(s)
+
+    # ------------------------------------------------------------------ schedule
+    def _plan_schedule(self):
+        """Place every backward segment as the single-GPU step graph places its calls
+        (engine.run_backward_streams): the input-gradient chain on the step's stream, the
+        side-tagged weight-gradient GEMMs (engine.dw_stream) on `wside` behind the chain, the
+        ConvTranspose2d scaler dW segment on `side` beside the T5 backward, and the squared-norm
+        partials of [0, a) on `side` as soon as the bucket holding `a` is reduced.  Each segment
+        is split into a chain part and a side part, replayed as two graphs: the next segment's
+        chain does not wait for this segment's weight gradients, and the bucket's collective is
+        issued on the stream that finishes the bucket (wside when the segment has side calls), so
+        it starts only once every gradient of the bucket is final."""
+        e = self.eng
+        self.parts = []                                     # per segment: (home, chain calls, side calls)
+        q0, q1 = e._bsplit                                  # DP call index == engine bwd_calls index
+        prev = 0
+        for k, seg in enumerate(self.segments):
+            lo, hi = prev, prev + len(seg)
+            prev = hi
+            home = "side" if (lo, hi) == (q0, q1) else "main"
+            if e.dw_stream:
+                chain, side = [c for c in seg if not c.side], [c for c in seg if c.side]
+            else:
+                chain, side = list(seg), []
+            self.parts.append((home, chain, side))
+        # the grad-norm partials of [0, a) (opt_calls[0]) need the buckets up to `a` reduced
+        self.sq_after = None
+        if not self.shard and e._sq_split is not None:
+            a = e._sq_split[1]
+            for k, (_, _, stop) in enumerate(self.buckets):
+                if stop >= a:
+                    self.sq_after = k
+                    break
+        self.opt_part = e.opt_calls[1:] if self.sq_after is not None else e.opt_calls
 
     def capture(self):
         e = self.eng
@@ -311,10 +379,16 @@ class DataParallelStep:
         gs["fwd"] = [g]
         if e.pipeline:                                      # the next batch's ResNet, replayed beside the step
             cap("res", e.res_calls)
-        for seg in self.segments:
-            cap("seg", seg)
+        for _, chain, side in self.parts:
+            cap("chain", chain)
+            if side:
+                cap("side", side)
+            else:
+                gs.setdefault("side", []).append(None)
         cap("tail", self.tail + [self.emb_call])
-        cap("opt", e.opt_calls)
+        if self.sq_after is not None:
+            cap("sq0", e.opt_calls[:1])
+        cap("opt", self.opt_part)
         return gs
 
     def _res_begin(self):
@@ -325,9 +399,7 @@ class DataParallelStep:
             return
         main = torch.cuda.current_stream(e.dev)
         e.copy_f4(L.stream_handle(main))
-        ev = torch.cuda.Event()
-        ev.record(main)
-        e._rstream.wait_event(ev)
+        _after(e._rstream, main)
         with torch.cuda.stream(e._rstream):
             if self.graphs is not None:
                 self.graphs["res"][0].replay()
@@ -337,49 +409,66 @@ class DataParallelStep:
     def _res_end(self):
         e = self.eng
         if e.pipeline:
-            ev = torch.cuda.Event()
-            ev.record(e._rstream)
-            torch.cuda.current_stream(e.dev).wait_event(ev)
+            _after(torch.cuda.current_stream(e.dev), e._rstream)
 
     def step(self):
         e = self.eng
+        g = self.graphs
+        main = torch.cuda.current_stream(e.dev)
+        streams = {"main": main, "side": e._side}
+        wside = e._wside
+
+        def play(name, k, calls):
+            if g is not None:
+                g[name][k].replay()
+            else:
+                self._run(calls)
         self._res_begin()
+        if g is not None:
+            g["fwd"][0].replay()
+        else:
+            e.forward()
         exchange = (lambda i, bk: self._sharded_collectives_after(i)) if self.shard else \
             (lambda i, bk: allreduce_buckets(e.G32, [bk], self.group))
-        if self.graphs is None:
-            e.forward()
-            works = []
-            for i, (seg, bk) in enumerate(zip(self.segments, self.buckets)):
-                self._run(seg)
-                works += exchange(i, bk)
-            works += gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
-            for w in works[-2:]:
-                w.wait()
-            self._run(self.tail + [self.emb_call])
-            for w in works[:-2]:
-                w.wait()
-            if self.shard:
-                self._sharded_optimizer()
-            else:
-                self._run(e.opt_calls)
-            self._res_end()
-            return
-        g = self.graphs
-        g["fwd"][0].replay()
-        works = []
-        for i, (seg, bk) in enumerate(zip(g["seg"], self.buckets)):
-            seg.replay()
-            works += exchange(i, bk)
-        works += gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
+        works, rows = [], None
+        nseg = len(self.parts)
+        for k, ((home, chain, side), bk) in enumerate(zip(self.parts, self.buckets)):
+            hs = streams[home]
+            if hs is not main:
+                _after(hs, main)                            # the scaler segment forks off the chain here
+            with torch.cuda.stream(hs):
+                play("chain", k, chain)
+            if k == nseg - 1:
+                # the embedding rows (dH32) are final with the last chain segment: gather them
+                # before the last bucket's collective, whose weight gradients still run
+                rows = gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
+            last = hs
+            if side:
+                _after(wside, hs)
+                with torch.cuda.stream(wside):
+                    play("side", k, side)
+                last = wside
+            with torch.cuda.stream(last):
+                works += exchange(k, bk)
+            if k == self.sq_after:                          # grad-norm partials of [0, a), beside the rest
+                sd = streams["side"]
+                for st in (main, wside):
+                    _after(sd, st)
+                with torch.cuda.stream(sd):
+                    for w in works:
+                        w.wait()
+                    play("sq0", 0, e.opt_calls[:1])
         evs = []
-        self._wait(works[-2:], evs)                         # the embedding rows: needed by the tail
-        g["tail"][0].replay()
-        for w in works[:-2]:
+        self._wait(rows, evs)                               # the embedding rows: needed by the tail
+        play("tail", 0, self.tail + [self.emb_call])
+        for w in works:
             self._wait([w], evs)
+        for st in (streams["side"], wside):                 # every segment's work (gloo: staged copies)
+            _after(main, st)
         if self.shard:
             self._sharded_optimizer()
         else:
-            g["opt"][0].replay()
+            play("opt", 0, self.opt_part)
         self._res_end()
         if self.timing:
             self._ev.append(evs)

@@ -84,7 +84,7 @@ def _gemm_key(d):
     return (d.m, d.n, d.k, d.batch, d.a_trans, d.b_trans, d.a_conv, d.b_conv,
             geo(d.ga) if d.a_conv else None, geo(d.gb) if d.b_conv else None,
             bool(d.c32), bool(d.c16), bool(d.bias), bool(d.res32), bool(d.res16), bool(d.mask16), d.relu,
-            d.beta != 0.0, d.drop.p > 0.0) + (("rownorm",) if d.rownorm else ()) + (("fp8",) if d.fp8 else ())
+            d.beta != 0.0, d.drop.p > 0.0) + (("fp8",) if d.fp8 else ())
 
 
 class _Seq:
@@ -205,8 +205,8 @@ class VQAEngine:
         # AdamW of step k applied inside step k+1's forward (see _plan_optimizer)
         self.defer_opt = bool(defer_optimizer)
         # weight-gradient GEMMs (calls tagged `side`) on a stream of their own beside the
-        # input-gradient chain: on by default for the single-GPU grouping, off for DP groups
-        self.dw_stream = self._default_dw if dw_stream is None else bool(dw_stream)
+        # input-gradient chain (single GPU and DP alike; dp.DataParallelStep keeps the placement)
+        self.dw_stream = True if dw_stream is None else bool(dw_stream)
         self.T = batch * seq_len
         self.lay = ParamLayout(vision, answer_spaces, num_blocks, dm)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
@@ -1354,9 +1354,10 @@ class VQAEngine:
     def _run_tagged(self, calls, main, wside):
         """Run `calls` in order on `main`, except runs of side-tagged calls (weight
         gradients), which go to `wside` after an event on `main` at that point
-        (`dw_stream`).  On for the single-GPU weight-gradient grouping (9, 3), where the
-        batched T5 dW launches trail the input-gradient chain (6.66 vs 6.78-6.84 ms per
-        step); off for the DP grouping, whose buckets must be final in chain order.  Every
+        (`dw_stream`, on by default): the batched T5 dW launches trail the input-gradient chain
+        (6.66 vs 6.78-6.84 ms per step).  dp.DataParallelStep replays each backward segment's
+        side-tagged calls as their own graph on the same stream, the segment's gradient bucket
+        all-reduced behind them (so a bucket is final when its collective starts).  Every
         bf16 gradient a side-tagged call reads has its own buffer (_gbuf), so no later chain
         call overwrites it (tests: test_dw_stream_matches_single_stream_bitwise)."""
         if not self.dw_stream:
@@ -1571,7 +1572,7 @@ class VQAEngine:
                     for sk in SPLITS:
                         # split only grids that leave CUs idle, with >= 2 k-tiles per slice
                         if sk > 1 and (tiles >= 512 or nk < 2 * sk or tiles > 16384 or d.a_conv == 2
-                                       or cfg in L.GEMM_BK128 or d.rownorm):
+                                       or cfg in L.GEMM_BK128):
                             continue
                         d.config = cfg
                         ops.set_splitk(d, sk)

@@ -48,7 +48,6 @@ class GemmDesc(ctypes.Structure):
         ("drop", Dropout),
         ("splitk", c_int), ("workspace", c_void_p), ("workspace_bytes", c_ll),
         ("stride_bias", c_ll), ("drop_site_stride", c_int),
-        ("rownorm", c_int), ("rownorm_eps", c_float),
         ("fp8", c_int), ("scale_a", c_void_p), ("scale_b", c_void_p),
         ("stride_scale_a", c_ll), ("stride_scale_b", c_ll),
     ]
@@ -62,11 +61,6 @@ class ImageDesc(ctypes.Structure):
 class ColsumJob(ctypes.Structure):
     _fields_ = [("ws", c_void_p), ("out", c_void_p), ("stride", c_ll), ("parts", c_int), ("cols", c_int),
                 ("beta", c_float), ("first_block", c_int)]
-
-
-class RmsNormJob(ctypes.Structure):
-    """vqa_rmsnorm_job: one RMSNorm of vqa_rmsnorm_fwd_batched."""
-    _fields_ = [("x", c_void_p), ("w", c_void_p), ("y16", c_void_p), ("rstd", c_void_p)]
 
 
 class AttnDesc(ctypes.Structure):
@@ -170,8 +164,6 @@ def register(name, *argtypes):
 
 P = c_void_p
 register("vqa_rmsnorm_fwd", P, P, P, P, P, c_int, c_int, c_float, P)
-register("vqa_rmsnorm_fwd_batched", P, c_int, c_int, c_int, c_float)
-register("vqa_scale_cols_bf16", P, P, P, c_int, c_int)
 register("vqa_rmsnorm_bwd", P, P, P, P, P, P, P, P, c_float, P, c_int, c_int, P, P, P)
 register("vqa_layernorm_fwd", P, P, P, P, P, P, P, c_int, c_int, c_float)
 register("vqa_layernorm_bwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P, P)

@@ -30,7 +30,7 @@ def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None
               bias=None, res32=None, res16=None, ldres=0, mask16=None, ldmask=0, alpha=1.0, beta=0.0,
               relu=False, ga=None, gb=None, batch=1, stride_a=0, stride_b=0, stride_c32=0, stride_c16=0,
               stride_res=0, splitk=0, workspace=None, stride_bias=0, drop_site_stride=0, a_patch=False,
-              rownorm_eps=0.0, fp8=False, scale_a=None, scale_b=None, stride_scale_a=0, stride_scale_b=0):
+              fp8=False, scale_a=None, scale_b=None, stride_scale_a=0, stride_scale_b=0):
     """fp8: a / b are e4m3 byte tensors (lda, ldb, k, strides in bytes = elements) with fp32 row
     scales scale_a [m] / scale_b [n] (vqa_gemm_desc.fp8)."""
     op_t = torch.uint8 if fp8 else torch.bfloat16
@@ -62,7 +62,6 @@ def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None
     d.batch, d.stride_a, d.stride_b = batch, stride_a, stride_b
     d.stride_c32, d.stride_c16, d.stride_res = stride_c32, stride_c16, stride_res
     d.stride_bias, d.drop_site_stride = stride_bias, drop_site_stride
-    d.rownorm, d.rownorm_eps = int(rownorm_eps > 0.0), rownorm_eps      # RMSNorm of A's rows folded in
     d.fp8, d.scale_a, d.scale_b = int(fp8), addr(scale_a), addr(scale_b)
     d.stride_scale_a, d.stride_scale_b = stride_scale_a, stride_scale_b
     set_splitk(d, splitk, workspace)

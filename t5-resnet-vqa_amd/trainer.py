@@ -177,6 +177,10 @@ class VQATrainer:
     # checkpoint written here loads into the reference's optimizer and back.
     def _param_groups(self):
         m = self.model
+        if not hasattr(m.engine, "optimizer_state"):
+            raise NotImplementedError("optimizer / scheduler checkpoints are implemented for ResnetVQAModel; the "
+                                      "ViT model (vit_vqa_trainer.py:300-323) checkpoints its weights only here "
+                                      "(model.state_dict())")
         scaler = "downscale_layer" if m.vision_model_name == "resnet50" else "upscale_layer"
         names = [("vision_model", "Vision Model"), ("lang_model", "Language Model"),
                  (scaler, "DownScaler Layer" if scaler == "downscale_layer" else "UpScaler Layer"),
@@ -193,7 +197,10 @@ class VQATrainer:
         return groups
 
     def optimizer_state_dict(self):
-        """torch.optim.AdamW(amsgrad=True).state_dict() of the reference's parameter groups."""
+        """torch.optim.AdamW(amsgrad=True).state_dict() of the reference's parameter groups.
+        With the sharded DP optimizer this is a COLLECTIVE (every rank's chunk moments are
+        all-gathered first): call it on every rank, as save_state_dict_checkpoint does."""
+        self._param_groups()                               # fails early for models without this state
         e = self.model.engine
         if self._dp is not None:
             self._dp.sync_optimizer_state()                # sharded: every chunk's moments on this rank
@@ -227,13 +234,23 @@ class VQATrainer:
                 "_get_lr_called_within_step": False, "_last_lr": [b * self._lr_factor(step) for b in base],
                 "lr_lambdas": [None] * len(base)}
 
-    def save_state_dict_checkpoint(self, path, epoch):
+    def save_state_dict_checkpoint(self, path, epoch, write=None):
         """callbacks.py:118-125: torch.save({'epoch', 'scheduler', 'optimizer'}) (+ this engine's
-        dropout RNG counter, so a resumed run draws the same masks)."""
+        dropout RNG counter, so a resumed run draws the same masks).
+
+        Data parallel: call it on EVERY rank (the sharded optimizer gathers the moments with
+        collectives; a save guarded by `if rank == 0` would leave rank 0 waiting for the others).
+        Only the ranks with `write` true write the file -- by default rank 0 of the process group
+        when training data-parallel, every caller otherwise."""
         e = self.model.engine
+        opt = self.optimizer_state_dict()                  # collective under the sharded optimizer
+        if write is None:
+            write = not self.data_parallel or torch.distributed.get_rank(self.process_group) == 0
+        if not write:
+            return
         rng = e.optimizer_state()[4]
         torch.save({"epoch": int(epoch), "scheduler": self.scheduler_state_dict(),
-                    "optimizer": self.optimizer_state_dict(), "vqa_rng": torch.from_numpy(rng.astype(np.int64))}, path)
+                    "optimizer": opt, "vqa_rng": torch.from_numpy(rng.astype(np.int64))}, path)
 
     def load_state_dict_checkpoint(self, path):
         """faster_rcnn_vqa_trainer.py:269-277: resume the optimizer (and the schedule position) from

@@ -1,6 +1,6 @@
 """The benched step (BASELINE configs[1]) against the CPU oracle.
 
-  python tests/bench_step_worker.py OUT.json      (stand-alone: writes the report to OUT.json)
+  python tests/bench_step_worker.py OUT.json [dp]   (stand-alone: writes the report to OUT.json)
 
 `run()` is called in the pytest session process by
 tests/test_z_bench_step_gpu.py::test_bench_step_b64_matches_oracle, after every other GPU
@@ -35,16 +35,36 @@ def _dev(nb):
     return {k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None}
 
 
-def run():
-    """Build, tune, capture and step the benched engine against the oracle; returns (report, fails)."""
+def _world1_group():
+    """A world-1 RCCL process group for the DP mode (bench.py --dp), unless one exists."""
+    import socket
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return False
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    return True
+
+
+def run(mode="engine"):
+    """Build, tune, capture and step the benched engine against the oracle; returns (report, fails).
+    mode "dp": the N > 1 step at world 1 -- dp.DataParallelStep over a world-1 RCCL group on the
+    DP engine (T5 weight-gradient groups dp.DP_T5_DW_GROUPS), built as `bench.py --dp` builds it."""
     pkg = load_package()
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     B, L, H = 64, 32, 224
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    dp = mode == "dp"
+    own_pg = _world1_group() if dp else False
     # bench.py main(): same constructor arguments, same priming / tuning / capture sequence
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, warmup=10, total=100000,
-                               dropout=0.1, seed=0, pipeline=True, t5_dw_group=None)
-    assert eng.defer_opt and eng.pipeline
+                               dropout=0.1, seed=0, pipeline=True,
+                               t5_dw_group=pkg.dp.DP_T5_DW_GROUPS if dp else None)
+    assert eng.defer_opt and eng.pipeline and eng.dw_stream
     nsteps = 3
     nbs = [pkg.synthetic.make_batch(B, L, H, seed=1 + i) for i in range(nsteps + 1)]
     pool = [_dev(nb) for nb in nbs]
@@ -54,7 +74,12 @@ def run():
     eng.forward()
     eng.backward()
     eng.autotune(table=TABLE)
-    eng.capture()
+    if dp:
+        dps = pkg.dp.DataParallelStep(eng, use_graph=True)
+        step = dps.step
+    else:
+        eng.capture()
+        step = eng.train_step
     eng.prime(pool[0]["image_tensors"])
     splitk = sum(1 for c in eng.res_calls + eng.fwd_calls + eng.bwd_calls if c.name == "vqa_gemm" and c.desc.splitk > 1)
 
@@ -65,7 +90,7 @@ def run():
     for i in range(nsteps):
         ot.rng_counter = int(eng.RNG[1].item())             # the same dropout draw (engine bumps, then uses)
         eng.load_batch(pool[i], next_images=pool[i + 1]["image_tensors"])
-        eng.train_step()
+        step()
         torch.cuda.synchronize()
         lp, loss, gn = eng.LOGP.cpu().numpy(), float(eng.LOSS.item()), eng.last_grad_norm()
         ggn = eng.group_grad_norms()
@@ -96,14 +121,20 @@ def run():
             den += float((do ** 2).sum())
         delta[g] = (num / den) ** 0.5 if den > 0 else 0.0
     rep["update_rel_l2"] = delta
+    rep["mode"] = mode
+    if dp:
+        rep["buckets"] = len(dps.buckets)
     torch.cuda.synchronize()
+    if own_pg:
+        import torch.distributed as dist
+        dist.destroy_process_group()
     return rep, fails
 
 
-def main(out_path):
-    rep, fails = run()
+def main(out_path, mode="engine"):
+    rep, fails = run(mode)
     json.dump({"report": rep, "fails": fails}, open(out_path, "w"), indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], *sys.argv[2:3])

@@ -2,11 +2,13 @@
 the gloo backend (several ranks share the one GPU of the test box; RCCL refuses two ranks
 on one device).  Rank r trains on samples [r*B, (r+1)*B) of each global batch.
 
-  python tests/dp_worker.py RANK WORLD PORT OUT.npz STEPS PIPELINE GRAPH [trainer|shard]
+  python tests/dp_worker.py RANK WORLD PORT OUT.npz STEPS PIPELINE GRAPH [trainer|shard|c5]
 
 `trainer`: drive the step through model.ResnetVQAModel + trainer.VQATrainer (data_parallel
 picked up from the initialised process group) instead of the engine directly; `shard`: the
-engine step with the sharded optimizer (reduce-scatter, AdamW on the own chunks, all-gather)."""
+engine step with the sharded optimizer (reduce-scatter, AdamW on the own chunks, all-gather);
+`c5`: the engine step at BASELINE configs[4] widths (T5-large, 6 SGA blocks, fp8 forward GEMMs,
+T5 weight-gradient groups (8, 8, 6, 2))."""
 import os
 import sys
 
@@ -25,26 +27,34 @@ def main():
     pkg = load_package()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    mode = sys.argv[8] if len(sys.argv) > 8 else "engine"
+    c5 = mode == "c5"
     B, L, H = 4, 32, 64
-    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    # c5: BASELINE configs[4] widths -- T5-large (24 layers, d 1024), 6 SGA blocks at 1024, e4m3
+    # forward weight GEMMs, the DP weight-gradient groups dp.dp_t5_dw_groups(24) = (8, 8, 6, 2)
+    ekw = dict(language_model="t5-large", num_blocks=6, fp8=True) if c5 else {}
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, **({"num_attention_blocks": 6, "language_model": "t5-large"}
+                                                              if c5 else {}))
     gb = [pkg.synthetic.make_batch(world * B, L, H, seed=40 + i) for i in range(steps + 1)]
     mine = [{k: (None if v is None else v[rank * B:(rank + 1) * B]) for k, v in nb.items()} for nb in gb]
     dev = [{k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None} for nb in mine]
-    if len(sys.argv) > 8 and sys.argv[8] == "trainer":
+    if mode == "trainer":
         tr = trainer_run(pkg, sd, B, L, H, dev, steps, graph)
         np.savez(out, **tr)
         dist.barrier()
         dist.destroy_process_group()
         return
+    groups = pkg.dp.dp_t5_dw_groups(24) if c5 else (4, 4, 3, 1)
     eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.0,
-                               seed=rank, pipeline=pipe, t5_dw_group=(4, 4, 3, 1), device="cuda:0")
+                               seed=rank, pipeline=pipe, t5_dw_group=groups, device="cuda:0", **ekw)
+    assert not c5 or (eng.t5_dw_groups == [8, 8, 6, 2] and eng.fp8)
     if pipe:
         eng.prime(dev[0]["image_tensors"])
         eng.F4.copy_(eng.F4N)
         eng.load_batch(dev[0], next_images=dev[1]["image_tensors"])
     else:
         eng.load_batch(dev[0])
-    shard = len(sys.argv) > 8 and sys.argv[8] == "shard"
+    shard = mode == "shard"
     step = pkg.dp.DataParallelStep(eng, bucket_mb=8, use_graph=graph, shard_optimizer=shard)
     if pipe:
         eng.prime(dev[0]["image_tensors"])

@@ -65,3 +65,21 @@ def test_oracle_train_mode_step_uses_dropout(pkg):
     assert not torch.equal(l2, l3)
     e0 = orc.OracleTrainer(sd, "resnet34", warmup=5, total=10, dropout=0.0)
     assert not torch.equal(e0.forward_backward(nb)[0], l1)
+
+
+def test_torch_hash_equals_uint32_hash():
+    """dropout_multiplier (int64 torch arithmetic, masked to 32 bits) == the numpy uint64 form,
+    element for element, across keys and sizes (incl. indices past 2^31)."""
+    for p, seed, counter, site, n in ((0.1, 0, 1, 16, 1 << 18), (0.5, 7, 123456, 5, 77777), (0.1, 3, 9, 131, 4099)):
+        np.testing.assert_array_equal(orc.dropout_multiplier(p, seed, counter, site, n),
+                                      orc.dropout_multiplier_np(p, seed, counter, site, n))
+    # the top of the index range: e * 0x9E3779B9 overflows int64 and must wrap like uint32 math
+    e = np.array([2**31 - 1, 2**31, 2**32 - 2], dtype=np.uint64)
+    key = orc.dropout_key(1, 2, 3)
+    ref = orc._mix32(((e * np.uint64(0x9E3779B9)) + np.uint64(key)) & np.uint64(0xFFFFFFFF))
+    x = ((torch.tensor(e.astype(np.int64)) * 0x9E3779B9) + key) & 0xFFFFFFFF
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    assert (x ^ (x >> 16)).numpy().astype(np.uint64).tolist() == ref.tolist()

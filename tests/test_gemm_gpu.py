@@ -399,55 +399,6 @@ def test_patch_configs_refused_elsewhere(ops, pkg):
         ops.run(d)
 
 
-@pytest.mark.parametrize("cfg", [0, 4, 6, 7, 21, 22, 23])
-@pytest.mark.parametrize("M,N,K", [(2048, 2304, 768), (64, 3072, 768), (100, 200, 256)])
-def test_rownorm_gemm_is_rmsnorm_then_linear(ops, pkg, M, N, K, cfg):
-    """rownorm: out = rsqrt(mean_k(x^2) + eps) * (x (W o w)^T) with the row statistic taken
-    from the bf16 A rows the k-loop stages; vqa_scale_cols_bf16 folds w into W.  Checked
-    against the fp32 evaluation of the same formula (tight), and against RMSNorm-then-Linear
-    on the fp32 rows (loose: bf16 rounding of x vs of the normalised rows)."""
-    x32 = torch.randn(M, K, device="cuda") * 3.0
-    w32 = (torch.rand(N, K, device="cuda") - 0.5) * 0.1
-    g = torch.rand(K, device="cuda") + 0.5
-    wf = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
-    pkg.lib.call("vqa_scale_cols_bf16", w32.data_ptr(), g.data_ptr(), wf.data_ptr(), N, K)
-    assert torch.equal(wf, (w32 * g).to(torch.bfloat16))
-    x16 = x32.to(torch.bfloat16)
-    out = torch.empty(M, N, device="cuda")
-    d = ops.gemm_desc(x16, wf, M, N, K, lda=K, ldb=K, c32=out, ldc32=N, rownorm_eps=1e-6)
-    d.config = cfg
-    ops.run(d)
-    torch.cuda.synchronize()
-    xf = x16.float()
-    r = torch.rsqrt(xf.pow(2).mean(1, keepdim=True) + 1e-6)
-    ref = r * (xf @ wf.float().T)
-    close(out, ref, (r * (xf.abs() @ wf.float().abs().T)).max().item())
-    n = (x32 * torch.rsqrt(x32.pow(2).mean(1, keepdim=True) + 1e-6) * g)
-    loose = n @ w32.T
-    rel = ((out - loose).norm() / loose.norm()).item()
-    assert rel < 1e-2, rel
-
-
-def test_rmsnorm_fwd_batched_matches_single(ops, pkg):
-    """vqa_rmsnorm_fwd_batched == vqa_rmsnorm_fwd (bf16 output, rstd) job by job."""
-    import ctypes
-    T, D = 300, 768
-    xs = [torch.randn(T, D, device="cuda") for _ in range(3)]
-    ws = [torch.rand(D, device="cuda") + 0.5 for _ in range(3)]
-    ys = [torch.empty(T, D, device="cuda", dtype=torch.bfloat16) for _ in range(3)]
-    rs = [torch.empty(T, device="cuda") for _ in range(3)]
-    jobs = (pkg.lib.RmsNormJob * 3)(*[pkg.lib.RmsNormJob(x.data_ptr(), w.data_ptr(), y.data_ptr(), r.data_ptr())
-                                       for x, w, y, r in zip(xs, ws, ys, rs)])
-    raw = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).cuda()
-    pkg.lib.call("vqa_rmsnorm_fwd_batched", raw.data_ptr(), 3, T, D, ctypes.c_float(1e-6))
-    for x, w, y, r in zip(xs, ws, ys, rs):
-        y1, r1 = torch.empty_like(y), torch.empty_like(r)
-        pkg.lib.call("vqa_rmsnorm_fwd", x.data_ptr(), w.data_ptr(), None, y1.data_ptr(), r1.data_ptr(), T, D,
-                     ctypes.c_float(1e-6), None)
-        torch.cuda.synchronize()
-        assert torch.equal(y, y1) and torch.equal(r, r1)
-
-
 def _fp8_deq(q, scale):
     """e4m3 bytes [rows, cols] + row scales -> fp64 values."""
     return q.view(torch.float8_e4m3fn).double() * scale.double()[:, None]

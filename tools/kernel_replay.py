@@ -2,10 +2,12 @@
 
   python tools/kernel_replay.py MANIFEST.json [REPS]
 
-Builds the engine exactly as bench.py does (B=64, 224x224, L=32, tuned tiles),
+Builds the engine exactly as bench.py does (B=64, 224x224, L=32, tuned tiles; mode c5: as
+bench.py --config5 builds it, 384x384, T5-large, 6 blocks, fp8),
 runs one forward/backward so every buffer holds real data, then replays, REPS
 times each and in this order: the whole-arena AdamW pass, the ConvTranspose2d
-weight-gradient GEMM, and every SGA launch bench.py's sga_mfma counts.  The
+weight-gradient GEMM, the largest e4m3 launch (config 5), and every SGA launch bench.py's
+sga_mfma counts.  The
 manifest lists (tag, kernel call name, FLOP, algorithmic bytes) per dispatch in
 issue order, so tools/pmc_step.py can map the LAST dispatches of a profile to
 them."""
@@ -21,14 +23,16 @@ from __graft_entry__ import load_package  # noqa: E402
 
 out_path = sys.argv[1]
 REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-MODE = sys.argv[3] if len(sys.argv) > 3 else "default"     # "res": every frozen-ResNet launch instead
-pkg = load_package()
+MODE = sys.argv[3] if len(sys.argv) > 3 else "default"     # "res": every frozen-ResNet launch instead;
+pkg = load_package()                                         # "c5": the config-5 engine (bench.py --config5)
 L = pkg.lib
 dev = torch.device("cuda", 0)
-B, Lq, H = 64, 32, 224
-sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+C5 = MODE == "c5"
+B, Lq, H = 64, 32, (384 if C5 else 224)
+lm, NB = ("t5-large", 6) if C5 else ("t5-base", 3)
+sd = pkg.synthetic.make_state_dict("resnet50", seed=0, num_attention_blocks=NB, language_model=lm)
 eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=Lq, image_size=H, device=dev, warmup=10,
-                           total=100000, dropout=0.1, seed=0)
+                           total=100000, dropout=0.1, seed=0, num_blocks=NB, language_model=lm, fp8=C5)
 del sd
 eng.load_batch(pkg.synthetic.make_batch(B, Lq, H, seed=1))
 eng.forward()
@@ -59,6 +63,10 @@ if MODE == "res":
 if MODE != "res":
     wg = eng.scaler_dw_call                                  # the tap-batched scaler dW GEMM
     plan.append(("convT_dW", wg, gemm_flop(wg), 0.0))
+    f8 = [c for c in eng.res_calls + eng.fwd_calls + eng.bwd_calls if c.name == "vqa_gemm" and c.desc.fp8]
+    if f8:                                                   # bench roofline_fp8: the largest e4m3 launch
+        c8 = max(f8, key=gemm_flop)
+        plan.append(("fp8_gemm", c8, gemm_flop(c8), 0.0))
     sga = [c for c in eng.sga_vision_calls + eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
            if c.name in ("vqa_gemm", "vqa_gemm_pair", "vqa_attn_fwd", "vqa_attn_bwd")]
     for c in sga:
