@@ -243,6 +243,8 @@ def main():
     ap.add_argument("--tune-save", default=None, help="write the tile choices used to this file")
     ap.add_argument("--model", choices=("resnet", "vit"), default="resnet",
                     help="vit: BASELINE configs[3], ViT-base + T5 encoder-decoder (1 GPU)")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP default 4; set before the runtime starts)")
     ap.add_argument("--dp", action="store_true",
                     help="N = 1: run the N > 1 step (dp.DataParallelStep over a world-1 RCCL group, the DP engine's "
                          "weight-gradient groups) instead of the single-GPU engine graph")
@@ -251,6 +253,9 @@ def main():
                          "gathers, capture, lockstep) on a one-GPU box; the timing is not a measurement")
     args = ap.parse_args()
 
+    if args.hw_queues:                             # before anything starts the HIP runtime
+        assert 1 <= args.hw_queues <= 16, args.hw_queues
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))          # one process per GPU, started before any GPU call
 

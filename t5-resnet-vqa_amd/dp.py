@@ -5,9 +5,10 @@ trainer/faster_rcnn_vqa_trainer.py:61-62; this is the build's added strategy,
 SURVEY.md §8e.)
 
 Step on every rank (identical initial weights, rank-local batch):
-  graph(forward) -> for each backward segment: graph(segment) ; async
-  all-reduce(SUM) of the gradient bucket that segment finalised  ->
-  all-gather of (token id, dH row) pairs -> deterministic embedding scatter ->
+  graph(forward) -> graph(backward, placed as the single-GPU step graph places it, an external
+  event recorded where each gradient bucket becomes final) ; for each bucket: a comm stream waits
+  on its events and launches an async all-reduce(SUM) of it (they run while the graph's later
+  segments do) -> all-gather of (token id, dH row) pairs -> deterministic embedding scatter ->
   wait for the buckets -> graph(clip + AdamW), grads scaled by 1/world.
 
 Buckets: the flat gradient arena is laid out in backward-completion order
@@ -317,28 +318,24 @@ class DataParallelStep:
 
     # ------------------------------------------------------------------ schedule
     def _plan_schedule(self):
-        """Place every backward segment as the single-GPU step graph places its calls
-        (engine.run_backward_streams): the input-gradient chain on the step's stream, the
-        side-tagged weight-gradient GEMMs (engine.dw_stream) on `wside` behind the chain, the
-        ConvTranspose2d scaler dW segment on `side` beside the T5 backward, and the squared-norm
-        partials of [0, a) on `side` as soon as the bucket holding `a` is reduced.  Each segment
-        is split into a chain part and a side part, replayed as two graphs: the next segment's
-        chain does not wait for this segment's weight gradients, and the bucket's collective is
-        issued on the stream that finishes the bucket (wside when the segment has side calls), so
-        it starts only once every gradient of the bucket is final."""
+        """The backward runs as ONE graph placed exactly as the single-GPU step graph places it
+        (engine.run_backward_streams: the input-gradient chain on the step's stream, the
+        side-tagged weight-gradient GEMMs on `wside`, the ConvTranspose2d scaler dW segment on
+        `side` beside the T5 backward), with an external event recorded, on every stream that
+        contributes to it, where each gradient bucket becomes final.  The host then issues each
+        bucket's collective from a comm stream that waits on that bucket's events, so the
+        collectives run while the graph's later segments do -- the same overlap as one launch per
+        segment, without giving up the graph's own multi-queue concurrency (round 4 measured the
+        per-segment launches 14 % slower than the engine step at world 1: the side-stream graph
+        launches shared a hardware queue with the chain).  The squared-norm partials of [0, a)
+        run on their own stream as soon as the buckets up to `a` are reduced."""
         e = self.eng
-        self.parts = []                                     # per segment: (home, chain calls, side calls)
         q0, q1 = e._bsplit                                  # DP call index == engine bwd_calls index
-        prev = 0
-        for k, seg in enumerate(self.segments):
+        self.homes, prev = [], 0
+        for seg in self.segments:
             lo, hi = prev, prev + len(seg)
             prev = hi
-            home = "side" if (lo, hi) == (q0, q1) else "main"
-            if e.dw_stream:
-                chain, side = [c for c in seg if not c.side], [c for c in seg if c.side]
-            else:
-                chain, side = list(seg), []
-            self.parts.append((home, chain, side))
+            self.homes.append("side" if (lo, hi) == (q0, q1) else "main")
         # the grad-norm partials of [0, a) (opt_calls[0]) need the buckets up to `a` reduced
         self.sq_after = None
         if not self.shard and e._sq_split is not None:
@@ -348,6 +345,36 @@ class DataParallelStep:
                     self.sq_after = k
                     break
         self.opt_part = e.opt_calls[1:] if self.sq_after is not None else e.opt_calls
+        self._comm = torch.cuda.Stream(e.dev)               # issues the collectives behind the bucket events
+        self._sqs = torch.cuda.Stream(e.dev)                # the early grad-norm partials
+        self.bucket_events = None
+
+    def _backward_marked(self, external):
+        """The backward without the embedding scatter, placed as engine.run_backward_streams
+        places it, recording after each segment one event per contributing stream; returns
+        [[events of bucket k]] (bucket k's first event is its chain's)."""
+        e = self.eng
+        main = torch.cuda.current_stream(e.dev)
+        side, wside = e._side, e._wside
+        for st in (side, wside):                            # both join the capture here
+            _after(st, main)
+        marks = []
+        for seg, home in zip(self.segments, self.homes):
+            if home == "side":                              # scaler dW beside the T5 backward
+                _after(side, main)
+                with torch.cuda.stream(side):
+                    self._run(seg)
+                evs = [torch.cuda.Event(external=external)]
+                evs[0].record(side)
+            else:
+                e._run_tagged(seg, main, wside)
+                evs = [torch.cuda.Event(external=external), torch.cuda.Event(external=external)]
+                evs[0].record(main)
+                evs[1].record(wside)
+            marks.append(evs)
+        for st in (side, wside):                            # joined again before the graph ends
+            _after(main, st)
+        return marks
 
     def capture(self):
         e = self.eng
@@ -372,19 +399,17 @@ class DataParallelStep:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
                 self._run(calls)
-            gs.setdefault(name, []).append(g)
+            gs[name] = g
         g = torch.cuda.CUDAGraph()                          # forward: ResNet || T5 encoder on two streams
         with torch.cuda.graph(g, stream=s):
             e.run_forward_streams()
-        gs["fwd"] = [g]
+        gs["fwd"] = g
         if e.pipeline:                                      # the next batch's ResNet, replayed beside the step
             cap("res", e.res_calls)
-        for _, chain, side in self.parts:
-            cap("chain", chain)
-            if side:
-                cap("side", side)
-            else:
-                gs.setdefault("side", []).append(None)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self.bucket_events = self._backward_marked(external=True)
+        gs["bwd"] = g
         cap("tail", self.tail + [self.emb_call])
         if self.sq_after is not None:
             cap("sq0", e.opt_calls[:1])
@@ -402,7 +427,7 @@ class DataParallelStep:
         _after(e._rstream, main)
         with torch.cuda.stream(e._rstream):
             if self.graphs is not None:
-                self.graphs["res"][0].replay()
+                self.graphs["res"].replay()
             else:
                 self._run(e.res_calls)
 
@@ -415,60 +440,52 @@ class DataParallelStep:
         e = self.eng
         g = self.graphs
         main = torch.cuda.current_stream(e.dev)
-        streams = {"main": main, "side": e._side}
-        wside = e._wside
 
-        def play(name, k, calls):
+        def play(name, calls):
             if g is not None:
-                g[name][k].replay()
+                g[name].replay()
             else:
                 self._run(calls)
         self._res_begin()
         if g is not None:
-            g["fwd"][0].replay()
+            g["fwd"].replay()
+            g["bwd"].replay()
+            marks = self.bucket_events
         else:
             e.forward()
+            marks = self._backward_marked(external=False)
         exchange = (lambda i, bk: self._sharded_collectives_after(i)) if self.shard else \
             (lambda i, bk: allreduce_buckets(e.G32, [bk], self.group))
+        comm, sqs = self._comm, self._sqs
         works, rows = [], None
-        nseg = len(self.parts)
-        for k, ((home, chain, side), bk) in enumerate(zip(self.parts, self.buckets)):
-            hs = streams[home]
-            if hs is not main:
-                _after(hs, main)                            # the scaler segment forks off the chain here
-            with torch.cuda.stream(hs):
-                play("chain", k, chain)
-            if k == nseg - 1:
-                # the embedding rows (dH32) are final with the last chain segment: gather them
-                # before the last bucket's collective, whose weight gradients still run
-                rows = gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
-            last = hs
-            if side:
-                _after(wside, hs)
-                with torch.cuda.stream(wside):
-                    play("side", k, side)
-                last = wside
-            with torch.cuda.stream(last):
+        nseg = len(self.segments)
+        for k, (bk, evs) in enumerate(zip(self.buckets, marks)):
+            comm.wait_event(evs[0])
+            with torch.cuda.stream(comm):
+                if k == nseg - 1:
+                    # the embedding rows (dH32) are final with the last chain segment: gathered
+                    # before the last bucket's collective, whose weight gradients may still run
+                    rows = gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
+                for ev in evs[1:]:
+                    comm.wait_event(ev)
                 works += exchange(k, bk)
             if k == self.sq_after:                          # grad-norm partials of [0, a), beside the rest
-                sd = streams["side"]
-                for st in (main, wside):
-                    _after(sd, st)
-                with torch.cuda.stream(sd):
+                _after(sqs, comm)
+                with torch.cuda.stream(sqs):
                     for w in works:
                         w.wait()
-                    play("sq0", 0, e.opt_calls[:1])
+                    play("sq0", e.opt_calls[:1])
         evs = []
         self._wait(rows, evs)                               # the embedding rows: needed by the tail
-        play("tail", 0, self.tail + [self.emb_call])
+        play("tail", self.tail + [self.emb_call])
         for w in works:
             self._wait([w], evs)
-        for st in (streams["side"], wside):                 # every segment's work (gloo: staged copies)
+        for st in (comm, sqs):                              # gloo: the staged copies ran on comm
             _after(main, st)
         if self.shard:
             self._sharded_optimizer()
         else:
-            play("opt", 0, self.opt_part)
+            play("opt", self.opt_part)
         self._res_end()
         if self.timing:
             self._ev.append(evs)

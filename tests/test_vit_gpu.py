@@ -211,18 +211,44 @@ def test_vit_engine_matches_reference_golden(cuda, pkg, parity_report):
           "group_grad_norm_rel": {k: abs(g0[k] - og[k]) / og[k] for k in GROUPS},
           "gradient_rel_l2": float(np.linalg.norm(ge - go) / np.linalg.norm(go))}
     del eng0
+    # the same A/B over the whole 3-step trajectory: the ViT is frozen and the batch fixed, so its
+    # pooled output is the same every step -- the oracle trained on the engine's pooled output
+    # separates the trained part's error from the frozen ViT's bf16 forward (op for op equal to
+    # bf16-operand arithmetic: tools/vit_layer_diag.py, profiles/r04_vit_layer_diag.json)
+    ot2 = orc.VitOracleTrainer(vm.make_state_dict(seed=0), warmup=int(fix["warmup"]), total=int(fix["total"]))
+    pe = torch.as_tensor(pool)
+    g2, n2, l2 = [], [], []
+    for _ in range(len(fix["losses"])):
+        _, lo = ot2.forward_backward(tb, pooled=pe)
+        gg = ot2.group_grad_norms()
+        g2.append([gg[k] for k in GROUPS])
+        n2.append(float(ot2.clip_and_step()))
+        l2.append(float(lo))
+    grel2 = np.abs(np.array(gnorms) - np.array(g2)) / np.array(g2)
+    nrel2 = np.abs(np.array(norms) - np.array(n2)) / np.array(n2)
+    lrel2 = np.abs(np.array(losses) - np.array(l2)) / np.abs(np.array(l2))
     parity_report["vit_golden_b4_l16"] = {
         "with_engine_vit_pooled": ab,
+        "trajectory_with_engine_vit_pooled": {"group_grad_norm_rel_per_step": [dict(zip(GROUPS, r)) for r in grel2.tolist()],
+                                              "grad_norm_rel": nrel2.tolist(), "loss_rel": lrel2.tolist()},
         "vit_pooled_rel": pool_err, "log_prob_max_abs": lp_err, "loss_rel": lrel.tolist(),
         "grad_norm_rel": nrel.tolist(), "group_grad_norm_rel_per_step": [dict(zip(GROUPS, r)) for r in grel.tolist()],
         "post_slice_err_over_update": serr}
     # the frozen ViT in bf16 (pooled max-abs 1.2e-2 of its max, measured) moves the fused token
     # and with it every downstream gradient: step 0 grad norms 4-6e-3 (measured); with the
     # engine's own pooled output the oracle agrees to the ResNet path's level (A/B above)
+    # measured (r03 / r04): pooled 1.24e-2, log-probs 1.07e-2, step-0 loss 1.2e-4 / grad norm 4.3e-3,
+    # step-0/1 groups <= 5.6e-3; step 2 (after the first nonzero-lr update, lr up to 5e-3 on T5):
+    # lang_model 0.114, classifier 0.025, fusing 0.017, grad norm 3.2e-2, loss 4.9e-3
     assert pool_err <= 2e-2, pool_err
     assert lp_err <= 2e-2, lp_err
-    assert lrel[0] <= 1e-3 and nrel[0] <= 1e-2, (lrel, nrel)
-    assert (grel[0] <= 1e-2).all(), dict(zip(GROUPS, grel[0]))
+    assert lrel[0] <= 3e-4 and nrel[0] <= 1e-2, (lrel, nrel)
+    for s_, lim in ((0, 1e-2), (1, 1e-2), (2, 0.2)):
+        assert (grel[s_] <= lim).all(), (s_, dict(zip(GROUPS, grel[s_])))
+    # ... and all of it is the frozen ViT's bf16 pooled output: trained on the engine's pooled
+    # output the oracle follows the engine over the whole trajectory to the ResNet path's level
+    assert (grel2[:2] <= 1e-2).all() and (grel2[2] <= 0.2).all(), grel2
+    assert (nrel2 <= 1e-2).all() and (lrel2 <= 1e-3).all(), (nrel2, lrel2)
     assert ab["log_prob_max_abs"] <= 2e-2 and ab["loss_rel"] <= 1e-3, ab
     # at B = 4 the T5 gradient enters through 4 answer rows and 4 CLS rows only, so the bf16
     # rounding does not average out (group norms 5e-3 at B = 4, 1.5e-3 at B = 32, measured
@@ -233,7 +259,7 @@ def test_vit_engine_matches_reference_golden(cuda, pkg, parity_report):
     # after two AdamW updates (lr up to 5e-3 on T5): m / sqrt(v) turns near-zero gradients'
     # rounding into O(lr) update differences
     assert (lrel <= 1e-2).all() and (nrel <= 5e-2).all(), (lrel, nrel)
-    assert max(serr.values()) <= 0.5, serr
+    assert max(serr.values()) <= 0.5, serr          # measured <= 0.35 (post_dec_xv0)
 
 
 def test_vit_engine_vs_oracle_train_mode(cuda, pkg, parity_report):

@@ -1,0 +1,31 @@
+"""Parity of BASELINE configs[4]'s benched step on the GPU.
+
+test_c5_bench_step_b64_matches_fp8_oracle: the engine built exactly as `bench.py --config5`
+builds it (R50 at 384 x 384, T5-large, 6 SGA blocks at width 1024, e4m3 forward weight GEMMs,
+B = 64, L = 32, pipelined frozen ResNet, tuned tile / split-K table, captured hipGraph step,
+deferred AdamW, dropout 0.1 from the shared counter hash) against the CPU oracle's fp8
+restatement (oracle/vqa_oracle.py fp8_rows / _Fp8Matmul) fed the same batches and masks, two
+steps: log-probs, loss, total and per-group grad norms, then the per-group parameter updates
+(trainer/faster_rcnn_vqa_trainer.py:391-406).  Tolerances: tests/bench_step_worker.py C5_*."""
+import os
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+# relative L2 of the per-group update vectors after two steps (AdamW's m / sqrt(v) turns the
+# rounding of near-zero gradients into O(lr) update differences; config 2 measured <= 5.5e-2)
+DELTA_RTOL = 0.2
+
+
+def test_c5_bench_step_b64_matches_fp8_oracle(parity_report):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    sys.path.insert(0, HERE)
+    import bench_step_worker
+    rep, fails = bench_step_worker.run("c5")
+    parity_report["config5_bench_b64"] = rep
+    assert not fails, (fails, rep)
+    assert max(rep["update_rel_l2"].values()) <= DELTA_RTOL, rep["update_rel_l2"]

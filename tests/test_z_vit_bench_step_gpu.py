@@ -37,36 +37,52 @@ def test_vit_bench_step_b64_matches_oracle(pkg, parity_report):
     eng.autotune(table=TABLE)
     eng.capture()
     ot = orc.VitOracleTrainer(sd, warmup=10, total=100000, dropout=0.1, seed=0)
+    # the A/B (tools/drift_ab_vit.py, tools/vit_layer_diag.py): the same oracle trained on the
+    # engine's own bf16 ViT pooled output of each batch -- what is left is the trained part's error
+    ot2 = orc.VitOracleTrainer(sd, warmup=10, total=100000, dropout=0.1, seed=0)
     p0 = {k: v.detach().clone() for k, v in ot.sd.items() if not k.startswith("vision_model.")}
-    rep = {}
+    rep, rep2 = {}, {}
+
+    def cmp(lp, loss, gn, ggn, olp, oloss, ogn, ogg):
+        return {"log_prob_max_abs": float(np.abs(lp - olp.numpy()).max()),
+                "loss_rel": abs(loss - float(oloss)) / abs(float(oloss)), "grad_norm_rel": abs(gn - ogn) / ogn,
+                "group_grad_norm_rel": {g: abs(ggn[g] - ogg[g]) / ogg[g] for g in GROUPS}}
     for i, nb in enumerate(nbs):
-        ot.rng_counter = int(eng.RNG[1].item())             # the same dropout draw (engine bumps, then uses)
+        ot.rng_counter = ot2.rng_counter = int(eng.RNG[1].item())   # the same dropout draw (engine bumps, then uses)
         eng.load_batch(dev(nb))
         eng.train_step()
         torch.cuda.synchronize()
         lp, loss, gn = eng.LOGP.cpu().numpy(), float(eng.LOSS.item()), eng.last_grad_norm()
         ggn = eng.group_grad_norms()
+        pooled = eng.vit_pooled().cpu()
         tb = {k: (None if v is None else torch.as_tensor(v)) for k, v in nb.items()}
         olp, oloss = ot.forward_backward(tb)
         ogg = ot.group_grad_norms()
         ogn = float(ot.clip_and_step())
-        rep[f"step{i}"] = {"log_prob_max_abs": float(np.abs(lp - olp.numpy()).max()),
-                           "loss_rel": abs(loss - float(oloss)) / abs(float(oloss)),
-                           "grad_norm_rel": abs(gn - ogn) / ogn,
-                           "group_grad_norm_rel": {g: abs(ggn[g] - ogg[g]) / ogg[g] for g in GROUPS}}
+        rep[f"step{i}"] = cmp(lp, loss, gn, ggn, olp, oloss, ogn, ogg)
+        olp, oloss = ot2.forward_backward(tb, pooled=pooled)
+        ogg = ot2.group_grad_norms()
+        ogn = float(ot2.clip_and_step())
+        rep2[f"step{i}"] = cmp(lp, loss, gn, ggn, olp, oloss, ogn, ogg)
     post = eng.state_dict()
-    delta = {}
-    for g in GROUPS:
-        num = den = 0.0
-        for k, v0 in p0.items():
-            if orc.group_of(k) != g or k not in post:
-                continue
-            do = (ot.sd[k].detach() - v0).double().numpy()
-            de = post[k].astype(np.float64) - v0.double().numpy()
-            num += float(((de - do) ** 2).sum())
-            den += float((do ** 2).sum())
-        delta[g] = (num / den) ** 0.5 if den > 0 else 0.0
+
+    def upd(o):
+        delta = {}
+        for g in GROUPS:
+            num = den = 0.0
+            for k, v0 in p0.items():
+                if orc.group_of(k) != g or k not in post:
+                    continue
+                do = (o.sd[k].detach() - v0).double().numpy()
+                de = post[k].astype(np.float64) - v0.double().numpy()
+                num += float(((de - do) ** 2).sum())
+                den += float((do ** 2).sum())
+            delta[g] = (num / den) ** 0.5 if den > 0 else 0.0
+        return delta
+    delta = upd(ot)
     rep["update_rel_l2"] = delta
+    rep2["update_rel_l2"] = upd(ot2)
+    rep["with_engine_vit_pooled"] = rep2
     parity_report["vit_bench_b64"] = rep
     for i in range(3):
         r = rep[f"step{i}"]
@@ -74,11 +90,16 @@ def test_vit_bench_step_b64_matches_oracle(pkg, parity_report):
         # max); at B = 64 the gradient sums 64 answer / CLS rows, so the rounding averages out:
         # measured log-probs 1.9e-2 / 1.6e-2 / 0.10 (the max over 64 x 170 after two AdamW
         # updates, whose first steps move every weight by ~lr * sign(g)), loss <= 2.6e-4, grad
-        # norm <= 1.2e-3, groups <= 6.6e-3
-        assert r["log_prob_max_abs"] <= (3e-2 if i == 0 else 0.15), rep
-        assert r["loss_rel"] <= 1e-3 * (1 + i), rep
-        assert r["grad_norm_rel"] <= 5e-3 * (1 + i), rep
-        assert max(r["group_grad_norm_rel"].values()) <= 1e-2 * (1 + i), rep
+        # norm <= 1.2e-3, groups <= 7.8e-3 (fusing layer, step 2)
+        assert r["log_prob_max_abs"] <= (3e-2 if i < 2 else 0.13), rep
+        assert r["loss_rel"] <= 5e-4, rep
+        assert r["grad_norm_rel"] <= 2.5e-3, rep
+        assert max(r["group_grad_norm_rel"].values()) <= (3e-3 if i < 2 else 1.2e-2), rep
     # relative L2 of the per-group update vectors after three steps: measured 0.04 (classifier),
     # 0.16 (T5), 0.19 (fusing layer, whose Dropout(0.5) input is the bf16 ViT token)
-    assert max(delta.values()) <= 0.3, delta
+    assert max(delta.values()) <= 0.25, delta
+    # with the engine's pooled outputs the oracle follows the engine much more closely: the bulk of
+    # the trajectory error above is the frozen ViT's bf16 forward (each of its ops equals bf16-operand
+    # arithmetic on the engine's inputs: tools/vit_layer_diag.py)
+    r2 = rep2["step2"]
+    assert r2["log_prob_max_abs"] <= r["log_prob_max_abs"] and max(rep2["update_rel_l2"].values()) <= 0.25, rep2

@@ -91,5 +91,66 @@ torch.cuda.synchronize()
 pe = eng.vit_pooled().cpu()
 out["pooled"] = {"engine_vs_fp32": rel(pe, p32), "engine_vs_bf16ops": rel(pe, p16), "bf16ops_vs_fp32": rel(p16, p32)}
 print(json.dumps(out["pooled"]), flush=True)
+# ---- layer 0 op by op: each engine op against fp32 / bf16-operand math on the ENGINE's own
+# inputs (so every op's own error is isolated); relative L2 over the whole tensor
+def rl2(a, b):
+    return float((a - b).norm() / b.norm())
+
+
+def upto(n):
+    for c in eng.fwd_calls[:n]:
+        c(s)
+    torch.cuda.synchronize()
+
+
+g = lambda k: sd["vision_model." + k].float()
+p0 = "encoder.layer.0."
+a0 = eng._vit_attn_at[0]                 # index of the o-projection; the attention is a0 - 1
+steps = {}
+upto(a0 - 3)                              # patch embedding + CLS / position rows -> VH32
+x = eng.VH32.view(B, -1, 768).cpu().clone()
+upto(a0 - 2)                              # ln1 -> VLN16
+n16 = eng.VLN16.float().view(B, -1, 768).cpu()
+ref = F.layer_norm(x, (768,), g(p0 + "layernorm_before.weight"), g(p0 + "layernorm_before.bias"), 1e-12)
+steps["ln1"] = {"vs_fp32": rl2(n16, ref), "vs_fp32_rounded": rl2(n16, ref.bfloat16().float())}
+upto(a0 - 1)                              # qkv GEMM -> VQKV16
+qkv16 = eng.VQKV16.float().view(B, -1, 2304).cpu()
+W = torch.cat([g(p0 + f"attention.attention.{t}.weight") for t in ("query", "key", "value")])
+bq = torch.cat([g(p0 + f"attention.attention.{t}.bias") for t in ("query", "key", "value")])
+ref = n16 @ W.T + bq
+ref16 = n16 @ W.bfloat16().float().T + bq
+steps["qkv"] = {"vs_fp32": rl2(qkv16, ref), "vs_bf16ops": rl2(qkv16, ref16),
+                "vs_bf16ops_rounded": rl2(qkv16, ref16.bfloat16().float())}
+upto(a0)                                  # attention -> VO16
+o16 = eng.VO16.float().view(B, -1, 768).cpu()
+q, k, v = (qkv16[..., j * 768:(j + 1) * 768].reshape(B, -1, 12, 64).transpose(1, 2) for j in range(3))
+P = torch.softmax(q @ k.transpose(2, 3) / 8.0, -1)
+ref = (P @ v).transpose(1, 2).reshape(B, -1, 768)
+ref16 = (P.bfloat16().float() @ v).transpose(1, 2).reshape(B, -1, 768)
+steps["attention"] = {"vs_fp32": rl2(o16, ref), "vs_bf16P": rl2(o16, ref16),
+                      "fp32_rounded_vs_fp32": rl2(ref.bfloat16().float(), ref)}
+upto(a0 + 1)                              # o-proj + bias + residual -> VH32
+h = eng.VH32.view(B, -1, 768).cpu().clone()
+ref = o16 @ g(p0 + "attention.output.dense.weight").T + g(p0 + "attention.output.dense.bias") + x
+ref16 = o16 @ g(p0 + "attention.output.dense.weight").bfloat16().float().T + g(p0 + "attention.output.dense.bias") + x
+steps["o_proj"] = {"vs_fp32": rl2(h - x, ref - x), "vs_bf16ops": rl2(h - x, ref16 - x)}
+upto(a0 + 2)                              # ln2 -> VLN16
+n16 = eng.VLN16.float().view(B, -1, 768).cpu()
+ref = F.layer_norm(h, (768,), g(p0 + "layernorm_after.weight"), g(p0 + "layernorm_after.bias"), 1e-12)
+steps["ln2"] = {"vs_fp32": rl2(n16, ref), "vs_fp32_rounded": rl2(n16, ref.bfloat16().float())}
+upto(a0 + 3)                              # fc1 + GELU -> VFF16
+f16 = eng.VFF16.float().view(B, -1, 3072).cpu()
+ref = F.gelu(n16 @ g(p0 + "intermediate.dense.weight").T + g(p0 + "intermediate.dense.bias"))
+ref16 = F.gelu(n16 @ g(p0 + "intermediate.dense.weight").bfloat16().float().T + g(p0 + "intermediate.dense.bias"))
+steps["fc1_gelu"] = {"vs_fp32": rl2(f16, ref), "vs_bf16ops": rl2(f16, ref16),
+                     "vs_bf16ops_rounded": rl2(f16, ref16.bfloat16().float())}
+upto(a0 + 4)                              # fc2 + bias + residual -> VH32
+h2 = eng.VH32.view(B, -1, 768).cpu().clone()
+ref = f16 @ g(p0 + "output.dense.weight").T + g(p0 + "output.dense.bias") + h
+ref16 = f16 @ g(p0 + "output.dense.weight").bfloat16().float().T + g(p0 + "output.dense.bias") + h
+steps["fc2"] = {"vs_fp32": rl2(h2 - h, ref - h), "vs_bf16ops": rl2(h2 - h, ref16 - h)}
+out["layer0_ops_rel_l2"] = steps
+for k_, v_ in steps.items():
+    print(k_, json.dumps(v_), flush=True)
 if len(sys.argv) > 1:
     json.dump(out, open(sys.argv[1], "w"), indent=1)
