@@ -356,15 +356,7 @@ __device__ __forceinline__ float epi_act(float v, int a) {
 // dirty line back before the next dependent launch may start (MI355X_MICROARCH.md, `boundary`:
 // + bytes / 6 TB/s per boundary); a write-through store sends it on as it is issued, overlapped
 // with the rest of the tile loop (the consumer re-reads it past its own launch's L2 invalidate
-// either way).  VQA_EPI_PLAIN_STORES builds the plain-store form (A/B only).
-#ifndef VQA_EPI_PLAIN_STORES
-#define VQA_EPI_WT 1
-#else
-#define VQA_EPI_WT 0
-#endif
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFF0, 0x00020000);
-}
+// either way).  VQA_EPI_PLAIN_STORES builds the plain-store form (A/B only; common.h).
 __device__ __forceinline__ void store16_wt(__amdgpu_buffer_rsrc_t r, long byte_off, void* p, const uint4& v) {
   if (VQA_EPI_WT) {
     const i32x4_t x = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
