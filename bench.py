@@ -248,6 +248,8 @@ def main():
     ap.add_argument("--dp", action="store_true",
                     help="N = 1: run the N > 1 step (dp.DataParallelStep over a world-1 RCCL group, the DP engine's "
                          "weight-gradient groups) instead of the single-GPU engine graph")
+    ap.add_argument("--dp-groups", action="store_true",
+                    help="the single-GPU engine step with the DP engine's T5 weight-gradient groups (A/B of --dp)")
     ap.add_argument("--rehearse", action="store_true",
                     help="run every rank on cuda:0 over gloo: exercises the N-rank code path (bucketing, "
                          "gathers, capture, lockstep) on a one-GPU box; the timing is not a measurement")
@@ -307,7 +309,7 @@ def main():
     dp_groups = pkg.dp.dp_t5_dw_groups(pkg.synthetic.lm_dims(lm).t5_layers)
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev, num_blocks=NB,
                                warmup=10, total=100000, dropout=0.1, seed=rank, pipeline=pipe,
-                               t5_dw_group=None if not use_dp else dp_groups, language_model=lm,
+                               t5_dw_group=dp_groups if (use_dp or args.dp_groups) else None, language_model=lm,
                                fp8=args.config5)
     del sd
     pool = []
@@ -435,8 +437,9 @@ def main():
         "roofline": roofline,
         "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
     }
-    if use_dp:
-        out["dp"] = dps.timing_report()
+    if use_dp:                             # graphed: measured on eager steps after the timed region
+        out["dp"] = (dps.measure_exposed(lambda: step(0), 3) if dps.graphs is not None and dps.in_graph
+                     else dps.timing_report())
         out["dp"]["backend"] = dist.get_backend()
     if args.rehearse:                               # the N-rank path's results: lockstep across ranks
         eng.flush_optimizer()

@@ -21,27 +21,6 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
-// Write-through (sc1) stores for kernel outputs a later launch reads (gemm_common.h
-// tile_epilogue, norms.hip): nothing is left dirty in L2 for the end-of-launch release to write
-// back before the next dependent launch starts.  VQA_EPI_PLAIN_STORES: plain stores (A/B only).
-#ifndef VQA_EPI_PLAIN_STORES
-#define VQA_EPI_WT 1
-#else
-#define VQA_EPI_WT 0
-#endif
-typedef int vqa_i32x4_t __attribute__((ext_vector_type(4)));
-typedef int vqa_i32x2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFF0, 0x00020000);
-}
-// a wave-uniform row pointer (readfirstlane: the buffer base must live in scalar registers)
-template <typename T>
-__device__ __forceinline__ T* uniform_ptr(T* p) {
-  const unsigned long long u = (unsigned long long)p;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
-  return (T*)(((unsigned long long)hi << 32) | lo);
-}
-
 // 64-lane reductions (wave = 64 on CDNA; never 32)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

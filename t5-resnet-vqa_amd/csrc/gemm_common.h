@@ -351,21 +351,6 @@ __device__ __forceinline__ float epi_act(float v, int a) {
   return copysignf((1.f - e) / (1.f + e), v);
 }
 
-// Output stores of the vectorised epilogue: write-through (sc1) 16-B buffer stores.  A plain
-// store leaves the line dirty in this XCD's L2 and the kernel's end-of-launch release writes every
-// dirty line back before the next dependent launch may start (MI355X_MICROARCH.md, `boundary`:
-// + bytes / 6 TB/s per boundary); a write-through store sends it on as it is issued, overlapped
-// with the rest of the tile loop (the consumer re-reads it past its own launch's L2 invalidate
-// either way).  VQA_EPI_PLAIN_STORES builds the plain-store form (A/B only; common.h).
-__device__ __forceinline__ void store16_wt(__amdgpu_buffer_rsrc_t r, long byte_off, void* p, const uint4& v) {
-  if (VQA_EPI_WT) {
-    const i32x4_t x = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)byte_off, 0, 16);      // aux 16: sc1
-  } else {
-    *reinterpret_cast<uint4*>(p) = v;
-  }
-}
-
 template <int BM, int BN, int STAGES, int NWM, int NWN, bool EXT = false, int BKT = BK>
 __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&acc)[BM / NWM / 32][BN / NWN / 32],
                                               const int z, const int m0, const int n0, const int mlim, char* smem) {
@@ -405,7 +390,6 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
     constexpr int GPW = TM / G;                         // passes per wave row
     static_assert(TM % G == 0 && HALF * LDR * 4 <= RING, "epilogue image must fit the ring");
     float* img = reinterpret_cast<float*>(smem);
-    const __amdgpu_buffer_rsrc_t r32 = out_rsrc(C32), r16 = out_rsrc(C16);
     constexpr int TPR = BN / 8;                         // threads per row
     constexpr int RPP = NT / TPR;                       // rows per sweep
     // __syncthreads (waits for this wave's LDS ops, then barriers); no LDS-DMA is in flight now
@@ -479,16 +463,15 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
           for (int t = 0; t < 8; ++t) v[t] = EXT ? epi_act(v[t], P.relu) : fmaxf(v[t], 0.f);
         }
         if (C32) {
-          const long eo = (long)row * P.ldc32 + col;
-          float4* cp = reinterpret_cast<float4*>(C32 + eo);
+          float4* cp = reinterpret_cast<float4*>(C32 + (long)row * P.ldc32 + col);
           float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
           if (beta) {
             const float4 c0 = cp[0], c1 = cp[1];
             o0.x += P.beta * c0.x; o0.y += P.beta * c0.y; o0.z += P.beta * c0.z; o0.w += P.beta * c0.w;
             o1.x += P.beta * c1.x; o1.y += P.beta * c1.y; o1.z += P.beta * c1.z; o1.w += P.beta * c1.w;
           }
-          store16_wt(r32, eo * 4, cp, __builtin_bit_cast(uint4, o0));
-          store16_wt(r32, eo * 4 + 16, cp + 1, __builtin_bit_cast(uint4, o1));
+          cp[0] = o0;
+          cp[1] = o1;
         }
         if (C16) {
           uint4 u;
@@ -496,8 +479,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
           u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
           u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
           u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-          const long eo = (long)row * P.ldc16 + col;
-          store16_wt(r16, eo * 2, C16 + eo, u);
+          *reinterpret_cast<uint4*>(C16 + (long)row * P.ldc16 + col) = u;
         }
       }
       if (pass + 1 < NWM * GPW) __syncthreads();        // image reused by the next pass

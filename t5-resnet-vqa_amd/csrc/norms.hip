@@ -24,16 +24,6 @@ __device__ __forceinline__ void load_row(const float* __restrict__ p, float (&x)
 template <int NV>
 __device__ __forceinline__ void store_row32(float* __restrict__ p, const float (&x)[NV][4]) {
   const int l = threadIdx.x & 63;
-  if (VQA_EPI_WT) {                                   // write-through (common.h): p is one wave's row
-    const __amdgpu_buffer_rsrc_t r = out_rsrc(uniform_ptr(p));
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const vqa_i32x4_t v = {__float_as_int(x[i][0]), __float_as_int(x[i][1]), __float_as_int(x[i][2]),
-                             __float_as_int(x[i][3])};
-      __builtin_amdgcn_raw_buffer_store_b128(v, r, (i * 64 + l) * 16, 0, 16);
-    }
-    return;
-  }
 #pragma unroll
   for (int i = 0; i < NV; ++i)
     reinterpret_cast<float4*>(p)[i * 64 + l] = make_float4(x[i][0], x[i][1], x[i][2], x[i][3]);
@@ -46,12 +36,7 @@ __device__ __forceinline__ void store_row16(bf16_t* __restrict__ p, const float 
     uint2 u;
     u.x = (uint32_t)f2bf(x[i][0]) | ((uint32_t)f2bf(x[i][1]) << 16);
     u.y = (uint32_t)f2bf(x[i][2]) | ((uint32_t)f2bf(x[i][3]) << 16);
-    if (VQA_EPI_WT) {
-      const vqa_i32x2_t v = {(int)u.x, (int)u.y};
-      __builtin_amdgcn_raw_buffer_store_b64(v, out_rsrc(uniform_ptr(p)), (i * 64 + l) * 8, 0, 16);
-    } else {
-      reinterpret_cast<uint2*>(p)[i * 64 + l] = u;
-    }
+    reinterpret_cast<uint2*>(p)[i * 64 + l] = u;
   }
 }
 template <int NV>

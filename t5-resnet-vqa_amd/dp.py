@@ -5,11 +5,11 @@ trainer/faster_rcnn_vqa_trainer.py:61-62; this is the build's added strategy,
 SURVEY.md §8e.)
 
 Step on every rank (identical initial weights, rank-local batch):
-  graph(forward) -> graph(backward, placed as the single-GPU step graph places it, an external
-  event recorded where each gradient bucket becomes final) ; for each bucket: a comm stream waits
-  on its events and launches an async all-reduce(SUM) of it (they run while the graph's later
-  segments do) -> all-gather of (token id, dH row) pairs -> deterministic embedding scatter ->
-  wait for the buckets -> graph(clip + AdamW), grads scaled by 1/world.
+  graph(forward) -> graph(backward placed as the single-GPU step graph places it; per bucket, a
+  comm stream waits on the events where the bucket becomes final and all-reduces it (SUM), while
+  the later segments run; all-gather of (token id, dH row) pairs; deterministic embedding
+  scatter; wait for the buckets; clip + AdamW with grads scaled by 1/world) -- with RCCL the
+  collectives are captured into the backward graph itself.
 
 Buckets: the flat gradient arena is laid out in backward-completion order
 (layout.py), so each finished bucket is a contiguous slice [a, b) of G32 and
@@ -20,6 +20,8 @@ Because every exchange and kernel is deterministic, all ranks hold bit-identical
 parameters after every step.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -318,17 +320,21 @@ class DataParallelStep:
 
     # ------------------------------------------------------------------ schedule
     def _plan_schedule(self):
-        """The backward runs as ONE graph placed exactly as the single-GPU step graph places it
+        """The backward is placed exactly as the single-GPU step graph places it
         (engine.run_backward_streams: the input-gradient chain on the step's stream, the
         side-tagged weight-gradient GEMMs on `wside`, the ConvTranspose2d scaler dW segment on
-        `side` beside the T5 backward), with an external event recorded, on every stream that
-        contributes to it, where each gradient bucket becomes final.  The host then issues each
-        bucket's collective from a comm stream that waits on that bucket's events, so the
-        collectives run while the graph's later segments do -- the same overlap as one launch per
-        segment, without giving up the graph's own multi-queue concurrency (round 4 measured the
-        per-segment launches 14 % slower than the engine step at world 1: the side-stream graph
-        launches shared a hardware queue with the chain).  The squared-norm partials of [0, a)
-        run on their own stream as soon as the buckets up to `a` are reduced."""
+        `side` beside the T5 backward), with an event recorded, on every stream that contributes
+        to it, where each gradient bucket becomes final.  A comm stream waits on a bucket's events
+        and issues its collective, so the collectives run while the later segments do.  With RCCL
+        the collectives, the row gather, the tail and the optimizer are captured into the SAME
+        graph as the backward (one replay per step; the graph executor keeps its own multi-queue
+        placement -- round 4 measured one graph per segment 14 % slower than the engine step at
+        world 1, the side-stream launches sharing a hardware queue with the chain, and ROCm's
+        torch refuses the external event records a host-issued exchange behind one graph would
+        need).  gloo (host-staged, tests only) replays the backward graph and then exchanges.
+        The squared-norm partials of [0, a) run on their own stream as soon as the buckets up to
+        `a` are reduced."""
+        import torch.distributed as dist
         e = self.eng
         q0, q1 = e._bsplit                                  # DP call index == engine bwd_calls index
         self.homes, prev = [], 0
@@ -347,9 +353,11 @@ class DataParallelStep:
         self.opt_part = e.opt_calls[1:] if self.sq_after is not None else e.opt_calls
         self._comm = torch.cuda.Stream(e.dev)               # issues the collectives behind the bucket events
         self._sqs = torch.cuda.Stream(e.dev)                # the early grad-norm partials
-        self.bucket_events = None
+        # VQA_DP_HOST_EXCHANGE=1: the RCCL exchange issued from the host after the backward graph
+        # (no overlap; an A/B of the graph executor's queue placement only)
+        self.in_graph = dist.get_backend(self.group) != "gloo" and os.environ.get("VQA_DP_HOST_EXCHANGE") != "1"
 
-    def _backward_marked(self, external):
+    def _backward_marked(self):
         """The backward without the embedding scatter, placed as engine.run_backward_streams
         places it, recording after each segment one event per contributing stream; returns
         [[events of bucket k]] (bucket k's first event is its chain's)."""
@@ -364,11 +372,11 @@ class DataParallelStep:
                 _after(side, main)
                 with torch.cuda.stream(side):
                     self._run(seg)
-                evs = [torch.cuda.Event(external=external)]
+                evs = [torch.cuda.Event()]
                 evs[0].record(side)
             else:
                 e._run_tagged(seg, main, wside)
-                evs = [torch.cuda.Event(external=external), torch.cuda.Event(external=external)]
+                evs = [torch.cuda.Event(), torch.cuda.Event()]
                 evs[0].record(main)
                 evs[1].record(wside)
             marks.append(evs)
@@ -376,7 +384,52 @@ class DataParallelStep:
             _after(main, st)
         return marks
 
+    def _exchange(self, marks):
+        """Per bucket: the comm stream waits on the bucket's events (None: on everything issued
+        so far) and issues its collective; the embedding rows are gathered before the last
+        bucket's collective; the [0, a) grad-norm partials run on their own stream once their
+        buckets are reduced; then the embedding scatter (tail) and, unless sharded, the optimizer
+        plan.  Runs eagerly or under capture alike.  Returns the timing events (timing mode)."""
+        e = self.eng
+        main = torch.cuda.current_stream(e.dev)
+        exchange = (lambda i, bk: self._sharded_collectives_after(i)) if self.shard else \
+            (lambda i, bk: allreduce_buckets(e.G32, [bk], self.group))
+        comm, sqs = self._comm, self._sqs
+        works, rows = [], None
+        nseg = len(self.segments)
+        for k, bk in enumerate(self.buckets):
+            evs = marks[k] if marks is not None else []
+            if evs:
+                comm.wait_event(evs[0])
+            else:
+                _after(comm, main)
+            with torch.cuda.stream(comm):
+                if k == nseg - 1:
+                    # the embedding rows (dH32) are final with the last chain segment: gathered
+                    # before the last bucket's collective, whose weight gradients may still run
+                    rows = gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
+                for ev in evs[1:]:
+                    comm.wait_event(ev)
+                works += exchange(k, bk)
+            if k == self.sq_after:                          # grad-norm partials of [0, a), beside the rest
+                _after(sqs, comm)
+                with torch.cuda.stream(sqs):
+                    for w in works:
+                        w.wait()
+                    self._run(e.opt_calls[:1])
+        tev = []
+        self._wait(rows, tev)                               # the embedding rows: needed by the tail
+        self._run(self.tail + [self.emb_call])
+        for w in works:
+            self._wait([w], tev)
+        for st in (comm, sqs):                              # gloo: the staged copies ran on comm
+            _after(main, st)
+        if not self.shard:
+            self._run(self.opt_part)
+        return tev
+
     def capture(self):
+        import torch.distributed as dist
         e = self.eng
         e.flush_optimizer()              # the warm-up's backward must not overwrite a pending update's G
         s = torch.cuda.Stream(e.dev)
@@ -385,6 +438,9 @@ class DataParallelStep:
         with torch.cuda.stream(s):                          # warm-up outside capture (no optimizer update)
             e._run(e.fwd_calls)
             e.backward()
+        if self.in_graph:                                   # communicators exist before the capture
+            with torch.cuda.stream(self._comm):
+                dist.all_reduce(torch.zeros(1, device=e.dev), group=self.group)
         torch.cuda.current_stream(e.dev).wait_stream(s)
         torch.cuda.synchronize(e.dev)
         e.RNG.copy_(saved_rng)                              # the warm-up must not consume a dropout draw
@@ -394,26 +450,21 @@ class DataParallelStep:
     def _capture_all(self, s):
         e = self.eng
         gs = {}
-
-        def cap(name, calls):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s):
-                self._run(calls)
-            gs[name] = g
         g = torch.cuda.CUDAGraph()                          # forward: ResNet || T5 encoder on two streams
         with torch.cuda.graph(g, stream=s):
             e.run_forward_streams()
         gs["fwd"] = g
         if e.pipeline:                                      # the next batch's ResNet, replayed beside the step
-            cap("res", e.res_calls)
-        g = torch.cuda.CUDAGraph()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self._run(e.res_calls)
+            gs["res"] = g
+        g = torch.cuda.CUDAGraph()                          # backward (+ collectives, tail, optimizer)
         with torch.cuda.graph(g, stream=s):
-            self.bucket_events = self._backward_marked(external=True)
+            marks = self._backward_marked()
+            if self.in_graph:
+                self._exchange(marks)
         gs["bwd"] = g
-        cap("tail", self.tail + [self.emb_call])
-        if self.sq_after is not None:
-            cap("sq0", e.opt_calls[:1])
-        cap("opt", self.opt_part)
         return gs
 
     def _res_begin(self):
@@ -439,56 +490,37 @@ class DataParallelStep:
     def step(self):
         e = self.eng
         g = self.graphs
-        main = torch.cuda.current_stream(e.dev)
-
-        def play(name, calls):
-            if g is not None:
-                g[name].replay()
-            else:
-                self._run(calls)
         self._res_begin()
-        if g is not None:
+        tev = None
+        if g is None:                                       # eager: the same schedule, issued live
+            e.forward()
+            tev = self._exchange(self._backward_marked())
+        else:
             g["fwd"].replay()
             g["bwd"].replay()
-            marks = self.bucket_events
-        else:
-            e.forward()
-            marks = self._backward_marked(external=False)
-        exchange = (lambda i, bk: self._sharded_collectives_after(i)) if self.shard else \
-            (lambda i, bk: allreduce_buckets(e.G32, [bk], self.group))
-        comm, sqs = self._comm, self._sqs
-        works, rows = [], None
-        nseg = len(self.segments)
-        for k, (bk, evs) in enumerate(zip(self.buckets, marks)):
-            comm.wait_event(evs[0])
-            with torch.cuda.stream(comm):
-                if k == nseg - 1:
-                    # the embedding rows (dH32) are final with the last chain segment: gathered
-                    # before the last bucket's collective, whose weight gradients may still run
-                    rows = gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
-                for ev in evs[1:]:
-                    comm.wait_event(ev)
-                works += exchange(k, bk)
-            if k == self.sq_after:                          # grad-norm partials of [0, a), beside the rest
-                _after(sqs, comm)
-                with torch.cuda.stream(sqs):
-                    for w in works:
-                        w.wait()
-                    play("sq0", e.opt_calls[:1])
-        evs = []
-        self._wait(rows, evs)                               # the embedding rows: needed by the tail
-        play("tail", self.tail + [self.emb_call])
-        for w in works:
-            self._wait([w], evs)
-        for st in (comm, sqs):                              # gloo: the staged copies ran on comm
-            _after(main, st)
+            if not self.in_graph:                           # gloo: exchange after the backward graph
+                tev = self._exchange(None)
         if self.shard:
             self._sharded_optimizer()
-        else:
-            play("opt", self.opt_part)
         self._res_end()
-        if self.timing:
-            self._ev.append(evs)
+        if self.timing and tev is not None:
+            self._ev.append(tev)
+
+    def measure_exposed(self, step_fn, steps=3):
+        """Per-collective exposed waits are host-visible only when the exchange is issued from
+        the host: run `steps` calls of step_fn with the graphs off (the same schedule, eager)
+        and timing on, then restore.  Returns timing_report()."""
+        saved, t = self.graphs, self.timing
+        self.graphs, self.timing, self._ev = None, True, []
+        try:
+            for _ in range(steps):
+                step_fn()
+            rep = self.timing_report()
+        finally:
+            self.graphs, self.timing = saved, t
+        if rep is not None:
+            rep["mode"] = "eager steps after the timed region (graphed steps issue their collectives in the backward graph)"
+        return rep
 
     def _wait(self, works, evs):
         if not self.timing:
