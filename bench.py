@@ -351,7 +351,7 @@ def main():
     for i in range(args.warmup):
         step(i)
     stream = torch.cuda.current_stream(dev)
-    if use_dp:                             # per-collective exposed wait (HIP events around each wait)
+    if use_dp:                             # collective completion + exposed wait (HIP events)
         dps.timing = True
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
@@ -437,9 +437,8 @@ def main():
         "roofline": roofline,
         "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
     }
-    if use_dp:                             # graphed: measured on eager steps after the timed region
-        out["dp"] = (dps.measure_exposed(lambda: step(0), 3) if dps.graphs is not None and dps.in_graph
-                     else dps.timing_report())
+    if use_dp:
+        out["dp"] = dps.timing_report()
         out["dp"]["backend"] = dist.get_backend()
     if args.rehearse:                               # the N-rank path's results: lockstep across ranks
         eng.flush_optimizer()

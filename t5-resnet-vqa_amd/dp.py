@@ -5,11 +5,11 @@ trainer/faster_rcnn_vqa_trainer.py:61-62; this is the build's added strategy,
 SURVEY.md §8e.)
 
 Step on every rank (identical initial weights, rank-local batch):
-  graph(forward) -> graph(backward placed as the single-GPU step graph places it; per bucket, a
-  comm stream waits on the events where the bucket becomes final and all-reduces it (SUM), while
-  the later segments run; all-gather of (token id, dH row) pairs; deterministic embedding
-  scatter; wait for the buckets; clip + AdamW with grads scaled by 1/world) -- with RCCL the
-  collectives are captured into the backward graph itself.
+  graph(forward) -> the backward as a few stage graphs (stage j: chain segment j beside the
+  pending weight-gradient GEMMs of the segments before it), and after each stage an async
+  all-reduce(SUM) of the buckets it finished, issued on a comm stream (they run while the next
+  stages do) -> all-gather of (token id, dH row) pairs -> deterministic embedding scatter ->
+  wait for the buckets -> graph(clip + AdamW), grads scaled by 1/world.
 
 Buckets: the flat gradient arena is laid out in backward-completion order
 (layout.py), so each finished bucket is a contiguous slice [a, b) of G32 and
@@ -20,8 +20,6 @@ Because every exchange and kernel is deterministic, all ranks hold bit-identical
 parameters after every step.
 """
 from __future__ import annotations
-
-import os
 
 import numpy as np
 import torch
@@ -55,7 +53,10 @@ def plan_buckets(ready_marks, end, min_bytes=24 << 20):
         stop = min(stop, end)
         last = i == len(ready_marks) - 1
         if stop - start >= min_bytes // 4 or (last and stop > start):
-            out.append((ci, start, stop))
+            if last and out and stop - start < min_bytes // 32:
+                out[-1] = (ci, out[-1][1], stop)            # a tiny remainder joins the last bucket
+            else:
+                out.append((ci, start, stop))
             start = stop
     return out
 
@@ -147,6 +148,50 @@ def gather_rows(ids, rows, out_ids, out_rows, group=None):
     w1 = dist.all_gather_into_tensor(out_ids, ids.reshape(-1), group=group, async_op=True)
     w2 = dist.all_gather_into_tensor(out_rows, rows, group=group, async_op=True)
     return [w1, w2]
+
+
+def plan_stages(segments, scaler, dw_stream=True):
+    """The DP backward's stages (DataParallelStep._plan_schedule).  segments: the backward's
+    calls cut at the bucket marks (bucket k final after segment k's calls); scaler: the
+    (lo, hi) call range of the ConvTranspose2d scaler segment (all weight gradient); calls with
+    `.side` set are weight-gradient calls.  Each stage is {"ops": [("main" | "fork", calls)],
+    "final": [bucket]}: a segment's weight-gradient calls are forked beside the NEXT segment
+    that has chain calls, a stage ends after a chain segment only where buckets become final,
+    and the last segment's weight gradients end the last stage.  Returns (stages, index of the
+    stage with the last chain call)."""
+    stages, ops, fin, pend, pend_b, prev = [], [], [], [], [], 0
+    for k, seg in enumerate(segments):
+        lo, hi = prev, prev + len(seg)
+        prev = hi
+        if (lo, hi) == tuple(scaler):
+            chain, dw = [], list(seg)
+        elif dw_stream:
+            chain, dw = [c for c in seg if not c.side], [c for c in seg if c.side]
+        else:
+            chain, dw = list(seg), []
+        if chain:
+            if pend:                                        # the pending dW, beside this chain
+                ops.append(("fork", pend))
+                fin, pend, pend_b = fin + pend_b, [], []
+            ops.append(("main", chain))
+        if dw:
+            pend, pend_b = pend + dw, pend_b + [k]
+        else:                                               # final with its own chain
+            fin = fin + [k]
+        if chain and fin:                                   # a stage ends where buckets become final
+            stages.append({"ops": ops, "final": fin})
+            ops, fin = [], []
+    if pend:                           # the last dW: nothing left to overlap it with, no stage of its own
+        if ops or not stages:
+            ops.append(("fork", pend))
+            fin = fin + pend_b
+        else:
+            stages[-1]["ops"].append(("fork", pend))
+            stages[-1]["final"] = stages[-1]["final"] + pend_b
+    if ops or fin:
+        stages.append({"ops": ops, "final": fin})
+    rows = max(j for j, st in enumerate(stages) if any(kd == "main" for kd, _ in st["ops"]))
+    return stages, rows
 
 
 class DataParallelStep:
@@ -320,28 +365,26 @@ class DataParallelStep:
 
     # ------------------------------------------------------------------ schedule
     def _plan_schedule(self):
-        """The backward is placed exactly as the single-GPU step graph places it
-        (engine.run_backward_streams: the input-gradient chain on the step's stream, the
-        side-tagged weight-gradient GEMMs on `wside`, the ConvTranspose2d scaler dW segment on
-        `side` beside the T5 backward), with an event recorded, on every stream that contributes
-        to it, where each gradient bucket becomes final.  A comm stream waits on a bucket's events
-        and issues its collective, so the collectives run while the later segments do.  With RCCL
-        the collectives, the row gather, the tail and the optimizer are captured into the SAME
-        graph as the backward (one replay per step; the graph executor keeps its own multi-queue
-        placement -- round 4 measured one graph per segment 14 % slower than the engine step at
-        world 1, the side-stream launches sharing a hardware queue with the chain, and ROCm's
-        torch refuses the external event records a host-issued exchange behind one graph would
-        need).  gloo (host-staged, tests only) replays the backward graph and then exchanges.
-        The squared-norm partials of [0, a) run on their own stream as soon as the buckets up to
-        `a` are reduced."""
-        import torch.distributed as dist
+        """The backward as a short sequence of STAGES, each one graph: a stage runs chain
+        segments (the input-gradient chain, the step's stream) with the weight-gradient calls
+        of the segments before them forked beside them (`wside`) -- the same placement as the
+        single-GPU step graph, where the batched dW GEMMs trail the chain on their own stream,
+        software-pipelined across graph boundaries so no stage waits for its own last segment's
+        weight gradients; a stage ends only where buckets become final, and the last segment's
+        dW ends the last stage.  A bucket is final when the stage that ran its last call has ended;
+        the host then issues its collective from a comm stream behind an event on the step's
+        stream, so it runs while the next stages do.  (Measured in round 4: one graph per
+        segment with the dW calls replayed as separate graphs on `wside` ran 14 % slower than the
+        engine step at world 1 -- those launches shared a hardware queue with the chain; the
+        collectives captured INTO one backward graph ran 11 % slower -- that graph executed
+        with its captured streams on the step stream's hardware queue, profiles/r04_dp_trace.txt;
+        ROCm's torch refuses external event records in a capture.)  The ConvTranspose2d scaler
+        dW segment (engine: on `side`, beside the T5 backward) is all weight gradient, so it is
+        deferred into the next stage like the others.  The squared-norm partials of [0, a) run on
+        their own stream once the buckets up to `a` are reduced."""
         e = self.eng
-        q0, q1 = e._bsplit                                  # DP call index == engine bwd_calls index
-        self.homes, prev = [], 0
-        for seg in self.segments:
-            lo, hi = prev, prev + len(seg)
-            prev = hi
-            self.homes.append("side" if (lo, hi) == (q0, q1) else "main")
+        self.stages, self.rows_stage = plan_stages(self.segments, e._bsplit, e.dw_stream)
+        assert sorted(k for st in self.stages for k in st["final"]) == list(range(len(self.buckets)))
         # the grad-norm partials of [0, a) (opt_calls[0]) need the buckets up to `a` reduced
         self.sq_after = None
         if not self.shard and e._sq_split is not None:
@@ -350,86 +393,114 @@ class DataParallelStep:
                 if stop >= a:
                     self.sq_after = k
                     break
-        self.opt_part = e.opt_calls[1:] if self.sq_after is not None else e.opt_calls
-        self._comm = torch.cuda.Stream(e.dev)               # issues the collectives behind the bucket events
+        opt_part = e.opt_calls[1:] if self.sq_after is not None else e.opt_calls
+        # after the last collective: the embedding scatter, then (unless sharded) clip + AdamW
+        self.finish_calls = self.tail + [self.emb_call] + ([] if self.shard else opt_part)
+        # (high-priority streams -- hardware queues of their own -- measured 2.5x slower, r04)
+        self._comm = torch.cuda.Stream(e.dev)               # issues the collectives behind the stage events
         self._sqs = torch.cuda.Stream(e.dev)                # the early grad-norm partials
-        # VQA_DP_HOST_EXCHANGE=1: the RCCL exchange issued from the host after the backward graph
-        # (no overlap; an A/B of the graph executor's queue placement only)
-        self.in_graph = dist.get_backend(self.group) != "gloo" and os.environ.get("VQA_DP_HOST_EXCHANGE") != "1"
+        self._tstream = torch.cuda.Stream(e.dev)            # timing mode: collective completions
 
-    def _backward_marked(self):
-        """The backward without the embedding scatter, placed as engine.run_backward_streams
-        places it, recording after each segment one event per contributing stream; returns
-        [[events of bucket k]] (bucket k's first event is its chain's)."""
+    def stage_plan(self):
+        """Per stage: its calls in order as ("chain" | "dw_fork", count), and the buckets final
+        after it."""
+        return [{"ops": [("chain" if kd == "main" else "dw_fork", len(c)) for kd, c in st["ops"]],
+                 "final_buckets": st["final"]} for st in self.stages]
+
+    def _run_stage(self, st):
+        """One stage on the current stream: its chain calls, and at each fork point the pending
+        weight-gradient calls on `wside` (after everything issued so far on the chain), joined
+        at the end of the stage."""
         e = self.eng
         main = torch.cuda.current_stream(e.dev)
-        side, wside = e._side, e._wside
-        for st in (side, wside):                            # both join the capture here
-            _after(st, main)
-        marks = []
-        for seg, home in zip(self.segments, self.homes):
-            if home == "side":                              # scaler dW beside the T5 backward
-                _after(side, main)
-                with torch.cuda.stream(side):
-                    self._run(seg)
-                evs = [torch.cuda.Event()]
-                evs[0].record(side)
+        forked = False
+        for kind, calls in st["ops"]:
+            if kind == "main":
+                self._run(calls)
             else:
-                e._run_tagged(seg, main, wside)
-                evs = [torch.cuda.Event(), torch.cuda.Event()]
-                evs[0].record(main)
-                evs[1].record(wside)
-            marks.append(evs)
-        for st in (side, wside):                            # joined again before the graph ends
-            _after(main, st)
-        return marks
+                _after(e._wside, main)
+                with torch.cuda.stream(e._wside):
+                    self._run(calls)
+                forked = True
+        if forked:
+            _after(main, e._wside)
 
-    def _exchange(self, marks):
-        """Per bucket: the comm stream waits on the bucket's events (None: on everything issued
-        so far) and issues its collective; the embedding rows are gathered before the last
-        bucket's collective; the [0, a) grad-norm partials run on their own stream once their
-        buckets are reduced; then the embedding scatter (tail) and, unless sharded, the optimizer
-        plan.  Runs eagerly or under capture alike.  Returns the timing events (timing mode)."""
+    def _backward_exchange(self):
+        """The staged backward with the exchange issued between the stages; the step's stream
+        waits on the collectives only at the end, then runs the embedding scatter + (unless
+        sharded) the optimizer plan as one graph.  The comm stream never waits on a collective
+        (a wait packet there would hold back whatever stage kernels share its hardware queue);
+        only the grad-norm stream and the final join do.  Returns the timing record (timing
+        mode): stage-end and collective-done events, the final wait."""
         e = self.eng
+        g = self.graphs
         main = torch.cuda.current_stream(e.dev)
-        exchange = (lambda i, bk: self._sharded_collectives_after(i)) if self.shard else \
-            (lambda i, bk: allreduce_buckets(e.G32, [bk], self.group))
+        exchange = lambda i, bk: self._sharded_collectives_after(i)    # noqa: E731
         comm, sqs = self._comm, self._sqs
-        works, rows = [], None
-        nseg = len(self.segments)
-        for k, bk in enumerate(self.buckets):
-            evs = marks[k] if marks is not None else []
-            if evs:
-                comm.wait_event(evs[0])
-            else:
-                _after(comm, main)
-            with torch.cuda.stream(comm):
-                if k == nseg - 1:
-                    # the embedding rows (dH32) are final with the last chain segment: gathered
-                    # before the last bucket's collective, whose weight gradients may still run
-                    rows = gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
-                for ev in evs[1:]:
-                    comm.wait_event(ev)
-                works += exchange(k, bk)
-            if k == self.sq_after:                          # grad-norm partials of [0, a), beside the rest
-                _after(sqs, comm)
-                with torch.cuda.stream(sqs):
-                    for w in works:
+        tm = {"stage": {}, "done": {}} if self.timing else None
+        works = {}
+
+        def mark_done(key, ws):
+            if tm is not None:                              # completion seen from a timing-only stream
+                with torch.cuda.stream(self._tstream):
+                    for w in ws:
                         w.wait()
-                    self._run(e.opt_calls[:1])
-        tev = []
-        self._wait(rows, tev)                               # the embedding rows: needed by the tail
-        self._run(self.tail + [self.emb_call])
-        for w in works:
-            self._wait([w], tev)
+                    tm["done"][key] = torch.cuda.Event(enable_timing=True)
+                    tm["done"][key].record(self._tstream)
+        for j, st in enumerate(self.stages):
+            if g is not None:
+                g[f"stage{j}"].replay()
+            else:
+                self._run_stage(st)
+            if not (st["final"] or j == self.rows_stage):
+                continue
+            if tm is not None:
+                tm["stage"][j] = torch.cuda.Event(enable_timing=True)
+                tm["stage"][j].record(main)
+            _after(comm, main)
+            with torch.cuda.stream(comm):
+                if j == self.rows_stage:
+                    works["rows"] = gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
+                    mark_done("rows", works["rows"])
+                if self.shard:
+                    for k in st["final"]:
+                        works[k] = exchange(k, self.buckets[k])
+                        mark_done(k, works[k])
+                else:                                       # the stage's buckets are contiguous: one all-reduce
+                    ks = st["final"]
+                    assert ks == list(range(ks[0], ks[-1] + 1))
+                    ws = allreduce_buckets(e.G32, [(None, self.buckets[ks[0]][1], self.buckets[ks[-1]][2])], self.group)
+                    for k in ks:
+                        works[k] = ws if k == ks[-1] else []
+                        mark_done(k, ws)
+            if self.sq_after is not None and "sq" not in works and \
+                    all(k in works for k in range(self.sq_after + 1)):
+                works["sq"] = []                            # grad-norm partials of [0, a), beside the rest
+                with torch.cuda.stream(sqs):
+                    for k in range(self.sq_after + 1):
+                        for w in works[k]:
+                            w.wait()
+                    self._play("sq0", e.opt_calls[:1])
+        if tm is not None:
+            tm["wait"] = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            tm["wait"][0].record(main)
+        for key, ws in works.items():
+            for w in ws:
+                w.wait()
         for st in (comm, sqs):                              # gloo: the staged copies ran on comm
             _after(main, st)
-        if not self.shard:
-            self._run(self.opt_part)
-        return tev
+        if tm is not None:
+            tm["wait"][1].record(main)
+        self._play("finish", self.finish_calls)
+        return tm
+
+    def _play(self, name, calls):
+        if self.graphs is not None:
+            self.graphs[name].replay()
+        else:
+            self._run(calls)
 
     def capture(self):
-        import torch.distributed as dist
         e = self.eng
         e.flush_optimizer()              # the warm-up's backward must not overwrite a pending update's G
         s = torch.cuda.Stream(e.dev)
@@ -438,9 +509,6 @@ class DataParallelStep:
         with torch.cuda.stream(s):                          # warm-up outside capture (no optimizer update)
             e._run(e.fwd_calls)
             e.backward()
-        if self.in_graph:                                   # communicators exist before the capture
-            with torch.cuda.stream(self._comm):
-                dist.all_reduce(torch.zeros(1, device=e.dev), group=self.group)
         torch.cuda.current_stream(e.dev).wait_stream(s)
         torch.cuda.synchronize(e.dev)
         e.RNG.copy_(saved_rng)                              # the warm-up must not consume a dropout draw
@@ -450,21 +518,20 @@ class DataParallelStep:
     def _capture_all(self, s):
         e = self.eng
         gs = {}
-        g = torch.cuda.CUDAGraph()                          # forward: ResNet || T5 encoder on two streams
-        with torch.cuda.graph(g, stream=s):
-            e.run_forward_streams()
-        gs["fwd"] = g
-        if e.pipeline:                                      # the next batch's ResNet, replayed beside the step
+
+        def cap(name, fn):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
-                self._run(e.res_calls)
-            gs["res"] = g
-        g = torch.cuda.CUDAGraph()                          # backward (+ collectives, tail, optimizer)
-        with torch.cuda.graph(g, stream=s):
-            marks = self._backward_marked()
-            if self.in_graph:
-                self._exchange(marks)
-        gs["bwd"] = g
+                fn()
+            gs[name] = g
+        cap("fwd", e.run_forward_streams)                   # forward: ResNet || T5 encoder on two streams
+        if e.pipeline:                                      # the next batch's ResNet, replayed beside the step
+            cap("res", lambda: self._run(e.res_calls))
+        for j, st in enumerate(self.stages):
+            cap(f"stage{j}", lambda st=st: self._run_stage(st))
+        if self.sq_after is not None:
+            cap("sq0", lambda: self._run(e.opt_calls[:1]))
+        cap("finish", lambda: self._run(self.finish_calls))
         return gs
 
     def _res_begin(self):
@@ -489,62 +556,36 @@ class DataParallelStep:
 
     def step(self):
         e = self.eng
-        g = self.graphs
         self._res_begin()
-        tev = None
-        if g is None:                                       # eager: the same schedule, issued live
-            e.forward()
-            tev = self._exchange(self._backward_marked())
+        if self.graphs is not None:
+            self.graphs["fwd"].replay()
         else:
-            g["fwd"].replay()
-            g["bwd"].replay()
-            if not self.in_graph:                           # gloo: exchange after the backward graph
-                tev = self._exchange(None)
+            e.forward()
+        tev = self._backward_exchange()
         if self.shard:
             self._sharded_optimizer()
         self._res_end()
-        if self.timing and tev is not None:
+        if self.timing:
             self._ev.append(tev)
 
-    def measure_exposed(self, step_fn, steps=3):
-        """Per-collective exposed waits are host-visible only when the exchange is issued from
-        the host: run `steps` calls of step_fn with the graphs off (the same schedule, eager)
-        and timing on, then restore.  Returns timing_report()."""
-        saved, t = self.graphs, self.timing
-        self.graphs, self.timing, self._ev = None, True, []
-        try:
-            for _ in range(steps):
-                step_fn()
-            rep = self.timing_report()
-        finally:
-            self.graphs, self.timing = saved, t
-        if rep is not None:
-            rep["mode"] = "eager steps after the timed region (graphed steps issue their collectives in the backward graph)"
-        return rep
-
-    def _wait(self, works, evs):
-        if not self.timing:
-            for w in works:
-                w.wait()
-            return
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        for w in works:
-            w.wait()
-        b.record()
-        evs.append((a, b))
-
     def timing_report(self):
-        """Mean exposed wait per collective over the steps run with `timing` on: the row gather,
-        then each gradient bucket (its bytes, the slice of G32 it covers)."""
+        """Over the steps run with `timing` on (HIP events): for the row gather and each gradient
+        bucket, how long after the end of the stage that finished it its collective completed
+        (queueing behind the earlier ones included), and the step stream's exposed wait on the
+        exchange before the embedding scatter + optimizer."""
         torch.cuda.synchronize()
         if not self._ev:
             return None
-        waits = np.array([[a.elapsed_time(b) * 1e3 for a, b in evs] for evs in self._ev]).mean(0)
         e = self.eng
-        return {"world_size": self.world, "steps": len(self._ev),
+        stage_of = {k: j for j, st in enumerate(self.stages) for k in st["final"]}
+        stage_of["rows"] = self.rows_stage
+
+        def mean(f):
+            return round(float(np.mean([f(t) for t in self._ev])), 1)
+        lag = {k: mean(lambda t, k=k: t["stage"][stage_of[k]].elapsed_time(t["done"][k]) * 1e3) for k in stage_of}
+        return {"world_size": self.world, "steps": len(self._ev), "stages": self.stage_plan(),
                 "embedding_rows_gather": {"bytes": int(self.world * e.T * (e.D * 4 + 8)),
-                                          "exposed_wait_us": round(float(waits[0]), 1)},
-                "buckets": [{"start": int(a), "stop": int(b), "bytes": int(4 * (b - a)),
-                             "exposed_wait_us": round(float(w), 1)} for (_, a, b), w in zip(self.buckets, waits[1:])],
-                "exposed_wait_us_total": round(float(waits.sum()), 1)}
+                                          "done_us_after_stage": lag["rows"]},
+                "buckets": [{"start": int(a), "stop": int(b), "bytes": int(4 * (b - a)), "stage": stage_of[k],
+                             "done_us_after_stage": lag[k]} for k, (_, a, b) in enumerate(self.buckets)],
+                "exposed_wait_us_total": mean(lambda t: t["wait"][0].elapsed_time(t["wait"][1]) * 1e3)}

@@ -139,3 +139,44 @@ def test_dp_gradient_average_equals_global_batch(tmp_path):
     got = np.load(tmp_path / "dp_grads.npy")
     err = np.abs(got - ref).max() / np.abs(ref).max()
     assert err < 1e-5, err
+
+
+class _C:
+    def __init__(self, seg, i, side):
+        self.seg, self.i, self.side = seg, i, side
+
+
+@pytest.mark.parametrize("dw_stream", [True, False])
+def test_plan_stages_keep_order_and_finality(pkg, dw_stream):
+    """dp.plan_stages: every backward call lands in exactly one stage; the chain calls keep
+    their order; a segment's weight-gradient calls are forked only after that segment's chain
+    calls (and after everything forked before them); every bucket becomes final exactly once, in
+    a stage at or after the one running its last call; no stage ends without a final bucket."""
+    rng = np.random.default_rng(0)
+    sizes = [40, 9, 33, 26, 14, 6]                     # head+SGA, scaler dW, T5 groups, last layer
+    segs = []
+    for k, n in enumerate(sizes):
+        segs.append([_C(k, i, (k == 1) or bool(rng.random() < 0.3)) for i in range(n)])
+    scaler = (sizes[0], sizes[0] + sizes[1])
+    stages, rows = pkg.dp.plan_stages(segs, scaler, dw_stream)
+    seq = [(j, kd, c) for j, st in enumerate(stages) for kd, cs in st["ops"] for c in cs]
+    allc = [c for s in segs for c in s]
+    assert sorted(id(c) for _, _, c in seq) == sorted(id(c) for c in allc)
+    mains = [c for _, kd, c in seq if kd == "main"]
+    ref = [c for s in segs for c in s if not (c.seg == 1 or (dw_stream and c.side))]
+    assert [id(c) for c in mains] == [id(c) for c in ref]
+    pos = {id(c): p for p, (_, _, c) in enumerate(seq)}
+    last_main = {}
+    for c in mains:
+        last_main[c.seg] = pos[id(c)]
+    forks = [c for _, kd, c in seq if kd == "fork"]
+    assert [(c.seg, c.i) for c in forks] == sorted((c.seg, c.i) for c in forks)
+    for c in forks:
+        assert pos[id(c)] > last_main.get(c.seg, -1)
+    final_at = {k: j for j, st in enumerate(stages) for k in st["final"]}
+    assert sorted(final_at) == list(range(len(segs)))
+    assert sum(len(st["final"]) for st in stages) == len(segs)
+    for c in allc:
+        assert final_at[c.seg] >= next(j for j, _, x in seq if x is c)
+    assert all(st["final"] for st in stages)
+    assert len(stages) < len(segs) and rows == max(j for j, kd, _ in seq if kd == "main")

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def pg():
+def pg(pkg):
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     s = socket.socket()

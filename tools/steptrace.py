@@ -12,7 +12,7 @@ import sys
 db = sys.argv[1]
 marker = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else "rng_advance"
 c = sqlite3.connect(db)
-rows = c.execute("select start, end, name, queue_id from kernels order by start").fetchall()
+rows = c.execute("select start, end, name, queue_id, stream_id from kernels order by start").fetchall()
 
 
 def short(n):
@@ -30,6 +30,10 @@ for q in qs:
     ks = [r for r in win if r[3] == q]
     busy = sum(r[1] - r[0] for r in ks)
     print(f"queue {q}: {len(ks)} kernels, busy {busy / 1e3:.1f} us, span {(ks[-1][1] - ks[0][0]) / 1e3:.1f} us")
+pairs = {}
+for r in win:
+    pairs[(r[4], r[3])] = pairs.get((r[4], r[3]), 0) + 1
+print("(stream, queue): kernels  " + "  ".join(f"({s_},{q_}) {n_}" for (s_, q_), n_ in sorted(pairs.items())))
 # union busy (any queue)
 iv = sorted((r[0], r[1]) for r in win)
 u, cs, ce = 0, iv[0][0], iv[0][1]
@@ -42,11 +46,11 @@ for s, e in iv[1:]:
 u += ce - cs
 print(f"union busy {u / 1e3:.1f} us  (idle {(t1 - t0 - u) / 1e3:.1f} us)")
 fam = {}
-for s, e, n, q in win:
+for s, e, n, q, _ in win:
     k = short(n).split("<")[0]
     fam[k] = fam.get(k, 0) + e - s
 for k, v in sorted(fam.items(), key=lambda kv: -kv[1])[:20]:
     print(f"  {v / 1e3:8.1f} us  {k}")
 if "--list" in sys.argv:
-    for s, e, n, q in win:
-        print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} q{q} {short(n)}")
+    for s, e, n, q, sid in win:
+        print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} q{q} s{sid} {short(n)}")
