@@ -98,8 +98,10 @@ def test_vit_bench_step_b64_matches_oracle(pkg, parity_report):
     # relative L2 of the per-group update vectors after three steps: measured 0.04 (classifier),
     # 0.16 (T5), 0.19 (fusing layer, whose Dropout(0.5) input is the bf16 ViT token)
     assert max(delta.values()) <= 0.25, delta
-    # with the engine's pooled outputs the oracle follows the engine much more closely: the bulk of
-    # the trajectory error above is the frozen ViT's bf16 forward (each of its ops equals bf16-operand
-    # arithmetic on the engine's inputs: tools/vit_layer_diag.py)
+    # A/B with the engine's pooled outputs fed to the oracle: at B = 64 it does NOT bring the
+    # oracle closer (measured r04: step-2 log-probs 0.110 vs 0.100, grad norm 2.6e-3 vs 1.2e-3):
+    # the step-2 log-prob error is the first nonzero-lr AdamW update moving every weight by
+    # ~lr * sign(g) on near-zero gradient entries, not the frozen ViT's bf16 forward
     r2 = rep2["step2"]
-    assert r2["log_prob_max_abs"] <= r["log_prob_max_abs"] and max(rep2["update_rel_l2"].values()) <= 0.25, rep2
+    assert r2["log_prob_max_abs"] <= 0.13 and r2["grad_norm_rel"] <= 4e-3, rep2
+    assert max(rep2["update_rel_l2"].values()) <= 0.25, rep2
