@@ -52,62 +52,6 @@ pmc)
     echo "pmc summary $W written"
   done
   ;;
-bench), copied to profiles/:
-#   suite: GPU test suite -> parity report; smoke
-#   pmc:   kernel-trace stats of the config-2 and config-5 benches; PMC passes of both steps and of
-#          their replayed launches, stamped with this tree's digest and PMC_COMMIT
-#   bench: config-2 bench with the CPU baseline (quoting the PMC file), config 5, config 4, --dp,
-#          the collate bench, the SGA launch table, bench.py --gpus 8 --rehearse
-set -o pipefail
-R=$GRAFT_REPO_ROOT
-cd $R && mkdir -p gpurun_out
-export TMPDIR=/tmp
-case "${STAGE:-suite}" in
-suite)
-  rm -f gpurun_out/parity_report.json
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread -p no:cacheprovider \
-     > gpurun_out/r04_gputest.log 2>&1 || { grep -E "FAILED|ERROR|passed|failed" gpurun_out/r04_gputest.log | tail -20; exit 1; }
-  grep -E "passed|failed" gpurun_out/r04_gputest.log | tail -1
-  timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04_smoke.log 2>&1 || { echo SMOKEFAIL; tail -20 gpurun_out/r04_smoke.log; exit 1; }
-  tail -1 gpurun_out/r04_smoke.log
-  ;;
-pmc)
-  rm -rf gpurun_out/r04_stats gpurun_out/r04_stats_c5
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/r04_stats -o run -- python3 bench.py --no-cpu-baseline \
-     > gpurun_out/r04_stats_bench.json 2> gpurun_out/r04_stats_bench.err || { echo STATSFAIL; tail -20 gpurun_out/r04_stats_bench.err; exit 1; }
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/r04_stats_c5 -o run -- python3 bench.py --config5 --no-cpu-baseline \
-     > gpurun_out/r04_stats_c5.json 2> gpurun_out/r04_stats_c5.err || { echo STATSC5FAIL; tail -20 gpurun_out/r04_stats_c5.err; exit 1; }
-  cd /tmp
-  run() {  # tag counters... -- cmd   (each counter group in a run of its own)
-    local tag=$1; shift
-    local ctrs=()
-    while [ "$1" != "--" ]; do ctrs+=("$1"); shift; done; shift
-    rm -rf $R/gpurun_out/pmc_$tag
-    timeout -k 10 240 rocprofv3 --pmc "${ctrs[@]}" -f csv -d $R/gpurun_out/pmc_$tag -o $tag -- "$@" > $R/gpurun_out/pmc_$tag.log 2>&1 \
-      || { echo "PMCFAIL $tag"; tail -20 $R/gpurun_out/pmc_$tag.log; exit 1; }
-    echo "pass $tag ok"
-  }
-  for W in c2 c5; do
-    X=""; M=default
-    if [ $W = c5 ]; then X="--config5"; M=c5; fi
-    B="python3 $R/bench.py $X --steps 3 --warmup 1 --no-cpu-baseline --no-kernel-rooflines"
-    K="python3 $R/tools/kernel_replay.py $R/gpurun_out/replay_manifest_$W.json 5 $M"
-    run ${W}sF FETCH_SIZE -- $B
-    run ${W}sW WRITE_SIZE -- $B
-    run ${W}sM SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -- $B
-    run ${W}rF FETCH_SIZE -- $K
-    run ${W}rW WRITE_SIZE -- $K
-    run ${W}rM SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -- $K
-  done
-  cd $R
-  for W in c2 c5; do
-    OUT=gpurun_out/r04_pmc.json; [ $W = c5 ] && OUT=gpurun_out/r04_pmc_c5.json
-    python3 tools/pmc_step.py $OUT gpurun_out/pmc_${W}sF gpurun_out/pmc_${W}sW gpurun_out/pmc_${W}sM \
-       gpurun_out/pmc_${W}rF gpurun_out/pmc_${W}rW gpurun_out/pmc_${W}rM gpurun_out/replay_manifest_$W.json \
-       > gpurun_out/r04_pmc_$W.log 2>&1 || { echo "SUMFAIL $W"; tail -30 gpurun_out/r04_pmc_$W.log; exit 1; }
-  done
-  echo pmc summaries written
-  ;;
 bench)
   # profiles/r04_pmc*.json must hold this tree's passes (bench.py quotes them only on a digest match)
   timeout -k 10 400 python bench.py > gpurun_out/r04_bench_final.json 2> gpurun_out/r04_bench_final.err || { echo BENCHFAIL; tail -20 gpurun_out/r04_bench_final.err; exit 1; }
