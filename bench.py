@@ -409,7 +409,9 @@ def main():
     f8 = calls_flop(eng, fp8_only=True)
     peak = MFMA_PEAK_TFLOPS if f8 == 0 else calls_flop(eng) / (f8 / FP8_PEAK_TFLOPS + (calls_flop(eng) - f8) /
                                                                MFMA_PEAK_TFLOPS)
-    roofline = {"bound": "mfma", "kernel": f"whole train step (one hipGraph replay: ResNet50 fwd, ConvT, {lm}, {NB}xSGA, "
+    replay = ("DataParallelStep: forward graph, 4 backward stage graphs with the RCCL exchange between them, "
+              "finish graph" if use_dp else "one hipGraph replay")
+    roofline = {"bound": "mfma", "kernel": f"whole train step ({replay}: ResNet50 fwd, ConvT, {lm}, {NB}xSGA, "
                                            "head, backward, clip, AdamW)",
                 "achieved": round(step_tflops, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(step_tflops / peak, 4),
