@@ -77,3 +77,33 @@ def test_dp_world1_matches_single_gpu(pg, pkg, graph, pipe):
     e1.flush_optimizer()
     e2.flush_optimizer()
     assert torch.equal(e1.P32, e2.P32)
+
+
+def test_dp_world1_sharded_optimizer_rccl(pg, pkg):
+    """The sharded optimizer's RCCL path (reduce-scatter into the per-bucket output buffer, copy
+    into the own chunk, sharded AdamW, all-gather of the fp32 masters and bf16 shadows) at world 1:
+    the trajectory of the single-GPU step.  Multi-rank arithmetic: tests/test_a_dp2_gpu.py (gloo)."""
+    B, L, H = 4, 32, 96
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    nbs = [pkg.synthetic.make_batch(B, L, H, seed=1 + i) for i in range(3)]
+    dev = [{k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None} for nb in nbs]
+    e1 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20)
+    e2 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, t5_dw_group=(4, 4, 3, 1))
+    e1.capture()
+    step = pkg.dp.DataParallelStep(e2, bucket_mb=8, use_graph=True, shard_optimizer=True)
+    for i in range(3):
+        for e in (e1, e2):
+            e.load_batch(dev[i])
+        e1.train_step()
+        step.step()
+        torch.cuda.synchronize()
+        assert float(e1.LOSS) == float(e2.LOSS), i
+        n1, n2 = e1.last_grad_norm(), e2.last_grad_norm()
+        assert abs(n1 - n2) <= 1e-6 * abs(n1), (i, n1, n2)
+    e1.flush_optimizer()
+    e2.flush_optimizer()
+    step.sync_optimizer_state()
+    rel = float((e1.P32 - e2.P32).norm() / e1.P32.norm())
+    assert rel <= 1e-6, rel
+    vrel = float((e1.VMAX - e2.VMAX).norm() / e1.VMAX.norm())
+    assert vrel <= 1e-5, vrel
