@@ -351,8 +351,6 @@ def main():
     for i in range(args.warmup):
         step(i)
     stream = torch.cuda.current_stream(dev)
-    if use_dp:                             # collective completion + exposed wait (HIP events)
-        dps.timing = True
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if dist:
@@ -439,9 +437,13 @@ def main():
         "roofline": roofline,
         "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
     }
-    if use_dp:
+    if use_dp:                             # collective completion + exposed wait (HIP events), on 3
+        dps.timing = True                  # steps after the timed region (its waits would perturb it)
+        for i in range(3):
+            step(args.steps + i)
         out["dp"] = dps.timing_report()
         out["dp"]["backend"] = dist.get_backend()
+        out["dp"]["timing_steps"] = "3 steps after the timed region"
     if args.rehearse:                               # the N-rank path's results: lockstep across ranks
         eng.flush_optimizer()
         p = eng.P32[:: max(1, eng.P32.numel() // 65536)].cpu()

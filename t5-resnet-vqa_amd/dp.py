@@ -380,25 +380,18 @@ class DataParallelStep:
         with its captured streams on the step stream's hardware queue, profiles/r04_dp_trace.txt;
         ROCm's torch refuses external event records in a capture.)  The ConvTranspose2d scaler
         dW segment (engine: on `side`, beside the T5 backward) is all weight gradient, so it is
-        deferred into the next stage like the others.  The squared-norm partials of [0, a) run on
-        their own stream once the buckets up to `a` are reduced."""
+        deferred into the next stage like the others."""
         e = self.eng
         self.stages, self.rows_stage = plan_stages(self.segments, e._bsplit, e.dw_stream)
         assert sorted(k for st in self.stages for k in st["final"]) == list(range(len(self.buckets)))
-        # the grad-norm partials of [0, a) (opt_calls[0]) need the buckets up to `a` reduced
-        self.sq_after = None
-        if not self.shard and e._sq_split is not None:
-            a = e._sq_split[1]
-            for k, (_, _, stop) in enumerate(self.buckets):
-                if stop >= a:
-                    self.sq_after = k
-                    break
-        opt_part = e.opt_calls[1:] if self.sq_after is not None else e.opt_calls
-        # after the last collective: the embedding scatter, then (unless sharded) clip + AdamW
-        self.finish_calls = self.tail + [self.emb_call] + ([] if self.shard else opt_part)
+        # after the last collective: the embedding scatter, then (unless sharded) the whole optimizer
+        # plan (grad-norm partials, clip, AdamW).  The [0, a) partials once ran on a stream of their own
+        # behind the early buckets' collectives: at world 1 they did not overlap anything (trace), and at
+        # N > 1 that stream's wait on a running collective would hold back whatever stage kernels share
+        # its hardware queue
+        self.finish_calls = self.tail + [self.emb_call] + ([] if self.shard else list(e.opt_calls))
         # (high-priority streams -- hardware queues of their own -- measured 2.5x slower, r04)
         self._comm = torch.cuda.Stream(e.dev)               # issues the collectives behind the stage events
-        self._sqs = torch.cuda.Stream(e.dev)                # the early grad-norm partials
         self._tstream = torch.cuda.Stream(e.dev)            # timing mode: collective completions
 
     def stage_plan(self):
@@ -436,7 +429,7 @@ class DataParallelStep:
         g = self.graphs
         main = torch.cuda.current_stream(e.dev)
         exchange = lambda i, bk: self._sharded_collectives_after(i)    # noqa: E731
-        comm, sqs = self._comm, self._sqs
+        comm = self._comm
         tm = {"stage": {}, "done": {}} if self.timing else None
         works = {}
 
@@ -473,22 +466,13 @@ class DataParallelStep:
                     for k in ks:
                         works[k] = ws if k == ks[-1] else []
                         mark_done(k, ws)
-            if self.sq_after is not None and "sq" not in works and \
-                    all(k in works for k in range(self.sq_after + 1)):
-                works["sq"] = []                            # grad-norm partials of [0, a), beside the rest
-                with torch.cuda.stream(sqs):
-                    for k in range(self.sq_after + 1):
-                        for w in works[k]:
-                            w.wait()
-                    self._play("sq0", e.opt_calls[:1])
         if tm is not None:
             tm["wait"] = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             tm["wait"][0].record(main)
         for key, ws in works.items():
             for w in ws:
                 w.wait()
-        for st in (comm, sqs):                              # gloo: the staged copies ran on comm
-            _after(main, st)
+        _after(main, comm)                                  # gloo: the staged copies ran on comm
         if tm is not None:
             tm["wait"][1].record(main)
         self._play("finish", self.finish_calls)
@@ -529,8 +513,6 @@ class DataParallelStep:
             cap("res", lambda: self._run(e.res_calls))
         for j, st in enumerate(self.stages):
             cap(f"stage{j}", lambda st=st: self._run_stage(st))
-        if self.sq_after is not None:
-            cap("sq0", lambda: self._run(e.opt_calls[:1]))
         cap("finish", lambda: self._run(self.finish_calls))
         return gs
 
