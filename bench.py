@@ -248,8 +248,6 @@ def main():
     ap.add_argument("--dp", action="store_true",
                     help="N = 1: run the N > 1 step (dp.DataParallelStep over a world-1 RCCL group, the DP engine's "
                          "weight-gradient groups) instead of the single-GPU engine graph")
-    ap.add_argument("--convt-copies", action="store_true",
-                    help="the r03 ConvTranspose2d dW form (9 tap-shifted copies + batched GEMM) instead of a_conv = 3")
     ap.add_argument("--dp-groups", action="store_true",
                     help="the single-GPU engine step with the DP engine's T5 weight-gradient groups (A/B of --dp)")
     ap.add_argument("--rehearse", action="store_true",
@@ -312,7 +310,7 @@ def main():
     eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev, num_blocks=NB,
                                warmup=10, total=100000, dropout=0.1, seed=rank, pipeline=pipe,
                                t5_dw_group=dp_groups if (use_dp or args.dp_groups) else None, language_model=lm,
-                               fp8=args.config5, convt_tap_gather=not args.convt_copies)
+                               fp8=args.config5)
     del sd
     pool = []
     for i in range(4):
@@ -482,18 +480,15 @@ def kernel_rooflines(eng, stream, pmc):
                            "traffic": (round(pmc["adamw_kernel"]["traffic_bytes"]) if "adamw_kernel" in pmc else None),
                            "algorithmic_bytes": adam_bytes, "kernel_avg_us": round(adam_dur * 1e6, 2)}
     # MFMA: the largest single launch, the ConvTranspose2d weight gradient as one GEMM batched
-    # over the 9 taps (M=768, N=2048, K=B*49, batch 9; A = dVIS read shifted per tap in place,
-    # vqa_gemm a_conv = 3 -- or, --convt-copies, over vqa_tap_shift copies; 2*M*N*K*9 FLOP, the
-    # same work as the implicit-im2col form M=768, N=9*2048)
+    # over the 9 taps (M=768, N=2048, K=B*49, batch 9 over vqa_tap_shift copies of dVIS;
+    # 2*M*N*K*9 FLOP, the same work as the implicit-im2col form M=768, N=9*2048)
     wg_call = eng.scaler_dw_call
     assert wg_call.name == "vqa_gemm" and wg_call.desc.batch == 9
     cfg = VL.load().vqa_gemm_select(wg_call.desc)
     bm, bn, st = VL.GEMM_TILES[cfg]
     wm, wn = VL.GEMM_WAVES[cfg]
-    ga = "true" if wg_call.desc.a_conv == 3 else "false"
-    kname = (f"gemm_kernel<{bm}, {bn}, {st}, {wm}, {wn}, false, false, {ga}, false> (ConvTranspose2d dW, tap-batched "
-             f"GEMM, batch 9, {'dVIS gathered per tap (a_conv 3)' if ga == 'true' else 'tap copies'}, "
-             f"splitk={max(1, wg_call.desc.splitk)})")
+    kname = (f"gemm_kernel<{bm}, {bn}, {st}, {wm}, {wn}, false, false, false, false> (ConvTranspose2d dW, tap-batched "
+             f"GEMM, batch 9, splitk={max(1, wg_call.desc.splitk)})")
     kdur = time_kernel(wg_call, 20, stream)
     kflop = 2.0 * wg_call.desc.m * wg_call.desc.n * wg_call.desc.k * wg_call.desc.batch
     k_tflops = kflop / kdur / 1e12

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 17
+#define VQA_ABI_VERSION 16
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -73,12 +73,6 @@ int vqa_dropout_mask(const vqa_dropout* d, float* out, long long n, hipStream_t 
  *   once per 64-channel chunk in LDS (each input pixel crosses L2 -> LDS once, not 9x):
  *   k = (c / 64, kh, kw, c % 64), i.e. weights stored [Cout][C/64][3][3][64]; C % 64 == 0,
  *   b_trans = 0, batch 1, no split-K; tile configs VQA_GEMM_PATCH_FIRST..VQA_GEMM_PATCH_LAST.
- * a_conv = 3: the ConvTranspose2d weight gradient's tap-batched A, read in place: batch z is
- *   the tap (ky, kx) = (z / ga.kw, z % ga.kw) and A(m,k) = map[k shifted by (pad - ky, pad - kx)][m]
- *   (zero outside), map = a, an NHWC map with ga.c = m channels, k = (img, y, x) over ga.n x
- *   ga.h x ga.w (= ga.oh x ga.ow); requires a_trans = 1, stride 1, stride_a = 0 and batch =
- *   ga.kh * ga.kw.  Replaces vqa_tap_shift's 9 materialised copies + the batched GEMM over them
- *   (bitwise the same result).
  * b_conv: B(k,n) is the implicit im2col with k = output pixel, n = (kh,kw,c);
  *   requires b_trans = 1 (weight-gradient of a convolution).
  * Epilogue: k = [mask(m,n) > 0] * dropout multiplier of element (z*m+row)*n+col

@@ -176,11 +176,7 @@ static int prepare(const vqa_gemm_desc* d, GemmParams& P) {
   VQA_REQUIRE((d->a_trans && d->b_trans) || d->k % 8 == 0, "vqa_gemm: k must be a multiple of 8 for a k-contig operand");
   VQA_REQUIRE(!d->a_trans || d->m % 8 == 0, "vqa_gemm: m must be a multiple of 8 for m-contig A");
   VQA_REQUIRE(!d->b_trans || d->n % 8 == 0, "vqa_gemm: n must be a multiple of 8 for n-contig B");
-  VQA_REQUIRE(d->a_conv == 3 ? d->a_trans : !(d->a_conv && d->a_trans), "vqa_gemm: a_conv 1 / 2 need a_trans=0, 3 a_trans=1");
-  VQA_REQUIRE(d->a_conv != 3 || (d->batch == d->ga.kh * d->ga.kw && d->ga.stride == 1 && d->stride_a == 0 &&
-                                 d->m == d->ga.c && d->ga.oh == d->ga.h && d->ga.ow == d->ga.w &&
-                                 (long long)d->k == (long long)d->ga.n * d->ga.h * d->ga.w && !d->b_conv && !d->fp8),
-              "vqa_gemm(a_conv=3): batch = kh*kw taps, stride 1, stride_a 0, m = map channels, k = n*h*w, same-size map");
+  VQA_REQUIRE(!(d->a_conv && d->a_trans), "vqa_gemm: a_conv needs a_trans=0");
   VQA_REQUIRE(!(d->b_conv && !d->b_trans), "vqa_gemm: b_conv needs b_trans=1");
   VQA_REQUIRE(!d->a_conv || d->ga.c % 8 == 0, "vqa_gemm: conv input channels must be a multiple of 8");
   VQA_REQUIRE(!d->b_conv || d->gb.c % 8 == 0, "vqa_gemm: conv input channels must be a multiple of 8");
@@ -283,7 +279,6 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   if (akc && bkc && !d->a_conv) return dispatch_tile<true, true, false, false>(P, batch, cfg, stream);
   if (akc && bkc && d->a_conv) return dispatch_tile<true, true, true, false>(P, batch, cfg, stream);
   if (akc && !bkc && !d->a_conv && !d->b_conv) return dispatch_tile<true, false, false, false>(P, batch, cfg, stream);
-  if (!akc && !bkc && d->a_conv == 3) return dispatch_tile<false, false, true, false>(P, batch, cfg, stream);
   if (!akc && !bkc && !d->b_conv) return dispatch_tile<false, false, false, false>(P, batch, cfg, stream);
   if (!akc && !bkc && d->b_conv) return dispatch_tile<false, false, false, true>(P, batch, cfg, stream);
   if (!akc && bkc) return dispatch_tile<false, true, false, false>(P, batch, cfg, stream);

@@ -58,16 +58,6 @@ __device__ __forceinline__ void gemm_body(const GemmParams& P, const int bid, ch
   LB lb;
   la.init(m0, P.m, P.lda, P.ga);
   lb.init(n0, P.n, P.ldb, P.gb);
-  if constexpr (GA && !AKC) {
-    // a_conv = 3 (ConvTranspose2d dW): the batch index is the tap (ky, kx) and A is the map read
-    // shifted by (pad - ky, pad - kx): the gather's ih = oh - pad + kh with kh = 2 pad - ky
-#pragma unroll
-    for (int j = 0; j < LA::NI; ++j) {
-      const int ky = blockIdx.z / P.ga.kw;
-      la.g0[j] = 2 * P.ga.pad - ky;
-      la.g2[j] = 2 * P.ga.pad - ((int)blockIdx.z - ky * P.ga.kw);
-    }
-  }
   using FA = FragAddr<BM, AKC, TM, BKT>;
   using FB = FragAddr<BN, BKC, TN, BKT>;
   static_assert(!F8 || (AKC && BKC && !GA && !GB), "fp8 operands: k-contiguous A and B, no implicit im2col");

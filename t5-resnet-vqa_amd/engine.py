@@ -146,7 +146,7 @@ class VQAEngine:
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, dropout=0.1, seed=0, pipeline=False,
                  t5_dw_group=None, defer_optimizer=True, dw_stream=None, sga_dw_batch=True, pair_bwd=True,
-                 language_model="t5-base", fp8=False, sga_attn_group=True, convt_tap_gather=True):
+                 language_model="t5-base", fp8=False, sga_attn_group=True):
         L.load()
         # pipeline: the frozen ResNet (no trainable input) of the NEXT batch runs on its own
         # stream beside this step's T5 / SGA / backward / optimizer (see train_step)
@@ -202,9 +202,6 @@ class VQAEngine:
         # the SGA blocks' self-attentions as ONE launch forward and ONE backward
         # (vqa_attn_desc.groups; False: one launch per block)
         self.sga_attn_group = bool(sga_attn_group)
-        # ConvTranspose2d dW: the GEMM gathers dVIS per tap in place (vqa_gemm a_conv = 3); False:
-        # the r03 form, 9 tap-shifted copies (vqa_tap_shift) + a batched GEMM (same bits)
-        self.convt_tap_gather = bool(convt_tap_gather)
         # AdamW of step k applied inside step k+1's forward (see _plan_optimizer)
         self.defer_opt = bool(defer_optimizer)
         # weight-gradient GEMMs (calls tagged `side`) on a stream of their own beside the
@@ -440,8 +437,7 @@ class VQAEngine:
         self.dO16 = t((T, D), BF16)
         self.dTXT = t((T, D))
         self.dVIS32, self.dVIS16 = t((V, D)), t((V, D), BF16)
-        if not self.convt_tap_gather:
-            self.dVIS9 = t((9, V, D), BF16)             # its 3x3 tap-shifted copies (scaler dW, r03 form)
+        self.dVIS9 = t((9, V, D), BF16)                 # its 3x3 tap-shifted copies (scaler dW)
         self.dH32 = t((T, D))
         self.dHM32 = t((T, D))
         self.dPB = t((self.h5, Lq, Lq), zero=True)
@@ -927,16 +923,10 @@ class VQAEngine:
         # dW[:, t*C:(t+1)*C] = shift_t(dVIS)^T @ F4 (vqa_tap_shift; no implicit im2col gather)
         self._bsplit = [len(b)]
         cin, fh = self.fc, self.fh
-        if self.convt_tap_gather:   # a_conv = 3: the GEMM reads dVIS shifted per tap in place (r04)
-            self._gemm(b, self.dVIS16, self.F4, D, cin, self.V_TOK, lda=D, ldb=cin, a_trans=True, b_trans=True,
-                       ga=ops.conv_geom(B, fh, fh, D, fh, fh, 3, 3, 1, 1), a_tap=True,
-                       c32=self.g32["scaler_w"], ldc32=9 * cin, batch=9, stride_a=0, stride_b=0,
-                       stride_c32=cin, keep=(self.G32,))
-        else:                       # r03: 9 materialised tap copies (vqa_tap_shift) + a batched GEMM
-            self._call(b, "vqa_tap_shift", self.dVIS16, self.dVIS9, B, fh, fh, D, 3, 3, 1)
-            self._gemm(b, self.dVIS9, self.F4, D, cin, self.V_TOK, lda=D, ldb=cin, a_trans=True, b_trans=True,
-                       c32=self.g32["scaler_w"], ldc32=9 * cin, batch=9, stride_a=self.V_TOK * D, stride_b=0,
-                       stride_c32=cin, keep=(self.G32,))
+        self._call(b, "vqa_tap_shift", self.dVIS16, self.dVIS9, B, fh, fh, D, 3, 3, 1)
+        self._gemm(b, self.dVIS9, self.F4, D, cin, self.V_TOK, lda=D, ldb=cin, a_trans=True, b_trans=True,
+                   c32=self.g32["scaler_w"], ldc32=9 * cin, batch=9, stride_a=self.V_TOK * D, stride_b=0,
+                   stride_c32=cin, keep=(self.G32,))
         self.scaler_dw_call = b[-1]                       # bench roofline_gemm: the step's largest launch
         self._call(b, "vqa_colsum", self.dVIS32, 0, self.V_TOK, D, D, self.g32["scaler_b"], 0.0, self.WS_COL2)
         mark("scaler_b")

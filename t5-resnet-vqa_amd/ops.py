@@ -30,10 +30,9 @@ def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None
               bias=None, res32=None, res16=None, ldres=0, mask16=None, ldmask=0, alpha=1.0, beta=0.0,
               relu=False, ga=None, gb=None, batch=1, stride_a=0, stride_b=0, stride_c32=0, stride_c16=0,
               stride_res=0, splitk=0, workspace=None, stride_bias=0, drop_site_stride=0, a_patch=False,
-              a_tap=False, fp8=False, scale_a=None, scale_b=None, stride_scale_a=0, stride_scale_b=0):
+              fp8=False, scale_a=None, scale_b=None, stride_scale_a=0, stride_scale_b=0):
     """fp8: a / b are e4m3 byte tensors (lda, ldb, k, strides in bytes = elements) with fp32 row
-    scales scale_a [m] / scale_b [n] (vqa_gemm_desc.fp8).  a_tap: a_conv = 3, the batch index is
-    the tap of the map `ga` that A reads shifted (the ConvTranspose2d weight gradient)."""
+    scales scale_a [m] / scale_b [n] (vqa_gemm_desc.fp8)."""
     op_t = torch.uint8 if fp8 else torch.bfloat16
     for t in (a, b):
         assert not isinstance(t, torch.Tensor) or t.dtype == op_t, f"{op_t} operand expected"
@@ -54,7 +53,7 @@ def gemm_desc(a, b, m, n, k, *, lda, ldb, a_trans=False, b_trans=False, c32=None
     d.mask16 = addr(mask16)
     d.ldmask = ldmask
     d.alpha, d.beta, d.relu = alpha, beta, int(relu)
-    d.a_conv = (3 if a_tap else 2 if a_patch else 1) if ga is not None else 0
+    d.a_conv = (2 if a_patch else 1) if ga is not None else 0
     if ga is not None:
         d.ga = ga
     d.b_conv = int(gb is not None)

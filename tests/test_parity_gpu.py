@@ -283,31 +283,6 @@ def test_deferred_optimizer_update_is_bit_identical(cuda, pkg):
             assert torch.equal(a, b)
 
 
-def test_convt_tap_gather_matches_tap_copies_bitwise(cuda, pkg):
-    """The ConvTranspose2d weight gradient read in place (vqa_gemm a_conv = 3, the default since
-    r04) and the r03 form (9 tap-shifted copies + a batched GEMM) give the same step bit for bit:
-    gradients, parameters and optimizer state over two train-mode steps."""
-    import torch
-    B, L, H = 4, 32, 64
-    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
-    batches = [pkg.synthetic.make_batch(B, L, H, seed=60 + i) for i in range(2)]
-    res = []
-    for gather in (True, False):
-        eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.1, seed=3,
-                                   convt_tap_gather=gather)
-        eng.capture()
-        for b in batches:
-            eng.load_batch(b)
-            eng.train_step()
-        g = eng.G32.clone()
-        eng.flush_optimizer()
-        torch.cuda.synchronize()
-        res.append((float(eng.LOSS.item()), g, eng.P32.clone(), eng.M.clone(), eng.VMAX.clone()))
-    assert res[0][0] == res[1][0]
-    for a, b in zip(res[0][1:], res[1][1:]):
-        assert torch.equal(a, b)
-
-
 def test_dw_stream_matches_single_stream_bitwise(cuda, pkg):
     """The default single-GPU step runs the side-tagged weight-gradient calls on a stream of
     their own (dw_stream); every bf16 gradient they read has a private buffer, so the
