@@ -248,6 +248,8 @@ def main():
     ap.add_argument("--dp", action="store_true",
                     help="N = 1: run the N > 1 step (dp.DataParallelStep over a world-1 RCCL group, the DP engine's "
                          "weight-gradient groups) instead of the single-GPU engine graph")
+    ap.add_argument("--dp-res-split", type=float, default=None,
+                    help="DP, pipelined: share of the next batch's ResNet calls beside the forward graph (dp.RES_SPLIT)")
     ap.add_argument("--dp-groups", action="store_true",
                     help="the single-GPU engine step with the DP engine's T5 weight-gradient groups (A/B of --dp)")
     ap.add_argument("--rehearse", action="store_true",
@@ -328,7 +330,8 @@ def main():
     eng.backward()
     eng.autotune(table=args.tune_table, save=args.tune_save if rank == 0 else None)   # tile choice: speed only
     if use_dp:
-        dps = pkg.dp.DataParallelStep(eng, use_graph=not args.no_graph, shard_optimizer=args.shard_optimizer)
+        dps = pkg.dp.DataParallelStep(eng, use_graph=not args.no_graph, shard_optimizer=args.shard_optimizer,
+                                      **({} if args.dp_res_split is None else {"res_split": args.dp_res_split}))
         run_step = dps.step
     else:
         if not args.no_graph:

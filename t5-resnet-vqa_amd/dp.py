@@ -150,6 +150,11 @@ def gather_rows(ids, rows, out_ids, out_rows, group=None):
     return [w1, w2]
 
 
+# share of the next batch's frozen-ResNet calls forked beside the forward graph (pipelined
+# engines; the rest go beside the first backward stage), DataParallelStep(res_split=...)
+RES_SPLIT = 1.0
+
+
 def plan_stages(segments, scaler, dw_stream=True):
     """The DP backward's stages (DataParallelStep._plan_schedule).  segments: the backward's
     calls cut at the bucket marks (bucket k final after segment k's calls); scaler: the
@@ -195,7 +200,7 @@ def plan_stages(segments, scaler, dw_stream=True):
 
 
 class DataParallelStep:
-    def __init__(self, engine, group=None, bucket_mb=24, use_graph=True, shard_optimizer=False):
+    def __init__(self, engine, group=None, bucket_mb=24, use_graph=True, shard_optimizer=False, res_split=RES_SPLIT):
         import torch.distributed as dist
         self.eng, self.group = engine, group
         self.world = dist.get_world_size(group)
@@ -229,6 +234,15 @@ class DataParallelStep:
         if self.shard:
             self._plan_sharded_optimizer()
         self._plan_schedule()
+        # pipelined engines: the next batch's frozen ResNet (IMG -> F4N, read by the next step's
+        # copy_f4 only) runs INSIDE the step's graphs, as on one GPU: its first `res_split` of the
+        # calls forked beside the forward, the rest beside the first backward stage.  (Replayed as a
+        # graph of its own on its stream it shared a hardware queue with the stage graphs' kernels,
+        # one ResNet kernel holding back the chain kernels queued behind it.)
+        r1 = int(round(len(e.res_calls) * float(res_split))) if e.pipeline else 0
+        self._res_a = list(e.res_calls[:r1]) if e.pipeline else []
+        if e.pipeline and r1 < len(e.res_calls):
+            self.stages[0]["ops"].insert(0, ("res", list(e.res_calls[r1:])))
         self.graphs = None
         # exposed-communication timing (bench at N > 1): HIP events on the compute stream right
         # before and after each collective's wait, i.e. how long the step's stream stalls on it
@@ -397,7 +411,7 @@ class DataParallelStep:
     def stage_plan(self):
         """Per stage: its calls in order as ("chain" | "dw_fork", count), and the buckets final
         after it."""
-        return [{"ops": [("chain" if kd == "main" else "dw_fork", len(c)) for kd, c in st["ops"]],
+        return [{"ops": [({"main": "chain", "fork": "dw_fork", "res": "resnet_fork"}[kd], len(c)) for kd, c in st["ops"]],
                  "final_buckets": st["final"]} for st in self.stages]
 
     def _run_stage(self, st):
@@ -406,17 +420,18 @@ class DataParallelStep:
         at the end of the stage."""
         e = self.eng
         main = torch.cuda.current_stream(e.dev)
-        forked = False
+        forked = set()
         for kind, calls in st["ops"]:
             if kind == "main":
                 self._run(calls)
-            else:
-                _after(e._wside, main)
-                with torch.cuda.stream(e._wside):
+            else:                                           # "fork": pending dW; "res": the next batch's ResNet
+                side = e._wside if kind == "fork" else e._rstream
+                _after(side, main)
+                with torch.cuda.stream(side):
                     self._run(calls)
-                forked = True
-        if forked:
-            _after(main, e._wside)
+                forked.add(side)
+        for side in forked:
+            _after(main, side)
 
     def _backward_exchange(self):
         """The staged backward with the exchange issued between the stages; the step's stream
@@ -508,45 +523,38 @@ class DataParallelStep:
             with torch.cuda.graph(g, stream=s):
                 fn()
             gs[name] = g
-        cap("fwd", e.run_forward_streams)                   # forward: ResNet || T5 encoder on two streams
-        if e.pipeline:                                      # the next batch's ResNet, replayed beside the step
-            cap("res", lambda: self._run(e.res_calls))
+        cap("fwd", self._fwd)
         for j, st in enumerate(self.stages):
             cap(f"stage{j}", lambda st=st: self._run_stage(st))
         cap("finish", lambda: self._run(self.finish_calls))
         return gs
 
-    def _res_begin(self):
-        """Pipelined engines: F4 <- F4N, then the next batch's frozen ResNet on its own
-        stream (graph or eager), overlapping this whole step; _res_end joins it."""
+    def _fwd(self):
+        """The forward (ConvTranspose2d || T5 encoder, then SGA; engine.run_forward_streams) with,
+        when pipelined, the first part of the next batch's frozen ResNet forked beside it on
+        `_rstream` -- captured first, as the single-GPU step graph captures it -- and joined at
+        its end."""
         e = self.eng
-        if not e.pipeline:
-            return
         main = torch.cuda.current_stream(e.dev)
-        e.copy_f4(L.stream_handle(main))
-        _after(e._rstream, main)
-        with torch.cuda.stream(e._rstream):
-            if self.graphs is not None:
-                self.graphs["res"].replay()
-            else:
-                self._run(e.res_calls)
-
-    def _res_end(self):
-        e = self.eng
-        if e.pipeline:
-            _after(torch.cuda.current_stream(e.dev), e._rstream)
+        if self._res_a:
+            _after(e._rstream, main)
+            with torch.cuda.stream(e._rstream):
+                self._run(self._res_a)
+        e.run_forward_streams()
+        if self._res_a:
+            _after(main, e._rstream)
 
     def step(self):
         e = self.eng
-        self._res_begin()
+        if e.pipeline:                                      # F4 <- F4N: this batch's features (last step's ResNet)
+            e.copy_f4(L.stream_handle(torch.cuda.current_stream(e.dev)))
         if self.graphs is not None:
             self.graphs["fwd"].replay()
         else:
-            e.forward()
+            self._fwd()
         tev = self._backward_exchange()
         if self.shard:
             self._sharded_optimizer()
-        self._res_end()
         if self.timing:
             self._ev.append(tev)
 

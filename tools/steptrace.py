@@ -1,6 +1,6 @@
 """One step of a rocprofv3 kernel trace (sqlite .db of ROCm 7.x), kernel by kernel.
 
-  python tools/steptrace.py gpurun_out/X/run_results.db [marker] [--list]
+  python tools/steptrace.py gpurun_out/X/run_results.db [marker] [--list] [--back N]
 
 Finds the last complete step (between two launches whose name contains
 `marker`, default rng_advance), prints the step wall time, per-queue busy
@@ -11,6 +11,7 @@ import sys
 
 db = sys.argv[1]
 marker = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else "rng_advance"
+# --back N: the N-th complete step from the end (default 2; bench --dp appends 3 timing steps)
 c = sqlite3.connect(db)
 rows = c.execute("select start, end, name, queue_id, stream_id from kernels order by start").fetchall()
 
@@ -21,7 +22,8 @@ def short(n):
 
 
 idx = [i for i, r in enumerate(rows) if marker in r[2]]
-a, b = idx[-3], idx[-2]
+back = int(sys.argv[sys.argv.index("--back") + 1]) if "--back" in sys.argv else 2   # which step from the end
+a, b = idx[-1 - back], idx[-back]
 win = rows[a:b]
 t0, t1 = win[0][0], rows[b][0]
 print(f"step wall {(t1 - t0) / 1e3:.1f} us, {len(win)} kernels")
