@@ -140,6 +140,7 @@ def bench_vit(args, pkg, dev):
     for i in range(args.steps):
         step(i)
     ev1.record(stream)
+    t_issue = time.perf_counter() - t0             # host time to issue the K steps (< dt: the host ran ahead)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     gpu_step = ev0.elapsed_time(ev1) * 1e-3 / args.steps
@@ -364,6 +365,7 @@ def main():
     for i in range(args.steps):
         step(i)
     ev1.record(stream)
+    t_issue = time.perf_counter() - t0             # host time to issue the K steps (< dt: the host ran ahead)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -439,6 +441,7 @@ def main():
            if args.rehearse else {}),
         "roofline": roofline,
         "loss": round(loss, 5), "grad_norm": round(gnorm, 4),
+        "host_issue_ms_per_step": round(t_issue * 1e3 / args.steps, 3),
     }
     if use_dp:                             # collective completion + exposed wait (HIP events), on 3
         dps.timing = True                  # steps after the timed region (its waits would perturb it)
