@@ -1355,9 +1355,9 @@ class VQAEngine:
         """Run `calls` in order on `main`, except runs of side-tagged calls (weight
         gradients), which go to `wside` after an event on `main` at that point
         (`dw_stream`, on by default): the batched T5 dW launches trail the input-gradient chain
-        (6.66 vs 6.78-6.84 ms per step).  dp.DataParallelStep replays each backward segment's
-        side-tagged calls as their own graph on the same stream, the segment's gradient bucket
-        all-reduced behind them (so a bucket is final when its collective starts).  Every
+        (6.66 vs 6.78-6.84 ms per step).  dp.DataParallelStep keeps this placement across its
+        stage graphs (dp.plan_stages: a segment's side-tagged calls forked beside the next
+        chain segment, its gradient bucket all-reduced once that stage has ended).  Every
         bf16 gradient a side-tagged call reads has its own buffer (_gbuf), so no later chain
         call overwrites it (tests: test_dw_stream_matches_single_stream_bitwise)."""
         if not self.dw_stream:
