@@ -88,7 +88,19 @@ void run(const char* tag, int M, int N, int K, bool res, int splitk = 0) {
   if (ws) CK(hipFree(ws));
 }
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1) {                                       // r04: wave / stage variants on the 2048-row shape
+    run<64, 64, 2, 2, 2, 128>("o", 2048, 768, 768, true);
+    run<64, 64, 3, 2, 2, 128>("o", 2048, 768, 768, true);
+    run<64, 64, 2, 1, 1, 128>("o", 2048, 768, 768, true);
+    run<64, 64, 2, 2, 1, 128>("o", 2048, 768, 768, true);
+    run<128, 64, 2, 4, 2>("o", 2048, 768, 768, true);
+    run<64, 128, 2, 2, 4, 128>("o", 2048, 768, 768, true);
+    run<64, 64, 2, 1, 1, 128>("qkv", 2048, 2304, 768, false);
+    run<64, 128, 2, 2, 2, 128>("qkv", 2048, 2304, 768, false);
+    run<64, 128, 2, 2, 4, 128>("qkv", 2048, 2304, 768, false);
+    return 0;
+  }
   run<64, 64, 2>("o", 2048, 768, 768, true);
   run<64, 64, 2, 2, 2, 128>("o", 2048, 768, 768, true);
   run<128, 64, 2, 2, 2, 128>("o", 2048, 768, 768, true);
