@@ -381,7 +381,7 @@ def main():
     pairs = world * B * args.steps
     value = pairs / dt
     survey_cfg = (args.image_size, args.seq_len, NB) == (224, 32, 3) and not args.config5
-    c5_cfg = args.config5 and (B, args.seq_len) == (64, 32)
+    c5_cfg = args.config5 and (B, args.seq_len, args.image_size, NB) == (64, 32, 384, 6)
     pfile = PMC_FILE if survey_cfg else PMC_FILE_C5
     pmc, pmc_note = {}, f"profiles/{pfile} absent"
     pmc_path = os.path.join(ROOT, "profiles", pfile)
@@ -392,6 +392,9 @@ def main():
         pmc = json.load(open(pmc_path))
         if args.no_pipeline or args.no_graph:
             pmc, pmc_note = {}, f"profiles/{pfile} was measured on the pipelined graph step: not quoted"
+        elif use_dp or args.dp_groups:                     # other stage graphs / T5 weight-gradient groups
+            pmc, pmc_note = {}, (f"profiles/{pfile} was measured on the single-GPU engine step, not on the "
+                                 "DataParallelStep schedule: not quoted")
         elif pmc.get("tree_digest") != tree_digest():      # counters of another tree: not quoted
             pmc, pmc_note = {}, f"profiles/{pfile} was measured on another tree (digest mismatch): not quoted"
         else:
@@ -412,8 +415,13 @@ def main():
     f8 = calls_flop(eng, fp8_only=True)
     peak = MFMA_PEAK_TFLOPS if f8 == 0 else calls_flop(eng) / (f8 / FP8_PEAK_TFLOPS + (calls_flop(eng) - f8) /
                                                                MFMA_PEAK_TFLOPS)
-    replay = ("DataParallelStep: forward graph, 4 backward stage graphs with the RCCL exchange between them, "
-              "finish graph" if use_dp else "one hipGraph replay")
+    if use_dp:
+        replay = (f"DataParallelStep: forward graph, {len(dps.stages)} backward stage graphs with the "
+                  f"{dist.get_backend()} exchange between them, finish graph")
+        if args.no_graph:
+            replay = f"DataParallelStep, eager: forward, {len(dps.stages)} backward stages, exchange, finish"
+    else:
+        replay = "eager stream launches (--no-graph)" if args.no_graph else "one hipGraph replay"
     roofline = {"bound": "mfma", "kernel": f"whole train step ({replay}: ResNet50 fwd, ConvT, {lm}, {NB}xSGA, "
                                            "head, backward, clip, AdamW)",
                 "achieved": round(step_tflops, 1), "peak": round(peak, 1), "unit": "TFLOP/s",

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 16
+#define VQA_ABI_VERSION 17
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -362,7 +362,11 @@ int vqa_xattn1_bwd(const void* dctx, long long ldd, float* dv32, void* dv16, lon
 /* ------------------------------------------------------------------ head ---
  * AttentionPooler (resnet_vqa_model.py:14-26) + classification_layer +
  * log_softmax + NLLLoss mean (:152-160).  fp32.  targets may be NULL in
- * forward (loss is then not computed, like annotation_ids=None).
+ * forward (loss is then not computed, like annotation_ids=None).  A negative
+ * target marks an ignored row, as nn.NLLLoss's ignore_index = -100: nll 0, no
+ * gradient, and the mean runs over the rows with a target >= 0 (the engines pad a
+ * loader's short final batch this way; ABI 17).  No valid row: loss = NaN (0/0),
+ * as in torch.
  * Limits: seq <= 64, d <= 1024 (d % 4 == 0; 1024 = T5-large), batch <= 1024, answers <= 1024.
  * The forward writes the logits through logp.
  * ws = vqa_head_workspace_floats(batch, seq, d, answers) floats. */

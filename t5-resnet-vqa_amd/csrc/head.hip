@@ -25,9 +25,10 @@ constexpr int MAXA = 1024;
 // Forward, three launches (resnet_vqa_model.py:152-160):
 //   head_pool_fwd      one workgroup per sample: scores, softmax over L, pooled row
 //   head_logits        (8 answers) x (16 samples) per workgroup: logits = pooled Wc^T + bc
-//   head_lse           one workgroup: log_softmax over the answers, NLL, mean loss
+//   head_lse           one workgroup: log_softmax over the answers, NLL, mean loss over the B' rows
+//                      whose target is >= 0 (nn.NLLLoss ignore_index: a short final batch padded to B)
 // Backward, three launches:
-//   head_dpooled       dlogits = (softmax - onehot)/B and dpooled = dlogits Wc, 64 columns x
+//   head_dpooled       dlogits = (softmax - onehot)/B' and dpooled = dlogits Wc, 64 columns x
 //                      16 samples per workgroup, the answer sum split over the 4 waves
 //   head_pool_bwd      one workgroup per sample: pooler backward -> dx, and the sample's
 //                      pooler-weight partial sum_l dscore_l x_l (the thread owns its columns)
@@ -161,6 +162,7 @@ __global__ __launch_bounds__(1024) void head_lse_kernel(float* __restrict__ lp, 
                                                         float* __restrict__ nll, float* __restrict__ loss, int B,
                                                         int A) {
   __shared__ float nl[1024];
+  __shared__ int nv[1024];                             // row b has a target >= 0 (not ignored)
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
   for (int b0 = wv * 4; b0 < B; b0 += 64) {            // 4 samples per wave and pass, all loads first
     float v[4][NI];
@@ -191,7 +193,12 @@ __global__ __launch_bounds__(1024) void head_lse_kernel(float* __restrict__ lp, 
 #pragma unroll
         for (int i = 0; i < NI; ++i)
           if (l + 64 * i < A) lp[(long)b * A + l + 64 * i] = v[q][i] - lse;
-        if (tgt && l == 0) { nl[b & 1023] = -(vt - lse); nll[b] = -(vt - lse); }
+        if (tgt && l == 0) {                            // ignore_index rows: nll 0, not in the mean
+          const float v = t[q] >= 0 ? -(vt - lse) : 0.f;
+          nl[b & 1023] = v;
+          nv[b & 1023] = t[q] >= 0;
+          nll[b] = v;
+        }
       }
     }
   }
@@ -199,8 +206,9 @@ __global__ __launch_bounds__(1024) void head_lse_kernel(float* __restrict__ lp, 
   __syncthreads();
   if (threadIdx.x == 0) {                             // fixed-order mean (NLLLoss reduction='mean')
     float s = 0.f;
-    for (int b = 0; b < B; ++b) s += nl[b];
-    loss[0] = s / (float)B;
+    int n = 0;
+    for (int b = 0; b < B; ++b) { s += nl[b]; n += nv[b]; }
+    loss[0] = s / (float)n;                           // n = B for a full batch: s / B as before
   }
 }
 
@@ -214,14 +222,18 @@ template <bool CHUNKED>                               // false: A <= 192, one ch
 __global__ __launch_bounds__(256) void head_dpooled_kernel(const float* __restrict__ lp,
                                                            const long long* __restrict__ tgt,
                                                            const float* __restrict__ wc, float* __restrict__ dl_out,
-                                                           float* __restrict__ dpooled, int B, int D, int A,
-                                                           float inv_b) {
+                                                           float* __restrict__ dpooled, int B, int D, int A) {
   constexpr int AP = 4 * DP_AQ;                       // padded answer row in LDS
   __shared__ __attribute__((aligned(16))) float dl[16][AP];
   __shared__ float red[4][16][64];
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const int c = blockIdx.x * 64 + l, s0 = blockIdx.y * 16;
   constexpr int FI = 16 * AP / 256;                   // fill elements per thread (all loads first)
+  // the NLL mean's divisor: rows with a target >= 0 (ignore_index rows get no gradient); a full
+  // batch gives 1 / B exactly as the host-computed factor did
+  int nvalid = 0;
+  for (int b0 = 0; b0 < B; b0 += 256) nvalid += __syncthreads_count(b0 + tid < B && tgt[min(b0 + tid, B - 1)] >= 0);
+  const float inv_b = 1.0f / (float)nvalid;
   float acc[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc[q] = 0.f;
@@ -238,7 +250,7 @@ __global__ __launch_bounds__(256) void head_dpooled_kernel(const float* __restri
 #pragma unroll
     for (int k = 0; k < FI; ++k) {
       const int i = tid + 256 * k, q = i / AP, j = i - q * AP, a = c0 + j, b = s0 + q;
-      const float g = (b < B && a < A) ? (__expf(ev[k]) - (a == tv[k] ? 1.f : 0.f)) * inv_b : 0.f;
+      const float g = (b < B && a < A && tv[k] >= 0) ? (__expf(ev[k]) - (a == tv[k] ? 1.f : 0.f)) * inv_b : 0.f;
       dl[q][j] = g;
       if (blockIdx.x == 0 && b < B && a < A) dl_out[(long)b * A + a] = g;
     }
@@ -484,11 +496,9 @@ extern "C" int vqa_head_bwd(const float* x, const float* att, const float* poole
   float* part = dpool + batch * d;
   const dim3 dg(vqa::cdiv(d, 64), vqa::cdiv(batch, 16));
   if (answers <= 4 * DP_AQ)
-    hipLaunchKernelGGL(head_dpooled_kernel<false>, dg, dim3(256), 0, s, logp, targets, wc, dl, dpool, batch, d, answers,
-                       1.0f / batch);
+    hipLaunchKernelGGL(head_dpooled_kernel<false>, dg, dim3(256), 0, s, logp, targets, wc, dl, dpool, batch, d, answers);
   else
-    hipLaunchKernelGGL(head_dpooled_kernel<true>, dg, dim3(256), 0, s, logp, targets, wc, dl, dpool, batch, d, answers,
-                       1.0f / batch);
+    hipLaunchKernelGGL(head_dpooled_kernel<true>, dg, dim3(256), 0, s, logp, targets, wc, dl, dpool, batch, d, answers);
   int rc = vqa::check_launch("vqa_head_bwd/dpooled");
   if (rc) return rc;
   rc = with_lmax(seq, [&](auto lm) {

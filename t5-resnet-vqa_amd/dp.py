@@ -83,14 +83,23 @@ def _after(stream, other):
     stream.wait_event(ev)
 
 
+def _wait_only(w):
+    """The current stream waits for the collective of `w` alone -- never its follow-up copy
+    (_Then): the timing stream only observes completions, it must not write anything."""
+    return w.wait_only() if hasattr(w, "wait_only") else w.wait()
+
+
 class _Done:
     """A completed collective (host-staged gloo path): wait() is a no-op."""
     def wait(self):
         return True
 
+    wait_only = wait
+
 
 class _Then:
-    """A collective followed by a device copy on the waiting stream (issued at wait())."""
+    """A collective followed by a device copy on the waiting stream (issued at wait(), once: the
+    step's stream calls wait(); bench.py's timing stream calls wait_only())."""
     def __init__(self, work, then):
         self.work, self.then = work, then
 
@@ -98,6 +107,9 @@ class _Then:
         self.work.wait()
         self.then()
         return True
+
+    def wait_only(self):
+        return self.work.wait()
 
 
 class _All:
@@ -108,6 +120,11 @@ class _All:
     def wait(self):
         for w in self.works:
             w.wait()
+        return True
+
+    def wait_only(self):
+        for w in self.works:
+            _wait_only(w)
         return True
 
 
@@ -450,9 +467,9 @@ class DataParallelStep:
 
         def mark_done(key, ws):
             if tm is not None:                              # completion seen from a timing-only stream
-                with torch.cuda.stream(self._tstream):
+                with torch.cuda.stream(self._tstream):      # (waits only: the copies stay on the step's stream)
                     for w in ws:
-                        w.wait()
+                        _wait_only(w)
                     tm["done"][key] = torch.cuda.Event(enable_timing=True)
                     tm["done"][key].record(self._tstream)
         for j, st in enumerate(self.stages):

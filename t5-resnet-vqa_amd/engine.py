@@ -141,6 +141,39 @@ def _h2d(dst, src):
     dst.copy_(src, non_blocking=src.is_cuda or src.is_pinned())
 
 
+IGNORE_INDEX = -100          # nn.NLLLoss's default ignore_index: the head skips rows with a target < 0
+
+
+def batch_rows(batch, key, planned):
+    """Rows of a collate batch (the reference's loaders have no drop_last, so an epoch's last
+    batch is short: faster_rcnn_vqa_trainer.py:172-197); 1 <= rows <= the planned batch."""
+    n = int(torch.as_tensor(batch[key]).shape[0])
+    if not 1 <= n <= planned:
+        raise ValueError(f"{key}: batch of {n} rows; this engine is planned for 1..{planned} rows")
+    return n
+
+
+def load_rows(dst, src, n, fill=None):
+    """dst[:n] <- src (n rows); the planned rows past n are padding: copies of rows 0..n-1
+    (real samples, so every activation stays finite) or `fill` (targets: IGNORE_INDEX, so the
+    padded rows add nothing to the loss or to any gradient -- the NLL mean runs over the n
+    real rows)."""
+    if src is None:
+        return
+    B = dst.shape[0]
+    _h2d(dst[:n] if n < B else dst, src)
+    if n == B:
+        return
+    if fill is not None:
+        dst[n:].fill_(fill)
+        return
+    i = n
+    while i < B:                                   # doubling copies of the real rows
+        k = min(i, B - i)
+        dst[i:i + k].copy_(dst[:k])
+        i += k
+
+
 class VQAEngine:
     def __init__(self, state_dict, vision="resnet50", batch=64, seq_len=32, image_size=224, device="cuda:0",
                  warmup=10, total=100, num_blocks=3, answer_spaces=170, grad_scale=1.0, max_norm=1.0,
@@ -187,7 +220,6 @@ class VQAEngine:
         # 6.78-6.84 ms per step against one group of 12 on the chain; tools/gpu/ab_env.sh).
         # DP passes (4, 4, 3, 1): the buckets become final, and are all-reduced, while the
         # backward runs, and the last, exposed bucket is one layer.
-        self._default_dw = t5_dw_group is None
         if t5_dw_group is None:
             t5_dw_group = (3 * self.nl // 4, self.nl - 3 * self.nl // 4)
         if isinstance(t5_dw_group, (list, tuple)):
@@ -208,6 +240,7 @@ class VQAEngine:
         # input-gradient chain (single GPU and DP alike; dp.DataParallelStep keeps the placement)
         self.dw_stream = True if dw_stream is None else bool(dw_stream)
         self.T = batch * seq_len
+        self.rows = batch                 # real rows of the loaded batch (a short last batch is padded)
         self.lay = ParamLayout(vision, answer_spaces, num_blocks, dm)
         sd = {k: np.asarray(v) for k, v in state_dict.items()}
         self._frozen = {k: v for k, v in sd.items() if k not in set(self.lay.trainable_keys)}
@@ -1178,19 +1211,21 @@ class VQAEngine:
         Pipelined engines take the batch's text and targets, and `next_images` = the image
         tensors of the batch that the FOLLOWING step trains on (this batch's images went
         in one step earlier, or through prime())."""
-        def cp(dst, src):
-            if src is not None:
-                _h2d(dst, src)
-        cp(self.IMG, next_images if self.pipeline else batch["image_tensors"])
-        cp(self.IDS, batch["question_input_ids"])
-        cp(self.MASK, batch["question_attention_masks"])
-        cp(self.TGT, batch.get("annotation_ids"))
+        n = self.rows = batch_rows(batch, "question_input_ids", self.B)
+        if self.pipeline:
+            if next_images is not None:
+                load_rows(self.IMG, next_images, batch_rows({"image_tensors": next_images}, "image_tensors", self.B))
+        else:
+            load_rows(self.IMG, batch["image_tensors"], n)
+        load_rows(self.IDS, batch["question_input_ids"], n)
+        load_rows(self.MASK, batch["question_attention_masks"], n)
+        load_rows(self.TGT, batch.get("annotation_ids"), n, fill=IGNORE_INDEX)
 
     def prime(self, images):
         """Pipelined engines: compute the layer4 features of the first batch's images, so
         that the first train_step has them (later steps produce their successor's)."""
         assert self.pipeline, "prime() is for pipelined engines"
-        _h2d(self.IMG, images)
+        load_rows(self.IMG, images, batch_rows({"image_tensors": images}, "image_tensors", self.B))
         self._run(self.res_calls)
 
     def forward(self):
@@ -1601,10 +1636,10 @@ class VQAEngine:
         self.forward()
         self.backward()
         torch.cuda.synchronize(self.dev)
-        return self.LOGP.cpu().numpy(), float(self.LOSS.item())
+        return self.LOGP[:self.rows].cpu().numpy(), float(self.LOSS.item())
 
     def log_probs(self):
-        return self.LOGP
+        return self.LOGP[:self.rows]
 
     def loss(self):
         return self.LOSS
@@ -1689,4 +1724,4 @@ class VQAEngine:
     def layer4_features(self):
         """The frozen ResNet's layer4 map of the current batch as NCHW fp32 (the kernels keep
         it NHWC bf16): the `features` generate_answers returns (resnet_vqa_model.py:186-203)."""
-        return self.F4.permute(0, 3, 1, 2).float()
+        return self.F4[:self.rows].permute(0, 3, 1, 2).float()

@@ -7,9 +7,13 @@ value `(log_probs [B, answer_spaces], loss or None)`, the same state-dict keys
 (`vision_model_name`, `device`).  What differs, by design:
 
 * shapes are planned once: `batch_size`, `seq_len` and `image_size` are fixed
-  at construction (the hipGraph step has static buffers); a batch of another
-  shape raises ValueError (use drop_last=True loaders, as the step is
-  per-batch anyway);
+  at construction (the hipGraph step has static buffers).  A batch of FEWER rows
+  -- the short last batch of the reference's loaders, which have no drop_last
+  (faster_rcnn_vqa_trainer.py:172-197) -- is padded to the planned batch with
+  copies of its own rows whose targets are ignore_index: the loss is the mean
+  over the real rows and the padding gets no gradient, so the step equals the
+  reference's step on the short batch; log-probs come back for the real rows.
+  More rows, or another question length / image size, raise ValueError;
 * weights come from a reference `state_dict` (e.g. `torch.load(best-model.pt,
   weights_only=True)`) or, offline, from the deterministic synthetic init —
   `from_pretrained` downloads are not available here;
@@ -148,8 +152,11 @@ class ResnetVQAModel:
 
     # ------------------------------------------------------------------ forward
     def _check_batch(self, question_input_ids, image_tensors):
-        want_q = (self.batch_size, self.seq_len)
-        want_i = (self.batch_size, 3, self.image_size, self.image_size)
+        n = int(question_input_ids.shape[0])
+        if not 1 <= n <= self.batch_size:
+            raise ValueError(f"batch of {n} rows: the model is planned for 1..{self.batch_size} rows")
+        want_q = (n, self.seq_len)
+        want_i = (n, 3, self.image_size, self.image_size)
         if tuple(question_input_ids.shape) != want_q:
             raise ValueError(f"question_input_ids shape {tuple(question_input_ids.shape)} != planned {want_q}")
         if tuple(image_tensors.shape) != want_i:
@@ -176,7 +183,7 @@ class ResnetVQAModel:
             raise TypeError("forward() needs question_attention_masks and image_tensors")
         self.load_batch(question_input_ids, question_attention_masks, image_tensors, annotation_ids)
         self.engine.forward()
-        log_probs = self.engine.LOGP.clone()
+        log_probs = self.engine.LOGP[:self.engine.rows].clone()
         loss = self.engine.LOSS[0].clone() if annotation_ids is not None else None
         return log_probs, loss
 
@@ -299,9 +306,13 @@ class VitVQAModel:
 
     def load_items(self, items):
         """The ViT collate's batch dict (dataset_utils/vit_vqa_daquar_dataset.py:168-195)."""
-        want = {"pixel_values": (self.batch_size, 3, self.image_size, self.image_size),
-                "question_input_ids": (self.batch_size, self.seq_len),
-                "decoder_question_input_ids": (self.batch_size, self.dec_len)}
+        q = items.get("question_input_ids")
+        n = int(q.shape[0]) if q is not None else 0
+        if not 1 <= n <= self.batch_size:                 # a short last batch is padded (ResnetVQAModel)
+            raise ValueError(f"batch of {n} rows: the model is planned for 1..{self.batch_size} rows")
+        want = {"pixel_values": (n, 3, self.image_size, self.image_size),
+                "question_input_ids": (n, self.seq_len),
+                "decoder_question_input_ids": (n, self.dec_len)}
         for k, shape in want.items():
             if items.get(k) is None or tuple(items[k].shape) != shape:
                 raise ValueError(f"{k}: expected shape {shape}")
@@ -316,7 +327,8 @@ class VitVQAModel:
                          "decoder_question_attention_masks": decoder_question_attention_masks,
                          "pixel_values": pixel_values, "annotation_ids": annotation_ids})
         self.engine.forward()
-        return self.engine.LOGP.clone(), (self.engine.LOSS[0].clone() if annotation_ids is not None else None)
+        e = self.engine
+        return e.LOGP[:e.rows].clone(), (e.LOSS[0].clone() if annotation_ids is not None else None)
 
     __call__ = forward
 
@@ -334,7 +346,7 @@ class VitVQAModel:
                          "pixel_values": pixel_values, "annotation_ids": annotation_ids})
         atts = e.forward_with_attentions()
         loss = e.LOSS[0].clone() if annotation_ids is not None else None
-        return e.LOGP.clone(), loss, tuple(a.clone() for a in atts)
+        return e.LOGP[:e.rows].clone(), loss, tuple(a[:e.rows].clone() for a in atts)
 
     @staticmethod
     def convert_logits_to_predictions(lm_logits):

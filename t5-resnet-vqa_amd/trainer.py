@@ -111,7 +111,7 @@ class VQATrainer:
                 e.capture()
             e.train_step()
         loss = float(e.LOSS.item()) if sync else e.LOSS[0]
-        return loss, e.LOGP
+        return loss, e.LOGP[:e.rows]
 
     @torch.no_grad()
     def valid_one_step(self, data_items):
@@ -177,10 +177,16 @@ class VQATrainer:
     # checkpoint written here loads into the reference's optimizer and back.
     def _param_groups(self):
         m = self.model
-        if not hasattr(m.engine, "optimizer_state"):
-            raise NotImplementedError("optimizer / scheduler checkpoints are implemented for ResnetVQAModel; the "
-                                      "ViT model (vit_vqa_trainer.py:300-323) checkpoints its weights only here "
-                                      "(model.state_dict())")
+        if hasattr(m, "trainer_group_lr"):
+            # VitVQAModel: the ViT trainer's four groups (vit_vqa_trainer.py:298-316), parameters in
+            # module order with the tied embedding once (lang_model.parameters() de-duplicates it)
+            from . import vit_model as VM
+            specs = [k for k in VM.model_specs(m.answer_spaces, m.image_size) if k not in VM.TIED]
+            names = [("vision_model", "Vision Model", self.vision_lr),
+                     ("lang_model", "Language Model", self.group_lr["lang_model"]),
+                     ("fusing_layer", "Fusion Layer", self.group_lr["fusing_layer"]),
+                     ("classification_layer", "Classifier Layer", self.group_lr["classification_layer"])]
+            return [(label, lr, [k for k in specs if k.split(".", 1)[0] == top]) for top, label, lr in names]
         scaler = "downscale_layer" if m.vision_model_name == "resnet50" else "upscale_layer"
         names = [("vision_model", "Vision Model"), ("lang_model", "Language Model"),
                  (scaler, "DownScaler Layer" if scaler == "downscale_layer" else "UpScaler Layer"),

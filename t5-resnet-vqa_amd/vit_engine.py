@@ -38,7 +38,8 @@ from . import lib as L
 from . import ops
 from . import synthetic as S
 from . import vit_model as VM
-from .engine import BF16, F32, I64, SITE_EMBED, SITE_FINAL, VQAEngine, _h2d, no_gc_capture, t5_site
+from .engine import (BF16, F32, I64, IGNORE_INDEX, SITE_EMBED, SITE_FINAL, VQAEngine, batch_rows, load_rows,
+                     no_gc_capture, t5_site)
 from .layout import t5_bucket_map
 
 D = S.D_MODEL
@@ -84,6 +85,7 @@ class VitVQAEngine:
         self.dev = torch.device(device)
         self.B, self.L, self.Ld, self.H = batch, seq_len, dec_len, image_size
         self.T, self.TD = batch * seq_len, batch * dec_len
+        self.rows = batch                 # real rows of the loaded batch (a short last batch is padded)
         self.NV = VM.vit_tokens(image_size)
         self.TV = batch * self.NV
         self.A = answer_spaces
@@ -522,13 +524,13 @@ class VitVQAEngine:
     def load_batch(self, batch):
         """The ViT collate's batch dict (pixel_values, question / decoder ids and masks,
         annotation_ids), numpy or torch, host or device."""
-        _h2d(self.PIX, batch["pixel_values"])
-        _h2d(self.IDS, batch["question_input_ids"])
-        _h2d(self.MASK, batch["question_attention_masks"])
-        _h2d(self.DIDS, batch["decoder_question_input_ids"])
-        _h2d(self.DMASK, batch["decoder_question_attention_masks"])
-        if batch.get("annotation_ids") is not None:
-            _h2d(self.TGT, batch["annotation_ids"])
+        n = self.rows = batch_rows(batch, "question_input_ids", self.B)
+        load_rows(self.PIX, batch["pixel_values"], n)
+        load_rows(self.IDS, batch["question_input_ids"], n)
+        load_rows(self.MASK, batch["question_attention_masks"], n)
+        load_rows(self.DIDS, batch["decoder_question_input_ids"], n)
+        load_rows(self.DMASK, batch["decoder_question_attention_masks"], n)
+        load_rows(self.TGT, batch.get("annotation_ids"), n, fill=IGNORE_INDEX)
 
     def forward(self):
         self._run(self.fwd_calls)
@@ -597,7 +599,7 @@ class VitVQAEngine:
         self.forward()
         self.backward()
         torch.cuda.synchronize(self.dev)
-        return self.LOGP.cpu().numpy(), float(self.LOSS.item())
+        return self.LOGP[:self.rows].cpu().numpy(), float(self.LOSS.item())
 
     def flush_optimizer(self):
         """Nothing is deferred here: the update runs at the end of the step."""
@@ -634,6 +636,29 @@ class VitVQAEngine:
     def refresh_shadow(self):
         self.P16.copy_(self.P32)
 
+    def optimizer_state(self):
+        """AdamW(amsgrad) state in reference layout, as VQAEngine.optimizer_state: ({key: exp_avg},
+        {key: exp_avg_sq}, {key: max_exp_avg_sq}, step, dropout RNG) over the trainable keys."""
+        torch.cuda.synchronize(self.dev)
+        unpack = lambda t: {k: v for k, v in self.lay.unpack(t.cpu().numpy()).items() if k not in VM.TIED}  # noqa: E731
+        return (unpack(self.M), unpack(self.V), unpack(self.VMAX), float(self.opt_state[L.ST_STEP].item()),
+                self.RNG.cpu().numpy().copy())
+
+    def load_optimizer_state(self, exp_avg, exp_avg_sq, max_exp_avg_sq, step, rng=None):
+        """Restore what optimizer_state() returned (keys missing from the dicts: zero state)."""
+        specs = VM.model_specs(self.A, self.H)
+        train = [k for s_ in self.lay.segments.values() for k in s_.parts]
+        zeros = {k: np.zeros(specs[k], np.float32) for k in train}
+        for arena, st in ((self.M, exp_avg), (self.V, exp_avg_sq), (self.VMAX, max_exp_avg_sq)):
+            full = dict(zeros)
+            full.update({k: np.asarray(v, np.float32) for k, v in st.items() if k in full})
+            arena.copy_(torch.from_numpy(self.lay.pack(full)))
+        self.opt_state.zero_()
+        self.opt_state[L.ST_STEP] = float(step)
+        if rng is not None:
+            self.RNG.copy_(torch.as_tensor(np.asarray(rng).astype(np.uint32).view(np.int32)))
+        torch.cuda.synchronize(self.dev)
+
     def vit_pooled(self):
-        """pooler_output of the frozen ViT for the current batch ([B, 768], from its bf16 copy)."""
-        return self.CAT16[:, :D].float()
+        """pooler_output of the frozen ViT for the current batch ([rows, 768], from its bf16 copy)."""
+        return self.CAT16[:self.rows, :D].float()

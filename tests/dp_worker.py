@@ -2,10 +2,11 @@
 the gloo backend (several ranks share the one GPU of the test box; RCCL refuses two ranks
 on one device).  Rank r trains on samples [r*B, (r+1)*B) of each global batch.
 
-  python tests/dp_worker.py RANK WORLD PORT OUT.npz STEPS PIPELINE GRAPH [trainer|shard|c5]
+  python tests/dp_worker.py RANK WORLD PORT OUT.npz STEPS PIPELINE GRAPH [trainer|trainer_short|shard|c5]
 
 `trainer`: drive the step through model.ResnetVQAModel + trainer.VQATrainer (data_parallel
-picked up from the initialised process group) instead of the engine directly; `shard`: the
+picked up from the initialised process group) instead of the engine directly; `trainer_short`:
+the same with a short last batch (3 rows per rank, padded to the planned 4); `shard`: the
 engine step with the sharded optimizer (reduce-scatter, AdamW on the own chunks, all-gather);
 `c5`: the engine step at BASELINE configs[4] widths (T5-large, 6 SGA blocks, fp8 forward GEMMs,
 T5 weight-gradient groups (8, 8, 6, 2))."""
@@ -35,10 +36,12 @@ def main():
     ekw = dict(language_model="t5-large", num_blocks=6, fp8=True) if c5 else {}
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0, **({"num_attention_blocks": 6, "language_model": "t5-large"}
                                                               if c5 else {}))
-    gb = [pkg.synthetic.make_batch(world * B, L, H, seed=40 + i) for i in range(steps + 1)]
-    mine = [{k: (None if v is None else v[rank * B:(rank + 1) * B]) for k, v in nb.items()} for nb in gb]
+    rows = short_rows(B, steps) if mode == "trainer_short" else [B] * (steps + 1)
+    gb = [pkg.synthetic.make_batch(world * rows[i], L, H, seed=40 + i) for i in range(steps + 1)]
+    mine = [{k: (None if v is None else v[rank * rows[i]:(rank + 1) * rows[i]]) for k, v in nb.items()}
+            for i, nb in enumerate(gb)]
     dev = [{k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None} for nb in mine]
-    if mode == "trainer":
+    if mode in ("trainer", "trainer_short"):
         tr = trainer_run(pkg, sd, B, L, H, dev, steps, graph)
         np.savez(out, **tr)
         dist.barrier()
@@ -82,6 +85,12 @@ def main():
              p16=eng.P16.float().cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()
+
+
+def short_rows(B, steps):
+    """trainer_short: per-rank rows of each step -- full batches, then a short last one (a
+    DistributedSampler loader without drop_last: every rank's last batch has the same 3 rows)."""
+    return [B] * (steps - 1) + [3, B]
 
 
 TRAINER_KW = dict(optimizer_kwargs={"type": "AdamW", "lm_encoder_lr": 1e-4, "classifier_lr": 1e-4,

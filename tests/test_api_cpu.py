@@ -29,3 +29,25 @@ def test_collate_refuses_interpolations_without_a_kernel(pkg):
     for strategy in ("LANCZOS4", "CUBIC", 4):
         with pytest.raises(NotImplementedError):
             pkg.data.DaquarCollate(interpolation_strategy=strategy, device="cpu")
+
+
+def test_short_batch_rows_are_padded_with_real_rows_and_ignored_targets(pkg):
+    """A loader's short last batch (no drop_last in the reference, faster_rcnn_vqa_trainer.py:172-197)
+    on a planned-B engine: rows past B' are copies of rows 0..B'-1 (every activation stays a real
+    sample's) and their targets NLLLoss's ignore_index, so the head's mean runs over B' rows."""
+    import torch
+    E = pkg.engine
+    dst = torch.full((7, 3), -1.0)
+    src = torch.arange(9.0).reshape(3, 3)
+    E.load_rows(dst, src, 3)
+    assert torch.equal(dst, src[torch.tensor([0, 1, 2, 0, 1, 2, 0])])
+    tgt = torch.zeros(7, dtype=torch.int64)
+    E.load_rows(tgt, torch.tensor([5, 6, 7]), 3, fill=E.IGNORE_INDEX)
+    assert tgt.tolist() == [5, 6, 7, -100, -100, -100, -100]
+    full = torch.zeros(7, dtype=torch.int64)
+    E.load_rows(full, torch.arange(7), 7, fill=E.IGNORE_INDEX)
+    assert full.tolist() == list(range(7))
+    assert E.batch_rows({"q": torch.zeros(5, 2)}, "q", 7) == 5
+    for bad in (0, 8):
+        with pytest.raises(ValueError):
+            E.batch_rows({"q": torch.zeros(bad, 2)}, "q", 7)

@@ -1,8 +1,9 @@
-"""The data-parallel step (bucketed async RCCL all-reduce captured into the backward graph,
-overlapped with its later segments, + (id, row) all-gather for the embedding) at
-world_size 1 on one MI355X: every exchange is then an identity, so it must
-reproduce the single-GPU graph step bit for bit.  Multi-rank arithmetic is
-covered by tests/test_dp_cpu.py (gloo)."""
+"""The data-parallel step (dp.DataParallelStep: the backward as stage graphs, the bucketed async
+RCCL all-reduce of each stage's finished buckets issued between them on a comm stream and
+overlapped with the later stages, + the (id, row) all-gather for the embedding) at world_size 1
+on one MI355X: every exchange is then an identity, so it must reproduce the single-GPU graph step
+bit for bit.  Multi-rank arithmetic is covered by tests/test_dp_cpu.py and
+tests/test_a_dp2_gpu.py (gloo)."""
 import os
 import socket
 
@@ -27,11 +28,11 @@ def pg(pkg):
     dist.destroy_process_group()
 
 
-# graphed cases first: in r04, a DP capture (RCCL collectives inside the backward graph) that
-# followed an earlier graphed DP object AND eager async collectives on the same communicator
-# segfaulted in capture_end; alone, or in this order, every capture passes
-# (profiles/r04_rccl_capture.txt).  A DataParallelStep captures once, before its first step.
-@pytest.mark.parametrize("graph,pipe", [(True, False), (True, True), (False, False), (False, True)])
+# (r04: a form that captured the collectives INTO the backward graph segfaulted in capture_end
+# when it followed eager async collectives on the same communicator, profiles/r04_rccl_capture.txt;
+# no collective is captured any more -- the stage graphs hold kernels only -- so the cases run in
+# their natural order)
+@pytest.mark.parametrize("graph,pipe", [(False, False), (False, True), (True, False), (True, True)])
 def test_dp_world1_matches_single_gpu(pg, pkg, graph, pipe):
     """World-1 DP (bucketed all-reduce, gathered-row embedding scatter, segmented graphs; with
     `pipe` also the separately replayed next-batch ResNet) == the single-GPU step, bit for bit,
@@ -89,21 +90,32 @@ def test_dp_world1_sharded_optimizer_rccl(pg, pkg):
     dev = [{k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None} for nb in nbs]
     e1 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20)
     e2 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, t5_dw_group=(4, 4, 3, 1))
+    # e3: the same sharded step with bench.py's collective timing on -- its timing stream only
+    # waits on the collectives (it once also re-ran the reduce-scatter's follow-up copy,
+    # unordered with the next step's backward); bit-identical to e2
+    e3 = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, t5_dw_group=(4, 4, 3, 1))
     e1.capture()
     step = pkg.dp.DataParallelStep(e2, bucket_mb=8, use_graph=True, shard_optimizer=True)
+    step3 = pkg.dp.DataParallelStep(e3, bucket_mb=8, use_graph=True, shard_optimizer=True)
+    step3.timing = True
     for i in range(3):
-        for e in (e1, e2):
+        for e in (e1, e2, e3):
             e.load_batch(dev[i])
         e1.train_step()
         step.step()
+        step3.step()
         torch.cuda.synchronize()
-        assert float(e1.LOSS) == float(e2.LOSS), i
+        assert float(e1.LOSS) == float(e2.LOSS) == float(e3.LOSS), i
         n1, n2 = e1.last_grad_norm(), e2.last_grad_norm()
         assert abs(n1 - n2) <= 1e-6 * abs(n1), (i, n1, n2)
-    e1.flush_optimizer()
-    e2.flush_optimizer()
+        assert torch.equal(e2.G32, e3.G32), i
+    assert step3.timing_report()["steps"] == 3
+    for e in (e1, e2, e3):
+        e.flush_optimizer()
     step.sync_optimizer_state()
+    step3.sync_optimizer_state()
     rel = float((e1.P32 - e2.P32).norm() / e1.P32.norm())
     assert rel <= 1e-6, rel
     vrel = float((e1.VMAX - e2.VMAX).norm() / e1.VMAX.norm())
     assert vrel <= 1e-5, vrel
+    assert torch.equal(e2.P32, e3.P32) and torch.equal(e2.M, e3.M) and torch.equal(e2.VMAX, e3.VMAX)

@@ -238,17 +238,24 @@ def test_causal_bias_with_key_mask_one_finfo_min(k, Lq):
     torch.testing.assert_close(p[0], torch.full_like(p[0], 1.0 / Lk))   # fully masked: uniform
 
 
-@pytest.mark.parametrize("B,L,A,D", [(8, 32, 170, 768), (64, 32, 170, 768), (37, 49, 13, 768), (5, 16, 192, 768),
-                                     (64, 32, 170, 1024), (19, 49, 37, 1024), (6, 16, 192, 836), (3, 7, 5, 20),
-                                     (16, 32, 193, 768), (21, 32, 700, 768), (5, 16, 1024, 1024)])
-def test_head_fwd_bwd(k, B, L, A, D):
+@pytest.mark.parametrize("B,L,A,D,ign", [(8, 32, 170, 768, 0), (64, 32, 170, 768, 0), (37, 49, 13, 768, 0),
+                                         (5, 16, 192, 768, 0), (64, 32, 170, 1024, 0), (19, 49, 37, 1024, 0),
+                                         (6, 16, 192, 836, 0), (3, 7, 5, 20, 0), (16, 32, 193, 768, 0),
+                                         (21, 32, 700, 768, 0), (5, 16, 1024, 1024, 0),
+                                         (64, 32, 170, 768, 27), (300, 16, 170, 768, 33), (9, 16, 700, 768, 8)])
+def test_head_fwd_bwd(k, B, L, A, D, ign):
     """D = 1024 is T5-large's width (BASELINE config 5); 836 / 20 exercise the masked
     column tail of the 256- and 192-column pooler layouts; A > 192 the chunked answer
-    loop of the dpooled kernel (193: a one-answer second chunk)."""
+    loop of the dpooled kernel (193: a one-answer second chunk).  ign > 0: that many rows
+    (the last, as the engines pad a short final batch) carry target -100, NLLLoss's
+    ignore_index: nll 0, the mean over the other rows, no gradient from them (300 rows:
+    the divisor's count runs over two 256-row passes)."""
     x = rnd((B, L, D), 20)
     wp, bp = 0.03 * rnd(D, 21), 0.1 * rnd(1, 22)
     wc, bc = 0.03 * rnd((A, D), 23), 0.1 * rnd(A, 24)
     tgt = torch.randint(0, A, (B,), device="cuda")
+    if ign:
+        tgt[B - ign:] = -100
     att, pooled, logp = torch.empty(B, L, device="cuda"), torch.empty(B, D, device="cuda"), \
         torch.empty(B, A, device="cuda")
     nll, loss = torch.empty(B, device="cuda"), torch.empty(1, device="cuda")
@@ -261,6 +268,7 @@ def test_head_fwd_bwd(k, B, L, A, D):
     ls.backward()
     torch.testing.assert_close(logp, lp.detach(), rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(loss[0], ls.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(nll, F.nll_loss(lp, tgt, reduction="none").detach(), rtol=1e-5, atol=1e-6)
     dx = torch.empty_like(x)
     dwp, dbp, dwc, dbc = torch.empty_like(wp), torch.empty(1, device="cuda"), torch.empty_like(wc), \
         torch.empty_like(bc)

@@ -1,8 +1,9 @@
 """Parity of the N > 1 training step at the benched size, on one GPU.
 
 test_dp_step_b64_matches_oracle: dp.DataParallelStep -- the step bench.py runs at N > 1
-(segmented backward graphs with the single-GPU stream placement, bucketed collectives,
-gathered embedding rows, grad-norm partials beside the backward) -- over a world-1 RCCL
+(the backward as stage graphs with the single-GPU stream placement, the bucketed collectives
+issued between them, gathered embedding rows, then the finish graph: embedding scatter,
+grad-norm partials, clip, AdamW) -- over a world-1 RCCL
 group on the DP engine (R50, B=64, 224x224, L=32, pipelined frozen ResNet, tuned tiles,
 deferred AdamW, dropout 0.1, T5 weight-gradient groups (4, 4, 3, 1)), stepped 3 times
 against the CPU fp32 oracle on the same batches and dropout masks

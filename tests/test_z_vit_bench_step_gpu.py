@@ -86,17 +86,20 @@ def test_vit_bench_step_b64_matches_oracle(pkg, parity_report):
     parity_report["vit_bench_b64"] = rep
     for i in range(3):
         r = rep[f"step{i}"]
-        # the frozen ViT's bf16 forward moves the fused token (B = 4 golden: pooled 1.2e-2 of its
-        # max); at B = 64 the gradient sums 64 answer / CLS rows, so the rounding averages out:
-        # measured log-probs 1.9e-2 / 1.6e-2 / 0.10 (the max over 64 x 170 after two AdamW
-        # updates, whose first steps move every weight by ~lr * sign(g)), loss <= 2.6e-4, grad
-        # norm <= 1.2e-3, groups <= 7.8e-3 (fusing layer, step 2)
+        # bf16 arithmetic: the fp32 oracle under oracle/bf16_mode.Bf16Operands (every matmul on
+        # bf16 operands) against the plain fp32 oracle on these batches measures log-probs
+        # 1.7e-2 / 1.7e-2 / 8.8e-2, loss <= 1.6e-4, grad norm <= 1.9e-3, groups <= 1.6e-2 (fusing
+        # layer, step 2) (tools/drift_ab_vit.py, profiles/r05_drift_ab_vit.json); the engine
+        # measured 1.9e-2 / 1.6e-2 / 0.10, loss <= 2.6e-4, grad norm <= 1.2e-3, groups <= 7.8e-3:
+        # the bounds are ~1.5x the bf16-operand oracle's own error (step 2 follows the first
+        # nonzero-lr AdamW update, which moves every weight by ~lr * sign(g): a near-zero
+        # gradient's rounding becomes an O(lr) difference in either arithmetic)
         assert r["log_prob_max_abs"] <= (3e-2 if i < 2 else 0.13), rep
         assert r["loss_rel"] <= 5e-4, rep
         assert r["grad_norm_rel"] <= 2.5e-3, rep
-        assert max(r["group_grad_norm_rel"].values()) <= (3e-3 if i < 2 else 1.2e-2), rep
+        assert max(r["group_grad_norm_rel"].values()) <= (5e-3 if i < 2 else 2.5e-2), rep
     # relative L2 of the per-group update vectors after three steps: measured 0.04 (classifier),
-    # 0.16 (T5), 0.19 (fusing layer, whose Dropout(0.5) input is the bf16 ViT token)
+    # 0.16 (T5), 0.19 (fusing layer); the bf16-operand oracle: 0.037 / 0.14 / 0.19
     assert max(delta.values()) <= 0.25, delta
     # A/B with the engine's pooled outputs fed to the oracle: at B = 64 it does NOT bring the
     # oracle closer (measured r04: step-2 log-probs 0.110 vs 0.100, grad norm 2.6e-3 vs 1.2e-3):

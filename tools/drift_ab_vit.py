@@ -25,53 +25,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-from torch.overrides import TorchFunctionMode  # noqa: E402
 
 from __graft_entry__ import load_package  # noqa: E402
 from oracle import vit_oracle as orc  # noqa: E402
+from oracle.bf16_mode import Bf16Operands  # noqa: E402,F401  (re-exported for tools/)
 
 torch.set_num_threads(min(16, os.cpu_count()))   # the GPU box shows the whole host
 F = torch.nn.functional
 GROUPS = ("lang_model", "fusing_layer", "classification_layer")
-
-
-def r16(t):
-    return t.bfloat16().float()
-
-
-class _Bf16MM(torch.autograd.Function):
-    """a @ b on bf16-rounded operands, fp32 accumulation; the backward rounds dY too."""
-
-    @staticmethod
-    def forward(ctx, a, b):
-        ctx.save_for_backward(a, b)
-        return torch.matmul(r16(a), r16(b))
-
-    @staticmethod
-    def backward(ctx, dy):
-        a, b = ctx.saved_tensors
-        # (run under the mode when backward() is called inside it: the operands are rounded
-        # already, so the mode's second rounding changes nothing)
-        d = r16(dy)
-        da = torch.matmul(d, r16(b).transpose(-1, -2)) if ctx.needs_input_grad[0] else None
-        db = torch.matmul(r16(a).transpose(-1, -2), d) if ctx.needs_input_grad[1] else None
-        if db is not None and db.dim() > b.dim():                  # broadcast weight: sum the batch dims
-            db = db.reshape(-1, *b.shape).sum(0)
-        if da is not None and da.shape != a.shape:                 # broadcast activation
-            da = da.reshape(-1, *a.shape).sum(0)
-        return da, db
-
-
-class Bf16Operands(TorchFunctionMode):
-    def __torch_function__(self, func, types, args=(), kwargs=None):
-        kwargs = kwargs or {}
-        if func in (torch.matmul, torch.Tensor.__matmul__) and all(torch.is_tensor(x) for x in args[:2]) \
-                and args[0].dim() >= 2 and args[1].dim() >= 2:
-            return _Bf16MM.apply(args[0], args[1])
-        if func is F.conv2d:                                      # the ViT patch embedding (frozen)
-            x, w = args[0], args[1]
-            return func(r16(x), r16(w), *args[2:], **kwargs)
-        return func(*args, **kwargs)
 
 
 def updates(tr, p0):
