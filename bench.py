@@ -99,6 +99,95 @@ def calls_flop(eng, fp8_only=False):
     return tot
 
 
+def _flat_calls(calls):
+    for c in calls:
+        if hasattr(c, "calls"):                                    # engine._Seq (AdamW range + e4m3 copies)
+            yield from _flat_calls(c.calls)
+        else:
+            yield c
+
+
+def step_calls(eng):
+    """Every prepared call one benched step launches: the next batch's frozen ResNet (pipelined),
+    the F4 copy, the deferred AdamW ranges, forward, backward and the optimizer plan."""
+    seq = []
+    if eng.pipeline:
+        seq += [eng.copy_f4] + list(eng.res_calls)
+    if eng.defer_opt:
+        seq += [c for _, c in eng.adam_segs] + [eng.clear_pending]
+    seq += list(eng.fwd_calls) + list(eng.bwd_calls) + list(eng.opt_calls)
+    return list(_flat_calls(seq))
+
+
+def call_bytes(c):
+    """ALGORITHMIC HBM bytes of one prepared call: every operand read once and every result
+    written once, at the precision the kernel stores it (SURVEY §8d's per-op byte model).
+      GEMM: A (or, implicit im2col, the input activation itself) + B + C (fp32 and / or bf16, read
+        too when beta != 0) + bias + residual + mask, per batch item where the stride is nonzero;
+      attention: q, k, v (+ o, P) forward; q, k, v, P, dO, dq, dk, dv (+ dbias) backward, per
+        (sample, head, group) + the shared bias / key mask;
+      AdamW-amsgrad: 38 B per parameter (read p g m v vmax, write p m v vmax + bf16 shadow);
+      embedding gather / scatter / row re-zeroing: the touched rows only (not the 98.7 MB table);
+      grad sq-norm: the gradient range once;
+      everything else (norms, column sums, copies, the image / pooling kernels, the head): the
+        tensors the call is declared to read and write (its `keep`), each once."""
+    n = c.name
+    d = c.desc
+    if n in ("vqa_gemm", "vqa_gemm_pair"):
+        return sum(_gemm_bytes(x) for x in (d if isinstance(d, (tuple, list)) else (d,)))
+    if n in ("vqa_attn_fwd", "vqa_attn_bwd"):
+        g = max(1, d.groups)
+        per = (d.lq + 2 * d.lk) * d.dh * 2                          # q, k, v (bf16)
+        if n == "vqa_attn_fwd":
+            per += d.lq * d.dh * 2 + (d.lq * d.lk * 4 if d.p else 0)  # o (+ saved P)
+        else:
+            per += d.lq * d.lk * 4 + d.lq * d.dh * 2 + (d.lq + 2 * d.lk) * d.dh * 2 + (d.lq * d.lk * 4 if d.dbias else 0)
+        shared = (d.heads * d.lq * d.lk * 4 if d.bias else 0) + (d.batch * d.lk * 8 if d.key_mask else 0)
+        return float(g * (d.batch * d.heads * per + shared))
+    if n == "vqa_adamw_amsgrad":
+        return 38.0 * d.n
+    if n == "vqa_grad_sqnorm":
+        return 4.0 * c.args[1]
+    if n == "vqa_embedding_fwd":                                    # ids, table, out, tokens, d, ...
+        t, dd = c.args[3], c.args[4]
+        return float(t * 8 + 2 * t * dd * 4)
+    if n == "vqa_embedding_bwd":                                    # ids, dh, dtable, tokens, d, ...
+        t, dd = c.args[3], c.args[4]
+        return float(t * 8 + 2 * t * dd * 4)
+    if n == "vqa_embedding_zero_rows":                              # prev, cur, tokens, dtable, d, ...
+        t, dd = c.args[2], c.args[4]
+        return float(2 * t * 8 + t * dd * 4)
+    seen, tot = set(), 0
+    for t in (c.keep or ()):
+        if isinstance(t, torch.Tensor):
+            key = (t.data_ptr(), t.numel(), t.element_size())
+            if key not in seen:
+                seen.add(key)
+                tot += t.numel() * t.element_size()
+    return float(tot)
+
+
+def _gemm_bytes(d):
+    e = 1 if d.fp8 else 2
+    b = max(1, d.batch)
+    m, n, k = d.m, d.n, d.k
+    if d.a_conv:
+        ga = d.ga
+        a = ga.n * ga.h * ga.w * ga.c * 2
+    else:
+        a = m * k * e * (b if d.stride_a else 1)
+    if d.b_conv:
+        gb = d.gb
+        bb = gb.n * gb.h * gb.w * gb.c * 2
+    else:
+        bb = n * k * e * (b if d.stride_b else 1)
+    out = m * n * b * ((4 * (2 if d.beta else 1) if d.c32 else 0) + (2 if d.c16 else 0))
+    extra = (n * 4 * (b if d.stride_bias else 1) if d.bias else 0)
+    rb = b if d.stride_res else 1
+    extra += m * n * rb * ((4 if d.res32 else 0) + (2 if d.res16 else 0) + (2 if d.mask16 else 0))
+    return float(a + bb + out + extra)
+
+
 def vit_flop_per_pair(lq, ld, nv=197, d=768, dff=3072, vff=3072, layers=12):
     """Algorithmic FLOPs of one config-4 pair (VitVQAModel, vit_vqa_model.py:166-225): the frozen
     ViT forward, the T5 encoder and decoder forward + backward (x3: the input and weight
@@ -410,6 +499,7 @@ def main():
     step_flop = FLOP_PER_PAIR * B if survey_cfg else calls_flop(eng)
     step_tflops = step_flop / gpu_step / 1e12
     st = pmc.get("step", {})
+    alg = sum(call_bytes(c) for c in step_calls(eng))            # algorithmic HBM bytes of one step
     # config 5 mixes e4m3 (forward weight GEMMs) and bf16 MFMA work: the peak is the rate at which
     # the step's FLOP mix would run with every launch at its dtype's dense peak
     f8 = calls_flop(eng, fp8_only=True)
@@ -428,6 +518,11 @@ def main():
                 "frac": round(step_tflops / peak, 4),
                 **({"fp8_flop_per_step": f8, "peak_note": "e4m3 FLOPs at 5034, bf16 FLOPs at 2517 TFLOP/s"} if f8 else {}),
                 "traffic": round(st["traffic_bytes"]) if "traffic_bytes" in st else None,
+                "alg_bytes": round(alg),
+                "traffic_over_alg": round(st["traffic_bytes"] / alg, 3) if "traffic_bytes" in st else None,
+                "alg_bytes_model": "bench.call_bytes: every operand read once, every result written once "
+                                   "(GEMM A/B/C/bias/residual; attention q/k/v/o/P; AdamW 38 B/param; "
+                                   "touched embedding rows; the declared tensors of the other kernels)",
                 "flop_per_step": step_flop, "flop_per_step_calls": calls_flop(eng),
                 "step_gpu_ms": round(gpu_step * 1e3, 4),
                 "traffic_source": pmc_note}
@@ -509,6 +604,9 @@ def kernel_rooflines(eng, stream, pmc):
     out["roofline_gemm"] = {"bound": "mfma", "kernel": kname, "achieved": round(k_tflops, 1), "peak": MFMA_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": round(k_tflops / MFMA_PEAK_TFLOPS, 4),
                             "traffic": (round(pmc["convT_dW"]["traffic_bytes"]) if "convT_dW" in pmc else None),
+                            "alg_bytes": call_bytes(wg_call),
+                            "traffic_over_alg": (round(pmc["convT_dW"]["traffic_bytes"] / call_bytes(wg_call), 3)
+                                                 if "convT_dW" in pmc else None),
                             "kernel_avg_us": round(kdur * 1e6, 2), "flop_per_launch": kflop}
     # north_star's SGA figure: MFMA utilisation of the SGA blocks' GEMM launches (the q/k/v,
     # merge and FFN linears of MHAtt / FFN, forward and backward; `gemm`) and of those plus
@@ -539,6 +637,11 @@ def kernel_rooflines(eng, stream, pmc):
         pk = fl / sum(call_flop(c) / call_peak(c) for c in cs)
         sga[tag] = {"launches": len(cs), "flop_per_step": fl, "kernel_us_per_step": round(tm * 1e6, 1),
                     "achieved": round(fl / tm / 1e12, 1), "peak": round(pk, 1), "frac": round(fl / tm / 1e12 / pk, 4)}
+    gb = sum(call_bytes(c) for c in sga_calls if c.name in ("vqa_gemm", "vqa_gemm_pair"))
+    sga["gemm"]["alg_bytes"] = gb
+    if "sga_gemm" in pmc:
+        sga["gemm"]["traffic"] = round(pmc["sga_gemm"]["traffic_bytes"])
+        sga["gemm"]["traffic_over_alg"] = round(pmc["sga_gemm"]["traffic_bytes"] / gb, 3)
     out["sga_mfma"] = {"peak": sga["gemm"]["peak"], "unit": "TFLOP/s", "target_frac": 0.40, **sga,
                        "pmc_mfma_busy": pmc.get("sga_mfma_busy")}
     # e4m3 (config 5): the largest fp8 launch of the step against the fp8 dense peak

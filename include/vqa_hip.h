@@ -139,7 +139,7 @@ typedef struct vqa_gemm_desc {
  * 7 64x128/2, 8 128x128/2 (4 waves); 9 256x128/2, 10 128x256/2, 11 256x256/2, 12 256x128/3 (8 waves);
  * 13..16 64x192 / 128x192 (k-contiguous B only); 17..20 the LDS-patch convolution;
  * 21 64x64/2, 22 64x128/2, 23 128x64/2 with 128-deep k-tiles (no implicit im2col, no split-K) */
-#define VQA_GEMM_CONFIGS 23
+#define VQA_GEMM_CONFIGS 24
 #define VQA_GEMM_PATCH_FIRST 17    /* configs 17..20: a_conv = 2 only */
 #define VQA_GEMM_PATCH_LAST 20
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);

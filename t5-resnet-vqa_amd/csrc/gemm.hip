@@ -59,7 +59,8 @@ __global__ __launch_bounds__(256) void gemm_pair_kernel(GemmParams P1, GemmParam
 //         12 = 256x128 (3, 8 waves 4x2); 13 = 64x192 (2); 14 = 128x192 (2); 15 = 64x192 (3);
 //         16 = 128x192 (3) -- 4 waves, k-contiguous B only;
 //         17..20 = the LDS-patch 3x3 convolution (a_conv = 2, conv_patch.inl): 128x64, 128x128,
-//         64x64, 64x128.
+//         64x64, 64x128; 21..23 = 64x64 / 64x128 / 128x64 with 128-deep k-tiles (4 waves);
+//         24 = 64x128 with 128-deep k-tiles on 8 waves (2x4).
 // Every config accumulates each output element in the same K order (BK = 64
 // k-tiles, 16-deep MFMA steps), so the choice changes speed, never the bits.
 // Auto (measured on MI355X, tools/callprof.py): fewer stages = less LDS = more
@@ -100,13 +101,16 @@ int dispatch_tile(GemmParams& P, int batch, int config, hipStream_t s) {
       } else {
         return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: tile config %d needs a k-contiguous B operand (b_trans=0)", config);
       }
-    case 21: case 22: case 23:
+    case 21: case 22: case 23: case 24:
       // 128-deep k-tiles: twice the bytes per ring slot and per barrier (the per-k-tile fixed
       // cost of the L2 -> LDS fill is amortised over 32-48 KB instead of 16-24 KB); plain
-      // (non-gathered) operands, no split-K
+      // (non-gathered) operands, no split-K.  24: config 22's 64x128 tile on 8 waves (2x4, each
+      // 32x32): twice the waves issuing the ring's DMA pieces (r04 stamps: 7 % faster on the
+      // 2048 x 2304 x 768 q|k|v projection)
       if constexpr (!GA && !GB) {
         if (config == 21) return launch<64, 64, 2, 2, 2, AKC, BKC, GA, GB, 128>(P, batch, s);
         if (config == 22) return launch<64, 128, 2, 2, 2, AKC, BKC, GA, GB, 128>(P, batch, s);
+        if (config == 24) return launch<64, 128, 2, 2, 4, AKC, BKC, GA, GB, 128>(P, batch, s);
         return launch<128, 64, 2, 2, 2, AKC, BKC, GA, GB, 128>(P, batch, s);
       } else {
         return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: tile config %d takes no implicit-im2col operand", config);
@@ -123,7 +127,7 @@ void tile_of(int config, int& bm, int& bn) {
                                                  {64, 64},   {128, 64},  {64, 128}, {128, 128}, {256, 128},
                                                  {128, 256}, {256, 256}, {256, 128}, {64, 192}, {128, 192},
                                                  {64, 192},  {128, 192}, {128, 64}, {128, 128}, {64, 64},
-                                                 {64, 128},  {64, 64},   {64, 128}, {128, 64}};
+                                                 {64, 128},  {64, 64},   {64, 128}, {128, 64}, {64, 128}};
   bm = T[config][0];
   bn = T[config][1];
 }

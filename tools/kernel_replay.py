@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 from __graft_entry__ import load_package  # noqa: E402
+from bench import call_bytes  # noqa: E402  (the algorithmic byte model bench.py reports)
 
 out_path = sys.argv[1]
 REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
@@ -56,21 +57,22 @@ def gemm_flop(c):
 
 plan = [("adamw", eng.adam_full, 0.0, 38.0 * eng.lay.total)]
 if MODE == "res":
-    plan = [(f"res{i:02d}", c, gemm_flop(c) if c.name == "vqa_gemm" else 0.0, 0.0) for i, c in enumerate(eng.res_calls)]
+    plan = [(f"res{i:02d}", c, gemm_flop(c) if c.name == "vqa_gemm" else 0.0, call_bytes(c))
+            for i, c in enumerate(eng.res_calls)]
     # the T5 layer-0 forward GEMMs for comparison
     t5 = [c for c in eng.fwd_calls[eng._t5_layer_start[0]:eng._t5_layer_start[1]] if c.name == "vqa_gemm"]
-    plan += [(f"t5_{i}", c, gemm_flop(c), 0.0) for i, c in enumerate(t5)]
+    plan += [(f"t5_{i}", c, gemm_flop(c), call_bytes(c)) for i, c in enumerate(t5)]
 if MODE != "res":
     wg = eng.scaler_dw_call                                  # the tap-batched scaler dW GEMM
-    plan.append(("convT_dW", wg, gemm_flop(wg), 0.0))
+    plan.append(("convT_dW", wg, gemm_flop(wg), call_bytes(wg)))
     f8 = [c for c in eng.res_calls + eng.fwd_calls + eng.bwd_calls if c.name == "vqa_gemm" and c.desc.fp8]
     if f8:                                                   # bench roofline_fp8: the largest e4m3 launch
         c8 = max(f8, key=gemm_flop)
-        plan.append(("fp8_gemm", c8, gemm_flop(c8), 0.0))
+        plan.append(("fp8_gemm", c8, gemm_flop(c8), call_bytes(c8)))
     sga = [c for c in eng.sga_vision_calls + eng.fwd_calls[eng._fsplit[2]:] + eng.bwd_calls[:eng._bsplit[0]]
            if c.name in ("vqa_gemm", "vqa_gemm_pair", "vqa_attn_fwd", "vqa_attn_bwd")]
     for c in sga:
-        plan.append(("sga_gemm" if c.name.startswith("vqa_gemm") else "sga_attn", c, gemm_flop(c), 0.0))
+        plan.append(("sga_gemm" if c.name.startswith("vqa_gemm") else "sga_attn", c, gemm_flop(c), call_bytes(c)))
 man = []
 for tag, c, fl, by in plan:
     for _ in range(REPS):

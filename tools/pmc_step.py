@@ -94,6 +94,9 @@ def main():
                                "algorithmic_bytes": res["adamw"]["alg_bytes"]}
     if "convT_dW" in res:
         res["convT_dW"] = dict(res["convT_dW"])
+    for tag, e in per.items():                             # measured HBM traffic over the algorithmic bytes
+        if tag in res and res[tag].get("alg_bytes"):
+            res[tag]["traffic_over_alg"] = res[tag]["traffic_bytes"] / res[tag]["alg_bytes"]
     if "sga_gemm" in res:
         g = res["sga_gemm"]
         res["sga_mfma_busy"] = {"mfma_pipe_frac_gemm": g.get("mfma_pipe_frac"),
