@@ -309,6 +309,121 @@ def time_kernel(call, reps, stream):
     return start.elapsed_time(end) / reps * 1e-3
 
 
+def make_step(args, pkg, dev, pool, use_dp, rank, lm):
+    """The engine at the bench shapes, tuned and captured: the single-GPU graph step, or for
+    `use_dp` the N > 1 code path (dp.DataParallelStep with the DP engine's weight-gradient
+    groups).  Returns (engine, DataParallelStep or None, step(i) loading pool batch i)."""
+    B, L, H, NB = args.batch, args.seq_len, args.image_size, args.blocks
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, num_attention_blocks=NB,
+                                       language_model=lm)      # identical init on every rank
+    pipe = not args.no_pipeline
+    dp_groups = pkg.dp.dp_t5_dw_groups(pkg.synthetic.lm_dims(lm).t5_layers)
+    eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev, num_blocks=NB,
+                               warmup=10, total=100000, dropout=0.1, seed=rank, pipeline=pipe,
+                               t5_dw_group=dp_groups if (use_dp or args.dp_groups) else None, language_model=lm,
+                               fp8=args.config5)
+    del sd
+    torch.cuda.synchronize()
+    if pipe:
+        # the frozen ResNet of batch k+1 runs beside step k (engine docstring): prime batch 0's features
+        eng.prime(pool[0]["image_tensors"])
+        eng.F4.copy_(eng.F4N)
+        eng.load_batch(pool[0], next_images=pool[1]["image_tensors"])
+    else:
+        eng.load_batch(pool[0])
+    eng.forward()
+    eng.backward()
+    eng.autotune(table=args.tune_table, save=args.tune_save if rank == 0 else None)   # tile choice: speed only
+    dps = None
+    if use_dp:
+        dps = pkg.dp.DataParallelStep(eng, use_graph=not args.no_graph, shard_optimizer=args.shard_optimizer,
+                                      **({} if args.dp_res_split is None else {"res_split": args.dp_res_split}))
+        run_step = dps.step
+    else:
+        if not args.no_graph:
+            eng.capture()
+        run_step = eng.train_step
+    if pipe:                                       # the tuning passes above consumed nothing: restart at batch 0
+        eng.prime(pool[0]["image_tensors"])
+    k = [0]
+
+    def step(_):
+        i = k[0]
+        k[0] += 1
+        if pipe:
+            eng.load_batch(pool[i % len(pool)], next_images=pool[(i + 1) % len(pool)]["image_tensors"])
+        else:
+            eng.load_batch(pool[i % len(pool)])
+        run_step()
+    return eng, dps, step
+
+
+def time_steps(args, step, dev, dist):
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize on both sides;
+    returns (wall seconds, GPU seconds per step from HIP events on the replay stream, host issue
+    seconds), each the max over ranks."""
+    for i in range(args.warmup):
+        step(i)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(i)
+    ev1.record(stream)
+    t_issue = time.perf_counter() - t0             # host time to issue the K steps (< dt: the host ran ahead)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    gpu_step = ev0.elapsed_time(ev1) * 1e-3 / args.steps       # HIP events on the replay stream
+    if dist:
+        t = torch.tensor([dt, gpu_step], device="cpu" if args.rehearse else dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, gpu_step = float(t[0].item()), float(t[1].item())
+    return dt, gpu_step, t_issue
+
+
+def init_world1(dev):
+    """A world-1 RCCL group of this process (the N > 1 code path on one GPU)."""
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+        s.close()
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    return dist
+
+
+def dp_world1_line(args, pkg, dev, pool, lm, engine_dt):
+    """The N > 1 code path at N = 1: the same workload through
+    dp.DataParallelStep over a world-1 RCCL group -- forward graph, backward stage graphs with
+    the bucketed all-reduce between them, finish graph -- timed exactly as the headline step,
+    so SCALE's N = 1 point (the engine graph) can be read against the path N > 1 runs."""
+    dist = init_world1(dev)
+    try:
+        eng, dps, step = make_step(args, pkg, dev, pool, True, 0, lm)
+        dt, gpu_step, _ = time_steps(args, step, dev, dist)
+        res = {"value": round(args.batch * args.steps / dt, 2), "unit": "pairs/s",
+               "ms_per_step": round(dt / args.steps * 1e3, 3), "step_gpu_ms": round(gpu_step * 1e3, 4),
+               "over_engine_step": round(dt / engine_dt, 4),
+               "path": f"dp.DataParallelStep over a world-1 {dist.get_backend()} group: forward graph, "
+                       f"{len(dps.stages)} backward stage graphs with the bucketed all-reduce between them, "
+                       "finish graph (the code path bench.py runs for N > 1)",
+               "loss": round(float(eng.LOSS.item()), 5)}
+        del eng, dps, step
+    finally:
+        dist.destroy_process_group()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -342,6 +457,9 @@ def main():
                     help="DP, pipelined: share of the next batch's ResNet calls beside the forward graph (dp.RES_SPLIT)")
     ap.add_argument("--dp-groups", action="store_true",
                     help="the single-GPU engine step with the DP engine's T5 weight-gradient groups (A/B of --dp)")
+    ap.add_argument("--no-dp-line", action="store_true",
+                    help="N = 1: skip the second timing of the same workload through the N > 1 code path "
+                         "(dp.DataParallelStep over a world-1 RCCL group; JSON key dp_world1)")
     ap.add_argument("--rehearse", action="store_true",
                     help="run every rank on cuda:0 over gloo: exercises the N-rank code path (bucketing, "
                          "gathers, capture, lockstep) on a one-GPU box; the timing is not a measurement")
@@ -377,13 +495,7 @@ def main():
     if use_dp:
         import torch.distributed as dist
         if world == 1:                                   # --dp: a world-1 RCCL group of this process
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            if "MASTER_PORT" not in os.environ:
-                s = socket.socket()
-                s.bind(("127.0.0.1", 0))
-                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
-                s.close()
-            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+            init_world1(dev)
         elif args.rehearse:
             dist.init_process_group("gloo")
         else:
@@ -395,76 +507,13 @@ def main():
     lm = "t5-large" if args.config5 else "t5-base"
     B, L, H = args.batch, args.seq_len, args.image_size
     NB = args.blocks
-    sd = pkg.synthetic.make_state_dict("resnet50", seed=0, num_attention_blocks=NB,
-                                       language_model=lm)      # identical init on every rank
     pipe = not args.no_pipeline
-    dp_groups = pkg.dp.dp_t5_dw_groups(pkg.synthetic.lm_dims(lm).t5_layers)
-    eng = pkg.engine.VQAEngine(sd, vision="resnet50", batch=B, seq_len=L, image_size=H, device=dev, num_blocks=NB,
-                               warmup=10, total=100000, dropout=0.1, seed=rank, pipeline=pipe,
-                               t5_dw_group=dp_groups if (use_dp or args.dp_groups) else None, language_model=lm,
-                               fp8=args.config5)
-    del sd
     pool = []
     for i in range(4):
         nb = pkg.synthetic.make_batch(B, L, H, seed=1 + rank * 16 + i)
         pool.append({k: torch.as_tensor(v).to(dev) for k, v in nb.items() if v is not None})
-    torch.cuda.synchronize()
-    if pipe:
-        # the frozen ResNet of batch k+1 runs beside step k (engine docstring): prime batch 0's features
-        eng.prime(pool[0]["image_tensors"])
-        eng.F4.copy_(eng.F4N)
-        eng.load_batch(pool[0], next_images=pool[1]["image_tensors"])
-    else:
-        eng.load_batch(pool[0])
-    eng.forward()
-    eng.backward()
-    eng.autotune(table=args.tune_table, save=args.tune_save if rank == 0 else None)   # tile choice: speed only
-    if use_dp:
-        dps = pkg.dp.DataParallelStep(eng, use_graph=not args.no_graph, shard_optimizer=args.shard_optimizer,
-                                      **({} if args.dp_res_split is None else {"res_split": args.dp_res_split}))
-        run_step = dps.step
-    else:
-        if not args.no_graph:
-            eng.capture()
-        run_step = eng.train_step
-
-    if pipe:                                       # the tuning passes above consumed nothing: restart at batch 0
-        eng.prime(pool[0]["image_tensors"])
-    k = [0]
-
-    def step(_):
-        i = k[0]
-        k[0] += 1
-        if pipe:
-            eng.load_batch(pool[i % len(pool)], next_images=pool[(i + 1) % len(pool)]["image_tensors"])
-        else:
-            eng.load_batch(pool[i % len(pool)])
-        run_step()
-
-    for i in range(args.warmup):
-        step(i)
-    stream = torch.cuda.current_stream(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        step(i)
-    ev1.record(stream)
-    t_issue = time.perf_counter() - t0             # host time to issue the K steps (< dt: the host ran ahead)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    gpu_step = ev0.elapsed_time(ev1) * 1e-3 / args.steps       # HIP events on the replay stream
-    if dist:
-        t = torch.tensor([dt, gpu_step], device="cpu" if args.rehearse else dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, gpu_step = float(t[0].item()), float(t[1].item())
+    eng, dps, step = make_step(args, pkg, dev, pool, use_dp, rank, lm)
+    dt, gpu_step, t_issue = time_steps(args, step, dev, dist)
     loss = float(eng.LOSS.item())
     gnorm = eng.last_grad_norm()
     pairs = world * B * args.steps
@@ -560,7 +609,13 @@ def main():
         dist.all_gather(ps, p)
         out["rehearsal_lockstep"] = all(torch.equal(q, ps[0]) for q in ps)
     elif not args.no_kernel_rooflines:
-        out.update(kernel_rooflines(eng, stream, pmc))       # PMC figures: the committed shapes only
+        out.update(kernel_rooflines(eng, torch.cuda.current_stream(dev), pmc))   # PMC: the committed shapes only
+    if world == 1 and not use_dp and not args.no_dp_line and not args.no_graph:
+        # the N > 1 code path at N = 1, a second line beside the headline (same workload, same timing)
+        del eng, dps, step
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        out["dp_world1"] = dp_world1_line(args, pkg, dev, pool, lm, dt)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pkg)
     if rank == 0:

@@ -10,7 +10,7 @@ for rep in $(seq $REPS); do
   for lib in $A $B; do
     i=$((i+1))
     cp $lib $L
-    timeout -k 10 300 python bench.py --no-cpu-baseline --no-kernel-rooflines > gpurun_out/abl_$i.json 2> gpurun_out/abl.err || { echo BENCHFAIL; tail -20 gpurun_out/abl.err; exit 1; }
+    timeout -k 10 300 python bench.py --no-cpu-baseline --no-kernel-rooflines --no-dp-line > gpurun_out/abl_$i.json 2> gpurun_out/abl.err || { echo BENCHFAIL; tail -20 gpurun_out/abl.err; exit 1; }
     echo "[$lib]" $(python -c "import json;d=json.load(open('gpurun_out/abl_$i.json'));print(d['value'], d['ms_per_step'])")
   done
 done
