@@ -340,6 +340,9 @@ def make_step(args, pkg, dev, pool, use_dp, rank, lm):
                                       **({} if args.dp_res_split is None else {"res_split": args.dp_res_split}))
         run_step = dps.step
     else:
+        eng.res_order = getattr(args, "res_order", "first")
+        if args.res_cumask:
+            eng.set_res_cumask(cumask_words(args.res_cumask, torch.cuda.get_device_properties(dev).multi_processor_count))
         if not args.no_graph:
             eng.capture()
         run_step = eng.train_step
@@ -356,6 +359,20 @@ def make_step(args, pkg, dev, pool, use_dp, rank, lm):
             eng.load_batch(pool[i % len(pool)])
         run_step()
     return eng, dps, step
+
+
+def cumask_words(spec, ncu):
+    """--res-cumask SPEC -> CU mask words: 'lo:N' CUs 0..N-1, 'hi:N' the last N, 'st:K:R' the CUs
+    i with i % K < R, 'all'."""
+    kind, *v = spec.split(":")
+    v = [int(x) for x in v]
+    sel = {"all": lambda i: True, "lo": lambda i: i < v[0], "hi": lambda i: i >= ncu - v[0],
+           "st": lambda i: i % v[0] < v[1]}[kind]
+    words = [0] * ((ncu + 31) // 32)
+    for i in range(ncu):
+        if sel(i):
+            words[i // 32] |= 1 << (i % 32)
+    return words
 
 
 def time_steps(args, step, dev, dist):
@@ -457,6 +474,12 @@ def main():
                     help="DP, pipelined: share of the next batch's ResNet calls beside the forward graph (dp.RES_SPLIT)")
     ap.add_argument("--dp-groups", action="store_true",
                     help="the single-GPU engine step with the DP engine's T5 weight-gradient groups (A/B of --dp)")
+    ap.add_argument("--res-cumask", default=None,
+                    help="experiment: the next batch's ResNet on a CU-masked stream beside the chain graph "
+                         "(lo:N | hi:N | st:K:R | all; bench.cumask_words)")
+    ap.add_argument("--res-order", choices=("first", "last", "root"), default="first",
+                    help="experiment: capture the next batch's ResNet branch before (default) or after the chain; "
+                         "root: F4 <- F4N issued before the replay, both branches graph roots")
     ap.add_argument("--no-dp-line", action="store_true",
                     help="N = 1: skip the second timing of the same workload through the N > 1 code path "
                          "(dp.DataParallelStep over a world-1 RCCL group; JSON key dp_world1)")

@@ -258,6 +258,7 @@ class VQAEngine:
         self._side = torch.cuda.Stream(self.dev)
         self._wside = torch.cuda.Stream(self.dev)
         self._rstream = torch.cuda.Stream(self.dev)
+        self.res_external = False        # set_res_cumask: the ResNet launched eagerly beside the graph
         self._scratch = None             # split-K workspace used while autotuning
 
     @classmethod
@@ -1413,30 +1414,78 @@ class VQAEngine:
                 self._run(calls[i:j])
             i = j
 
+    def set_res_cumask(self, words):
+        """Experiment (bench.py --res-cumask): run the next batch's ResNet on a stream restricted
+        to the CUs whose bits are set in `words` (hipExtStreamCreateWithCUMask, 32 CUs per word),
+        launched eagerly beside the step graph, which then holds the chain only.  Call before
+        capture().  Ordering as in the graph: F4 <- F4N, then the ResNet may overwrite F4N; the
+        next step's inputs wait for it."""
+        hip = L.hip_runtime()
+        s = ctypes.c_void_p()
+        arr = (ctypes.c_uint32 * len(words))(*words)
+        with torch.cuda.device(self.dev):
+            rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(len(words)), arr)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+        self._rstream_handle = s                      # lives as long as the engine's process
+        self._rstream = torch.cuda.ExternalStream(s.value, device=self.dev)
+        self.res_external = True
+
+    def _res_external_step(self):
+        main = torch.cuda.current_stream(self.dev)
+        self.copy_f4(L.stream_handle(main))
+        fork = torch.cuda.Event()
+        fork.record(main)
+        for g in self.graph:
+            g.replay()
+        self._rstream.wait_event(fork)
+        with torch.cuda.stream(self._rstream):
+            self._run(self.res_calls)
+        join = torch.cuda.Event()
+        join.record(self._rstream)
+        main.wait_event(join)
+
     def _step_pipelined(self):
         """One pipelined step: F4 <- F4N (features of this batch, made last step), then the
         ResNet of the next batch (IMG -> F4N) on its own stream, concurrently with this
         step's whole chain on the current stream; joined at the end.  The two sides share
         no buffer, so every result equals the unpipelined step's bit for bit."""
         main = torch.cuda.current_stream(self.dev)
-        self.copy_f4(L.stream_handle(main))
+        if self.res_external:                              # the chain only (set_res_cumask)
+            self.run_forward_streams()
+            self.run_backward_streams(sq_overlap=True)
+            self._run(self.opt_calls[2:])
+            return
+        if not (torch.cuda.is_current_stream_capturing() and getattr(self, "res_order", "first") == "root"):
+            self.copy_f4(L.stream_handle(main))            # ("root": issued before the replay, train_step)
         fork = torch.cuda.Event()
         fork.record(main)
         self._rstream.wait_event(fork)
 
         # the ResNet branch is captured first: a replayed graph submits nodes in capture order,
         # and issuing it after T5 layer 0 / 1 / 3 measured 0.7 ms slower (DESIGN §3.8)
-        with torch.cuda.stream(self._rstream):
-            self._run(self.res_calls)
+        # (res_order "last": the same dependencies, the ResNet's nodes created after the chain's)
+        last = getattr(self, "res_order", "first") == "last"
+        if not last:
+            with torch.cuda.stream(self._rstream):
+                self._run(self.res_calls)
         self.run_forward_streams()                         # ConvTranspose2d || T5 encoder, then SGA
         self.run_backward_streams(sq_overlap=True)
         self._run(self.opt_calls[2:])
+        if last:
+            with torch.cuda.stream(self._rstream):
+                self._run(self.res_calls)
         join = torch.cuda.Event()
         join.record(self._rstream)
         main.wait_event(join)
 
     def train_step(self):
         """zero_grad -> forward -> backward -> (all-reduce) -> clip -> AdamW -> sched, all on-device."""
+        if self.graph is not None and self.res_external:
+            self._res_external_step()
+            return
+        if self.graph is not None and self.pipeline and getattr(self, "res_order", "first") == "root":
+            self.copy_f4(L.stream_handle(torch.cuda.current_stream(self.dev)))
         if self.graph is not None:
             for g in self.graph:
                 if callable(g):

@@ -208,6 +208,18 @@ def ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def hip_runtime():
+    """The HIP runtime library this process already runs (torch's copy), for the few runtime
+    entry points torch does not wrap (hipExtStreamCreateWithCUMask)."""
+    import torch
+    torch.cuda.init()
+    with open("/proc/self/maps") as f:
+        paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
+    if not paths:
+        raise RuntimeError("libamdhip64.so is not mapped in this process")
+    return ctypes.CDLL(sorted(paths)[0])
+
+
 def stream_handle(stream=None):
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
