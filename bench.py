@@ -341,6 +341,7 @@ def make_step(args, pkg, dev, pool, use_dp, rank, lm):
         run_step = dps.step
     else:
         eng.res_order = getattr(args, "res_order", "first")
+        eng.res_head = getattr(args, "res_head", 4)
         if args.res_cumask:
             eng.set_res_cumask(cumask_words(args.res_cumask, torch.cuda.get_device_properties(dev).multi_processor_count))
         if not args.no_graph:
@@ -477,9 +478,13 @@ def main():
     ap.add_argument("--res-cumask", default=None,
                     help="experiment: the next batch's ResNet on a CU-masked stream beside the chain graph "
                          "(lo:N | hi:N | st:K:R | all; bench.cumask_words)")
-    ap.add_argument("--res-order", choices=("first", "last", "root"), default="first",
+    ap.add_argument("--res-order", choices=("first", "last", "root", "interleave"), default="first",
                     help="experiment: capture the next batch's ResNet branch before (default) or after the chain; "
                          "root: F4 <- F4N issued before the replay, both branches graph roots")
+    ap.add_argument("--res-head", type=int, default=4,
+                    help="--res-order interleave: ResNet calls issued before the T5 encoder's first layer")
+    ap.add_argument("--main-stream", choices=("default", "side"), default="default",
+                    help="experiment: issue the step on torch's default stream or on a stream of its own")
     ap.add_argument("--no-dp-line", action="store_true",
                     help="N = 1: skip the second timing of the same workload through the N > 1 code path "
                          "(dp.DataParallelStep over a world-1 RCCL group; JSON key dp_world1)")
@@ -508,6 +513,8 @@ def main():
         local = 0                                          # every rank shares the one GPU (gloo, host-staged)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.main_stream == "side":
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
     if args.model == "vit":
         if world != 1:
             raise SystemExit("bench --model vit: BASELINE configs[3] is a 1-GPU configuration")

@@ -138,10 +138,13 @@ typedef struct vqa_gemm_desc {
 /* tile configs: 1 128x128/3 stages, 2 128x64/4, 3 64x64/4, 4 64x64/2, 5 64x64/3, 6 128x64/2,
  * 7 64x128/2, 8 128x128/2 (4 waves); 9 256x128/2, 10 128x256/2, 11 256x256/2, 12 256x128/3 (8 waves);
  * 13..16 64x192 / 128x192 (k-contiguous B only); 17..20 the LDS-patch convolution;
- * 21 64x64/2, 22 64x128/2, 23 128x64/2 with 128-deep k-tiles (no implicit im2col, no split-K) */
-#define VQA_GEMM_CONFIGS 24
-#define VQA_GEMM_PATCH_FIRST 17    /* configs 17..20: a_conv = 2 only */
+ * 21 64x64/2, 22 64x128/2, 23 128x64/2 with 128-deep k-tiles (no implicit im2col, no split-K);
+ * 24 64x128/2 with 8 waves (2x4) and 128-deep k-tiles; 25 the LDS-patch convolution's 128x128 tile
+ * with 8 waves (4x2) */
+#define VQA_GEMM_CONFIGS 25
+#define VQA_GEMM_PATCH_FIRST 17    /* configs 17..20 and VQA_GEMM_PATCH_WIDE: a_conv = 2 only */
 #define VQA_GEMM_PATCH_LAST 20
+#define VQA_GEMM_PATCH_WIDE 25
 int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream);
 /* Row-wise e4m3 quantisation for vqa_gemm_desc.fp8: per row r of x (fp32, or bf16 when
  * x_bf16), scale[r] = max_c |x[r][c]| / 448 (1 for an all-zero row) and

@@ -190,7 +190,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv_patch_kernel(GemmParams P
 constexpr int PMAX_SB = 272;     // single chunk (C = 64): W = 56 / 64 at R = 2 -> 232 / 264 pixels
 constexpr int PMAX_DB = 208;     // double-buffered chunks: W <= 32 at BM = 128 -> <= 204 pixels
 
-template <int BM, int BN>
+template <int BM, int BN, int NWM = 2, int NWN = 2>
 int launch_patch(GemmParams& P, const PatchGeom& G, hipStream_t s) {
   P.tiles_m = P.ga.n * G.rbs;
   P.tiles_n = vqa::cdiv(P.n, BN);
@@ -199,10 +199,10 @@ int launch_patch(GemmParams& P, const PatchGeom& G, hipStream_t s) {
     if (G.npix > PMAX_SB) return vqa::fail(VQA_ERR_INVALID, "vqa_gemm(a_conv=2): patch of %d pixels > %d", G.npix, PMAX_SB);
     // one chunk: 2 B stages keep the block small (3 blocks / CU at BN = 64; measured 29.7 vs
     // 37.5 us at 3 stages for the layer1 3x3 conv, 44.6 us for the implicit-im2col path)
-    hipLaunchKernelGGL((conv_patch_kernel<BM, BN, 2, 2, PMAX_SB, false, 2>), grid, dim3(256), 0, s, P, G);
+    hipLaunchKernelGGL((conv_patch_kernel<BM, BN, NWM, NWN, PMAX_SB, false, 2>), grid, dim3(64 * NWM * NWN), 0, s, P, G);
   } else {
     if (G.npix > PMAX_DB) return vqa::fail(VQA_ERR_INVALID, "vqa_gemm(a_conv=2): patch of %d pixels > %d", G.npix, PMAX_DB);
-    hipLaunchKernelGGL((conv_patch_kernel<BM, BN, 2, 2, PMAX_DB, true, 3>), grid, dim3(256), 0, s, P, G);
+    hipLaunchKernelGGL((conv_patch_kernel<BM, BN, NWM, NWN, PMAX_DB, true, 3>), grid, dim3(64 * NWM * NWN), 0, s, P, G);
   }
   return vqa::check_launch("vqa_gemm(a_conv=2)");
 }
@@ -224,7 +224,7 @@ static int conv_patch_dispatch(GemmParams& P, int config, hipStream_t s) {
   VQA_REQUIRE(g.c % 64 == 0 && P.k == 9 * g.c && P.m == g.n * g.h * g.w, "vqa_gemm(a_conv=2): C %% 64, K = 9C, M = NHW");
   VQA_REQUIRE(P.splitk <= 1 && P.alpha == 1.f, "vqa_gemm(a_conv=2): no split-K, alpha = 1");
   int bm = (config == 19 || config == 20) ? 64 : 128;
-  const int bn = (config == 18 || config == 20) ? 128 : 64;
+  const int bn = (config == 18 || config == 20 || config == 25) ? 128 : 64;
   // a 128-row tile whose input patch exceeds the LDS buffer (e.g. C >= 128 at W 40-42 or 51-64,
   // where R = 128 / W leaves (R + 2)(W + 2) > PMAX_DB) runs as the 64-row tile: the tile
   // configs give the same bits, so this changes speed only
@@ -237,6 +237,10 @@ static int conv_patch_dispatch(GemmParams& P, int config, hipStream_t s) {
   G.pins = vqa::cdiv(G.npix, 8);
   G.chunks = g.c / 64;
   G.ppart = vqa::cdiv(G.pins, 10 - 3);          // double-buffered: parts on taps S-1..8 at S = 3 stages
+  // config 25: 8 waves -- 4 x 2 on the 128 x 128 tile (the layer2 / layer3 3x3 convs: 31.8 vs
+  // 36.6 us at 14 x 14 x 256, 35.7 vs 38.5 at 28 x 28 x 128, profiles/r05_conv_patch_micro.txt),
+  // 2 x 4 when the patch needs the 64-row tile
+  if (config == 25) return bm == 128 ? launch_patch<128, 128, 4, 2>(P, G, s) : launch_patch<64, 128, 2, 4>(P, G, s);
   if (bm == 128 && bn == 64) return launch_patch<128, 64>(P, G, s);
   if (bm == 128) return launch_patch<128, 128>(P, G, s);
   if (bn == 64) return launch_patch<64, 64>(P, G, s);

@@ -127,7 +127,8 @@ void tile_of(int config, int& bm, int& bn) {
                                                  {64, 64},   {128, 64},  {64, 128}, {128, 128}, {256, 128},
                                                  {128, 256}, {256, 256}, {256, 128}, {64, 192}, {128, 192},
                                                  {64, 192},  {128, 192}, {128, 64}, {128, 128}, {64, 64},
-                                                 {64, 128},  {64, 64},   {64, 128}, {128, 64}, {64, 128}};
+                                                 {64, 128},  {64, 64},   {64, 128}, {128, 64}, {64, 128},
+                                                 {128, 128}};
   bm = T[config][0];
   bn = T[config][1];
 }
@@ -263,7 +264,7 @@ extern "C" int vqa_gemm(const vqa_gemm_desc* d, hipStream_t stream) {
   const int batch = d->batch, cfg = d->config;
   if (d->fp8) return vqa_gemm_fp8_dispatch(&P, batch, cfg, stream);
   const bool akc = !d->a_trans, bkc = !d->b_trans;
-  const bool patch_cfg = cfg >= VQA_GEMM_PATCH_FIRST && cfg <= VQA_GEMM_PATCH_LAST;
+  const bool patch_cfg = (cfg >= VQA_GEMM_PATCH_FIRST && cfg <= VQA_GEMM_PATCH_LAST) || cfg == VQA_GEMM_PATCH_WIDE;
   if (d->a_conv == 2) {                                   // LDS-patch 3x3 convolution (conv_patch.inl)
     VQA_REQUIRE(akc && bkc && !d->b_conv && batch == 1, "vqa_gemm(a_conv=2): k-contiguous B, batch 1");
     VQA_REQUIRE(cfg == 0 || patch_cfg, "vqa_gemm(a_conv=2): tile config %d is not a patch config (%d..%d)", cfg,

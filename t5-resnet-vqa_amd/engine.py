@@ -1319,6 +1319,14 @@ class VQAEngine:
         vpost = vis[self._fvis_param - p0:]                # ConvTranspose2d + SGA block 0 k/v
         bounds = starts + [len(txt)]
         j = 0
+        feed = getattr(self, "_res_feed", None)            # the next batch's ResNet (res_order interleave)
+        nres = len(feed[0]) if feed else 0
+        head = min(nres, getattr(self, "res_head", 4))
+
+        def res_upto(n):
+            while feed and feed[0] and nres - len(feed[0]) < n:
+                feed[0].pop(0)(feed[1])
+        res_upto(head)
         for t in range(bounds[0]):                         # embedding + rel-bias
             txt[t](hs)
         for i in range(nl):
@@ -1327,6 +1335,7 @@ class VQAEngine:
             side.wait_event(ev[f"t5.{i}"])
             for t in range(bounds[i], bounds[i + 1]):
                 txt[t](hs)
+            res_upto(head + (i + 1) * (nres - head) // nl)
             # the ResNet calls spread over the layers (as in the plain interleave); the
             # parameter-reading vision calls follow the last of them (they read its output)
             while j < (i + 1) * len(vpre) // nl:
@@ -1466,10 +1475,16 @@ class VQAEngine:
         # and issuing it after T5 layer 0 / 1 / 3 measured 0.7 ms slower
         # (res_order "last": the same dependencies, the ResNet's nodes created after the chain's)
         last = getattr(self, "res_order", "first") == "last"
-        if not last:
+        inter = getattr(self, "res_order", "first") == "interleave"
+        if inter:                    # issued between the T5 encoder layers (_forward_branches_deferred)
+            self._res_feed = [list(self.res_calls), L.stream_handle(self._rstream)]
+        elif not last:
             with torch.cuda.stream(self._rstream):
                 self._run(self.res_calls)
         self.run_forward_streams()                         # ConvTranspose2d || T5 encoder, then SGA
+        if inter:
+            assert not self._res_feed[0], "every ResNet call issued"
+            self._res_feed = None
         self.run_backward_streams(sq_overlap=True)
         self._run(self.opt_calls[2:])
         if last:

@@ -6,7 +6,8 @@ tracer hides the effect: DESIGN §5):
   R  the ResNet alone, eager on the dedicated-queue stream
   R0 the ResNet alone, eager on an ordinary torch stream (shares the 4 default queues)
   AR both, as the --res-cumask step issues them
-  python tools/cumask_probe.py [SPEC]        (SPEC as bench.py --res-cumask, default all)
+  [MAIN_SIDE=1] python tools/cumask_probe.py [SPEC]   (SPEC as bench.py --res-cumask, default all;
+                                                       MAIN_SIDE: the step on a non-default stream)
 """
 import json
 import os
@@ -24,6 +25,8 @@ spec = sys.argv[1] if len(sys.argv) > 1 else "all"
 pkg = load_package()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
+if os.environ.get("MAIN_SIDE"):                  # issue everything on a stream of its own, not the null stream
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
 args = types.SimpleNamespace(batch=64, seq_len=32, image_size=224, blocks=3, no_pipeline=False, dp_groups=False,
                              config5=False, tune_table=os.path.join(ROOT, "t5-resnet-vqa_amd", "tuning",
                                                                     "gemm_gfx950.json"),
@@ -65,7 +68,7 @@ def res_on(s):
     return f
 
 
-out = {"spec": spec,
+out = {"spec": spec, "main_stream": "side" if os.environ.get("MAIN_SIDE") else "default",
        "A_chain_graph_ms": timed(chain),
        "R_resnet_dedicated_queue_ms": timed(res_on(eng._rstream), streams=(eng._rstream,)),
        "R0_resnet_shared_queue_ms": timed(res_on(plain), streams=(plain,)),
