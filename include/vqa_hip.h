@@ -279,6 +279,10 @@ int vqa_colsum_batched(const vqa_colsum_job* jobs, int njobs, int nblocks, hipSt
  *   over Z with W'[o,a,e,(2p+q)*3+c] = W[o,c,2a+p,2e+q] (0 at index 7).
  *   H and W must be even.
  * vqa_maxpool3x3s2_nhwc: torchvision ResNet maxpool (3, 2, pad 1), bf16 NHWC.
+ * vqa_subsample_nhwc: y[((b*oh + i)*ow + j)*ldy + c] = x[b, i*stride, j*stride, c] (bf16 NHWC,
+ *   oh = (h-1)/stride + 1; c and ldy multiples of 8, y 16-B aligned): the input of a bottleneck's
+ *   1x1 downsample placed beside conv2's output, so conv3 + downsample run as ONE GEMM over the
+ *   concatenated K (torchvision Bottleneck: out = relu(bn3(conv3(t)) + bn(downsample(x)))).
  * vqa_colsum: out[c] = beta*out[c] + sum_r x[r*ld + c] (bias gradients of
  *   every nn.Linear / ConvTranspose2d), ws = vqa_colsum_workspace_floats().
  * vqa_embedding_fwd/bwd: T5 embed_tokens gather (TF modeling_t5.py:678) and
@@ -290,6 +294,8 @@ int vqa_colsum_batched(const vqa_colsum_job* jobs, int njobs, int nblocks, hipSt
 int vqa_image_to_nhwc8(const float* img, void* out, int n, int h, int w, hipStream_t stream);
 int vqa_image_to_s2d16(const float* img, void* out, int n, int h, int w, hipStream_t stream);
 int vqa_maxpool3x3s2_nhwc(const void* x, void* y, int n, int h, int w, int c, int oh, int ow, hipStream_t stream);
+int vqa_subsample_nhwc(const void* x, int n, int h, int w, int c, int stride, void* y, long long ldy,
+                       hipStream_t stream);
 int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long long ld, float* out, float beta, float* ws,
                hipStream_t stream);
 int vqa_colsum_workspace_floats(int rows, int cols);

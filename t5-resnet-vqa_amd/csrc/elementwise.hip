@@ -403,6 +403,34 @@ extern "C" int vqa_maxpool3x3s2_nhwc(const void* x, void* y, int n, int h, int w
   return vqa::check_launch("vqa_maxpool3x3s2_nhwc");
 }
 
+namespace {
+// x[b, i*s, j*s, :] -> row (b, i, j) of y (row stride ldy); 8 channels (16 B) per thread
+__global__ __launch_bounds__(256) void subsample_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, int h,
+                                                        int w, int c8, int s, int oh, int ow, long ldy8, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int cc = (int)(i % c8);
+  const long r = i / c8;                              // output row (b, oy, ox)
+  const int ox = (int)(r % ow);
+  const long t = r / ow;
+  const int oy = (int)(t % oh);
+  const long b = t / oh;
+  y[r * ldy8 + cc] = x[((b * h + (long)oy * s) * w + (long)ox * s) * c8 + cc];
+}
+}  // namespace
+
+extern "C" int vqa_subsample_nhwc(const void* x, int n, int h, int w, int c, int stride, void* y, long long ldy,
+                                  hipStream_t s) {
+  VQA_REQUIRE(x && y && n > 0 && h > 0 && w > 0 && stride >= 1 && c % 8 == 0 && ldy % 8 == 0 && ldy >= c &&
+                  ((uintptr_t)y & 15) == 0 && ((uintptr_t)x & 15) == 0,
+              "vqa_subsample_nhwc: bad arguments (c, ldy multiples of 8, 16-B aligned buffers)");
+  const int oh = (h - 1) / stride + 1, ow = (w - 1) / stride + 1;
+  const long total = (long)n * oh * ow * (c / 8);
+  hipLaunchKernelGGL(subsample_kernel, dim3(vqa::cdiv(total, 256)), dim3(256), 0, s, (const uint4*)x, (uint4*)y, h, w,
+                     c / 8, stride, oh, ow, (long)(ldy / 8), total);
+  return vqa::check_launch("vqa_subsample_nhwc");
+}
+
 extern "C" int vqa_colsum_workspace_floats(int rows, int cols) { return vqa::cdiv(rows, COLSUM_ROWS) * cols; }
 extern "C" int vqa_colsum_parts(int rows) { return vqa::cdiv(rows, COLSUM_ROWS); }
 

@@ -366,6 +366,30 @@ class VQAEngine:
             t1, t2, ds, y = free[0], free[1], free[2], free[3]
             if idx == nblocks_total - 1:
                 y = self.F4N
+            fuse = bottleneck and (vm + p + "downsample.0.weight") in sd and os.environ.get("VQA_RES_FUSE_DS", "1") != "0"
+            if fuse:
+                # conv3 and the 1x1 downsample as ONE GEMM over the concatenated K (r05):
+                # [conv2 out | x subsampled] . [W3 | Wd]^T + (b3 + bd), ReLU -- conv2 writes the
+                # first `planes` columns of the `ds` buffer, vqa_subsample_nhwc the other `ci`;
+                # the downsample's output never goes to HBM and one launch goes away
+                kc = planes + ci
+                w, b = conv_w(p + "conv1", p + "bn1")
+                self._conv(x, (B, hi, hi, ci), w, b, 1, 0, t1, relu=True)
+                w, b = conv_w(p + "conv2", p + "bn2")
+                self._conv(t1, (B, hi, hi, planes), w, b, stride, 1, ds, relu=True, ldc16=kc)
+                self.res_calls.append(ops.Call("vqa_subsample_nhwc", x.data_ptr(), B, hi, hi, ci, stride,
+                                               ops.addr(ds, planes), kc, keep=(x, ds)))
+                w3, b3 = conv_w(p + "conv3", p + "bn3")
+                wd, bd = conv_w(p + "downsample.0", p + "downsample.1")
+                wcat = torch.cat([w3.reshape(out, planes), wd.reshape(out, ci)], dim=1).contiguous()
+                bcat = b3 + bd
+                self._res_keep += [wcat, bcat]
+                self._gemm(self.res_calls, ds, wcat, B * ho * ho, out, kc, lda=kc, ldb=kc, c16=y, ldc16=out,
+                           bias=bcat, relu=True)
+                if y is not self.F4N:
+                    free = [x, t1, t2, ds]
+                    x = y
+                continue
             if bottleneck:
                 w, b = conv_w(p + "conv1", p + "bn1")
                 self._conv(x, (B, hi, hi, ci), w, b, 1, 0, t1, relu=True)
@@ -390,7 +414,7 @@ class VQAEngine:
                 free = [x, t1, t2, ds]
                 x = y
 
-    def _conv(self, x, shape, w16, b32, stride, pad, out, relu, res16=None):
+    def _conv(self, x, shape, w16, b32, stride, pad, out, relu, res16=None, ldc16=None):
         n, h, w, c = shape
         cout, kh, kw, _ = w16.shape
         oh = (h + 2 * pad - kh) // stride + 1
@@ -404,7 +428,7 @@ class VQAEngine:
             w16 = w16.reshape(cout, 9, c // 64, 64).permute(0, 2, 1, 3).contiguous().reshape(cout, kh, kw, c)
             self._res_keep.append(w16)
         self._gemm(self.res_calls, x, w16, n * oh * oh, cout, kh * kw * c, lda=kh * kw * c, ldb=kh * kw * c, ga=g,
-                   c16=out, ldc16=cout, bias=b32, relu=relu, res16=res16, ldres=cout, a_patch=patch)
+                   c16=out, ldc16=ldc16 or cout, bias=b32, relu=relu, res16=res16, ldres=cout, a_patch=patch)
 
     def _alloc_activations(self):
         D = self.D

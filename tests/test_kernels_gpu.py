@@ -355,6 +355,20 @@ def test_image_and_maxpool(k):
     assert torch.equal(y.float(), ref)
 
 
+@pytest.mark.parametrize("n,h,c,s", [(2, 7, 64, 1), (3, 13, 256, 2), (2, 56, 64, 1), (1, 28, 512, 2)])
+def test_subsample_into_concatenated_rows(k, n, h, c, s):
+    """vqa_subsample_nhwc: x[:, ::s, ::s, :] written beside other columns (row stride ldy), the
+    second half of the fused conv3 + downsample GEMM's A operand -- exact, and the columns left
+    of it untouched."""
+    x = rnd((n, h, h, c), 37, dtype=torch.bfloat16)
+    oh = (h - 1) // s + 1
+    left = 64
+    y = torch.full((n * oh * oh, left + c), 7.0, device="cuda", dtype=torch.bfloat16)
+    run(k, "vqa_subsample_nhwc", x, n, h, h, c, s, k.ops.addr(y, left), left + c)
+    assert torch.equal(y[:, left:], x[:, ::s, ::s, :].reshape(-1, c))
+    assert torch.equal(y[:, :left], torch.full_like(y[:, :left], 7.0))
+
+
 @pytest.mark.parametrize("n,h,w,c", [(3, 7, 7, 768), (2, 5, 9, 24)])
 def test_tap_shift_and_tap_batched_conv_transpose_dw(k, n, h, w, c):
     """vqa_tap_shift's 3x3 shifted copies (exact), and the scaler weight gradient as the
