@@ -296,6 +296,18 @@ int vqa_image_to_s2d16(const float* img, void* out, int n, int h, int w, hipStre
 int vqa_maxpool3x3s2_nhwc(const void* x, void* y, int n, int h, int w, int c, int oh, int ow, hipStream_t stream);
 int vqa_subsample_nhwc(const void* x, int n, int h, int w, int c, int stride, void* y, long long ldy,
                        hipStream_t stream);
+/* vqa_stem_s2d_conv: the ResNet stem (conv1 7x7/2 pad 3 + folded bn1 + ReLU) as the 4x4 / stride-1 /
+ *   pad-1 convolution over the space-to-depth image z [n][hz][hz][16] bf16 (vqa_image_to_s2d16) with
+ *   weights w [64][4][4][16] bf16 and bias [64] fp32, into y [n][oh][oh][64] bf16; oh % 16 == 0,
+ *   hz == oh + 1, 16-B aligned buffers.  The input patch of each 8 x 16 output block is staged in LDS
+ *   once (the implicit GEMM re-reads every pixel per tap); bit-identical to vqa_gemm's a_conv = 1 form. */
+int vqa_stem_s2d_conv(const void* z, const void* w, const float* bias, void* y, int n, int hz, int oh,
+                      hipStream_t stream);
+/* vqa_stem_pool_s2d: vqa_stem_s2d_conv followed by vqa_maxpool3x3s2_nhwc in one pass, bit-identical:
+ *   y [n][oh/2][oh/2][64] bf16 (the pooled map only; the stem map is never stored); oh / 2 a multiple
+ *   of 8, hz == oh + 1, 16-B aligned buffers. */
+int vqa_stem_pool_s2d(const void* z, const void* w, const float* bias, void* y, int n, int hz, int oh,
+                      hipStream_t stream);
 int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long long ld, float* out, float beta, float* ws,
                hipStream_t stream);
 int vqa_colsum_workspace_floats(int rows, int cols);

@@ -354,10 +354,22 @@ class VQAEngine:
         self.res_calls.append(ops.Call("vqa_image_to_s2d16", self.IMG.data_ptr(), self.IMG8.data_ptr(), B, H, H,
                                        keep=(self.IMG, self.IMG8)))
         g = ops.conv_geom(B, hz, hz, 16, h1, h1, 4, 4, 1, 1)
-        self._gemm(self.res_calls, self.IMG8, w16, B * h1 * h1, 64, 256, lda=256, ldb=256, ga=g,
-                   c16=bufs[0], ldc16=64, bias=b32, relu=True)
-        self.res_calls.append(ops.Call("vqa_maxpool3x3s2_nhwc", bufs[0].data_ptr(), bufs[1].data_ptr(), B, h1, h1,
-                                       64, h2, h2, keep=(bufs[0], bufs[1])))
+        stem = os.environ.get("VQA_STEM", "pool")           # pool | patch | gemm (A/B switches)
+        if stem == "pool" and h1 % 16 == 0 and hz == h1 + 1 and h2 == h1 // 2:
+            # stem + maxpool in one pass from LDS input patches (csrc/stem.hip): only the pooled
+            # map is written; bit-identical to the implicit GEMM + vqa_maxpool3x3s2_nhwc below
+            self.res_calls.append(ops.Call("vqa_stem_pool_s2d", self.IMG8.data_ptr(), w16.data_ptr(), b32.data_ptr(),
+                                           bufs[1].data_ptr(), B, hz, h1, keep=(self.IMG8, w16, b32, bufs[1])))
+        else:
+            if stem in ("pool", "patch") and h1 % 16 == 0 and hz == h1 + 1:
+                self.res_calls.append(ops.Call("vqa_stem_s2d_conv", self.IMG8.data_ptr(), w16.data_ptr(),
+                                               b32.data_ptr(), bufs[0].data_ptr(), B, hz, h1,
+                                               keep=(self.IMG8, w16, b32, bufs[0])))
+            else:
+                self._gemm(self.res_calls, self.IMG8, w16, B * h1 * h1, 64, 256, lda=256, ldb=256, ga=g,
+                           c16=bufs[0], ldc16=64, bias=b32, relu=True)
+            self.res_calls.append(ops.Call("vqa_maxpool3x3s2_nhwc", bufs[0].data_ptr(), bufs[1].data_ptr(), B, h1,
+                                           h1, 64, h2, h2, keep=(bufs[0], bufs[1])))
         x = bufs[1]
         free = [bufs[0], bufs[2], bufs[3], bufs[4]]
         nblocks_total = len(plan)

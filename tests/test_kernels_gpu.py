@@ -531,3 +531,41 @@ def test_norm_and_embedding_dropout_hooks(k):
     run(k, "vqa_embedding_fwd", ids, table, out, T, D, Vv, pa(dC))
     torch.cuda.synchronize()
     torch.testing.assert_close(out, table[ids] * mult(42))
+
+
+@pytest.mark.parametrize("n,oh", [(2, 112), (3, 32), (1, 192)])
+def test_stem_patch_conv_equals_the_implicit_gemm(k, n, oh):
+    """vqa_stem_s2d_conv (LDS-patch stem) against the implicit-im2col vqa_gemm the engine used
+    before r05 (4x4 / stride 1 / pad 1 over the space-to-depth image, bias, ReLU): bit for bit."""
+    ops = k.ops
+    hz = oh + 1
+    z = rnd((n, hz, hz, 16), 51, dtype=torch.bfloat16)
+    w = rnd((64, 4, 4, 16), 52, scale=0.1, dtype=torch.bfloat16)
+    b = rnd(64, 53)
+    y_ref = torch.empty(n, oh, oh, 64, device="cuda", dtype=torch.bfloat16)
+    g = ops.conv_geom(n, hz, hz, 16, oh, oh, 4, 4, 1, 1)
+    ops.run(ops.gemm_desc(z, w, n * oh * oh, 64, 256, lda=256, ldb=256, ga=g, c16=y_ref, ldc16=64, bias=b, relu=True))
+    y = torch.full_like(y_ref, 3.0)
+    run(k, "vqa_stem_s2d_conv", z, w, b, y, n, hz, oh)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+
+
+@pytest.mark.parametrize("n,oh", [(2, 112), (3, 32), (1, 192), (2, 16)])
+def test_stem_pool_equals_stem_then_maxpool(k, n, oh):
+    """vqa_stem_pool_s2d (stem + 3x3/2 maxpool fused, only the pooled map written) against the
+    implicit-GEMM stem followed by vqa_maxpool3x3s2_nhwc: bit for bit, borders included."""
+    ops = k.ops
+    hz, ph = oh + 1, oh // 2
+    z = rnd((n, hz, hz, 16), 54, dtype=torch.bfloat16)
+    w = rnd((64, 4, 4, 16), 55, scale=0.1, dtype=torch.bfloat16)
+    b = rnd(64, 56)
+    s = torch.empty(n, oh, oh, 64, device="cuda", dtype=torch.bfloat16)
+    g = ops.conv_geom(n, hz, hz, 16, oh, oh, 4, 4, 1, 1)
+    ops.run(ops.gemm_desc(z, w, n * oh * oh, 64, 256, lda=256, ldb=256, ga=g, c16=s, ldc16=64, bias=b, relu=True))
+    ref = torch.empty(n, ph, ph, 64, device="cuda", dtype=torch.bfloat16)
+    run(k, "vqa_maxpool3x3s2_nhwc", s, ref, n, oh, oh, 64, ph, ph)
+    y = torch.full_like(ref, 5.0)
+    run(k, "vqa_stem_pool_s2d", z, w, b, y, n, hz, oh)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
