@@ -19,6 +19,7 @@ namespace {
 
 typedef int i32x4s_t __attribute__((ext_vector_type(4)));
 
+constexpr int STEM_CUS = 256;                  // MI355X compute units (the persistent grids' size)
 constexpr int SR = 8, SC = 16;                 // output rows x columns per workgroup
 constexpr int PR = SR + 3, PC = SC + 3;        // input patch rows x columns (4 x 4 taps, pad 1)
 constexpr int PATCH_BYTES = PR * PC * 32;      // 32 B per pixel: 16 bf16 channels
@@ -290,16 +291,10 @@ extern "C" int vqa_stem_s2d_conv(const void* z, const void* w, const float* bias
                   ((uintptr_t)y & 15) == 0,
               "vqa_stem_s2d_conv: 16-B aligned buffers needed");
   const int ntiles = n * (oh / SR) * (oh / SC);
-  // persistent: two workgroups per CU (the kernel's occupancy: 161 VGPRs + 32 AGPRs), a multiple
-  // of 8 XCDs
-  static const int cus = [] {
-    int dev = 0, n = 256;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      n = 256;
-    return n;
-  }();
-  const int grid = std::min(ntiles, 2 * cus) / 8 * 8 > 0 ? std::min(ntiles, 2 * cus) / 8 * 8 : ntiles;
+  // persistent: two workgroups per CU of the MI355X's 256 (the kernel's occupancy: 161 VGPRs + 32
+  // AGPRs), a multiple of 8 XCDs.  (No runtime query here: this launch is also captured into the
+  // step graph, and a device-attribute call inside a stream capture is best avoided.)
+  const int grid = std::min(ntiles, 2 * STEM_CUS) / 8 * 8 > 0 ? std::min(ntiles, 2 * STEM_CUS) / 8 * 8 : ntiles;
   hipLaunchKernelGGL(stem_patch_kernel, dim3(grid), dim3(256), 0, s, (const uint4*)z, (const bf16_t*)w, bias,
                      (bf16_t*)y, hz, oh, oh, ntiles);
   return vqa::check_launch("vqa_stem_s2d_conv");
@@ -315,14 +310,7 @@ extern "C" int vqa_stem_pool_s2d(const void* z, const void* w, const float* bias
                   ((uintptr_t)y & 15) == 0,
               "vqa_stem_pool_s2d: 16-B aligned buffers needed");
   const int ntiles = n * (ph / PY) * (ph / PX);
-  static const int cus = [] {
-    int dev = 0, m = 256;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&m, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      m = 256;
-    return m;
-  }();
-  const int grid = std::min(ntiles, 2 * cus) / 8 * 8 > 0 ? std::min(ntiles, 2 * cus) / 8 * 8 : ntiles;
+  const int grid = std::min(ntiles, 2 * STEM_CUS) / 8 * 8 > 0 ? std::min(ntiles, 2 * STEM_CUS) / 8 * 8 : ntiles;
   hipLaunchKernelGGL(stem_pool_kernel, dim3(grid), dim3(256), 0, s, (const uint4*)z, (const bf16_t*)w, bias,
                      (bf16_t*)y, hz, oh, ph, ntiles);
   return vqa::check_launch("vqa_stem_pool_s2d");
