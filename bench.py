@@ -157,6 +157,21 @@ def call_bytes(c):
     if n == "vqa_embedding_zero_rows":                              # prev, cur, tokens, dtable, d, ...
         t, dd = c.args[2], c.args[4]
         return float(2 * t * 8 + t * dd * 4)
+    # calls whose `keep` holds whole arenas or the ResNet's max-size ping-pong buffers: the bytes
+    # they actually touch, from their arguments
+    if n == "vqa_quant_rows_fp8":                                   # x, x_bf16, ldx, rows, cols, q, ldq, scale
+        rows, cols = c.args[3], c.args[4]
+        return float(rows * cols * (2 if c.args[1] else 4) + rows * cols + rows * 4)
+    if n in ("vqa_stem_pool_s2d", "vqa_stem_s2d_conv"):             # z, w, bias, y, n, hz, oh
+        nb, hz, oh = c.args[4], c.args[5], c.args[6]
+        oy = oh // 2 if n == "vqa_stem_pool_s2d" else oh
+        return float(nb * hz * hz * 16 * 2 + 64 * 256 * 2 + 64 * 4 + nb * oy * oy * 64 * 2)
+    if n == "vqa_subsample_nhwc":                                   # x, n, h, w, c, stride, y, ldy
+        nb, h, w, ch, s = c.args[1:6]
+        return float(2 * nb * ((h - 1) // s + 1) * ((w - 1) // s + 1) * ch * 2)
+    if n == "vqa_maxpool3x3s2_nhwc":                                # x, y, n, h, w, c, oh, ow
+        nb, h, w, ch, oh, ow = c.args[2:8]
+        return float(nb * h * w * ch * 2 + nb * oh * ow * ch * 2)
     seen, tot = set(), 0
     for t in (c.keep or ()):
         if isinstance(t, torch.Tensor):

@@ -42,3 +42,18 @@ def test_cumask_words():
     assert bench.cumask_words("st:2:1", 256) == [0x55555555] * 8
     assert bench.cumask_words("st:4:1", 256) == [0x11111111] * 8
     assert sum(bin(w).count("1") for w in bench.cumask_words("lo:100", 256)) == 100
+
+
+def test_byte_model_of_argument_calls():
+    """Calls whose `keep` holds whole arenas or the ResNet's max-size ping-pong buffers are
+    counted from their arguments (the bytes they touch)."""
+    import types
+    C = lambda name, *args: types.SimpleNamespace(name=name, args=args, desc=None, keep=())  # noqa: E731
+    # e4m3 row quantisation of a bf16 [3072 x 1024] weight: read 2 B, write 1 B per element + scales
+    assert bench.call_bytes(C("vqa_quant_rows_fp8", 0, 1, 1024, 3072, 1024, 0, 1024, 0)) == 3072 * 1024 * 3 + 3072 * 4
+    # stem + pool at B = 64, 224^2: the s2d image, weights, bias and the pooled map only
+    want = 64 * 113 * 113 * 32 + 64 * 256 * 2 + 256 + 64 * 56 * 56 * 128
+    assert bench.call_bytes(C("vqa_stem_pool_s2d", 0, 0, 0, 0, 64, 113, 112)) == want
+    # stride-2 subsample of a 56x56x256 map: read and write the 28x28 samples
+    assert bench.call_bytes(C("vqa_subsample_nhwc", 0, 64, 56, 56, 256, 2, 0, 384)) == 2 * 64 * 28 * 28 * 256 * 2
+    assert bench.call_bytes(C("vqa_maxpool3x3s2_nhwc", 0, 0, 2, 21, 21, 64, 11, 11)) == (2 * 21 * 21 + 2 * 11 * 11) * 128
