@@ -119,3 +119,60 @@ def test_dp_world1_sharded_optimizer_rccl(pg, pkg):
     vrel = float((e1.VMAX - e2.VMAX).norm() / e1.VMAX.norm())
     assert vrel <= 1e-5, vrel
     assert torch.equal(e2.P32, e3.P32) and torch.equal(e2.M, e3.M) and torch.equal(e2.VMAX, e3.VMAX)
+
+
+def test_dp_exchange_never_queues_stage_work_behind_a_collective(pg, pkg, monkeypatch):
+    """The placement DESIGN §5 states, asserted on the issue order of one graphed, pipelined
+    world-1 DP step: every collective is issued on the comm stream (never on the step's stream,
+    whose packets the stage graphs follow), every wait on a collective is issued on the step's
+    stream and only after the LAST stage graph has been replayed (a wait packet holds back every
+    later packet of its hardware queue), and the finish graph comes after those waits."""
+    dpm = pkg.dp
+    B, L, H = 4, 32, 96
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    nb = {k: torch.as_tensor(v).cuda() for k, v in pkg.synthetic.make_batch(B, L, H, seed=1).items() if v is not None}
+    e = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, t5_dw_group=(4, 4, 3, 1),
+                             pipeline=True)
+    e.prime(nb["image_tensors"])
+    e.F4.copy_(e.F4N)
+    e.load_batch(nb, next_images=nb["image_tensors"])
+    step = dpm.DataParallelStep(e, bucket_mb=8, use_graph=True)
+    step.step()                                      # captured and run once
+    torch.cuda.synchronize()
+    log = []
+    main = torch.cuda.current_stream()
+
+    class _W:
+        def __init__(self, w):
+            self.w = w
+
+        def wait(self):
+            log.append(("wait", torch.cuda.current_stream() == main))
+            return self.w.wait()
+
+        def __getattr__(self, k):
+            return getattr(self.w, k)
+    real_ar, real_ag = dist.all_reduce, dist.all_gather_into_tensor
+
+    def all_reduce(*a, **kw):
+        log.append(("collective", torch.cuda.current_stream() == main))
+        return _W(real_ar(*a, **kw))
+
+    def all_gather_into_tensor(*a, **kw):
+        log.append(("collective", torch.cuda.current_stream() == main))
+        return _W(real_ag(*a, **kw))
+    monkeypatch.setattr(dist, "all_reduce", all_reduce)
+    monkeypatch.setattr(dist, "all_gather_into_tensor", all_gather_into_tensor)
+    for name, g in step.graphs.items():
+        monkeypatch.setattr(g, "replay", (lambda n, r: (lambda: (log.append(("graph", n)), r())[1]))(name, g.replay))
+    e.load_batch(nb, next_images=nb["image_tensors"])
+    step.step()
+    torch.cuda.synchronize()
+    kinds = [k for k, _ in log]
+    assert "collective" in kinds and "wait" in kinds, log
+    assert all(not on_main for k, on_main in log if k == "collective"), log   # collectives: comm stream
+    assert all(on_main for k, on_main in log if k == "wait"), log             # waits: the step's stream
+    stages = [i for i, x in enumerate(log) if x[0] == "graph" and x[1].startswith("stage")]
+    waits = [i for i, x in enumerate(log) if x[0] == "wait"]
+    finish = [i for i, x in enumerate(log) if x == ("graph", "finish")]
+    assert stages and finish and min(waits) > max(stages) and max(waits) < finish[0], log
