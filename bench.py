@@ -166,6 +166,9 @@ def call_bytes(c):
         nb, hz, oh = c.args[4], c.args[5], c.args[6]
         oy = oh // 2 if n == "vqa_stem_pool_s2d" else oh
         return float(nb * hz * hz * 16 * 2 + 64 * 256 * 2 + 64 * 4 + nb * oy * oy * 64 * 2)
+    if n == "vqa_stem_pool_img":                                    # img, w, bias, y, n, h
+        nb, h = c.args[4], c.args[5]
+        return float(nb * 3 * h * h * 4 + 64 * 256 * 2 + 64 * 4 + nb * (h // 4) * (h // 4) * 64 * 2)
     if n == "vqa_subsample_nhwc":                                   # x, n, h, w, c, stride, y, ldy
         nb, h, w, ch, s = c.args[1:6]
         return float(2 * nb * ((h - 1) // s + 1) * ((w - 1) // s + 1) * ch * 2)

@@ -308,6 +308,10 @@ int vqa_stem_s2d_conv(const void* z, const void* w, const float* bias, void* y, 
  *   of 8, hz == oh + 1, 16-B aligned buffers. */
 int vqa_stem_pool_s2d(const void* z, const void* w, const float* bias, void* y, int n, int hz, int oh,
                       hipStream_t stream);
+/* vqa_stem_pool_img: vqa_image_to_s2d16 + vqa_stem_pool_s2d in one pass, bit-identical: the input
+ *   patches are staged from the fp32 NCHW image img [n][3][h][h] directly (the space-to-depth image is
+ *   never stored); y [n][h/4][h/4][64] bf16; h a multiple of 32, 16-B aligned w, bias and y. */
+int vqa_stem_pool_img(const float* img, const void* w, const float* bias, void* y, int n, int h, hipStream_t stream);
 int vqa_colsum(const void* x, int x_bf16, int rows, int cols, long long ld, float* out, float beta, float* ws,
                hipStream_t stream);
 int vqa_colsum_workspace_floats(int rows, int cols);

@@ -148,9 +148,16 @@ __device__ __forceinline__ int fpatch_off(int pr, int pc, int h) {
   return (pr * FPC + pc) * 32 + 16 * (h ^ ((pc >> 3) & 1));
 }
 
-__global__ __launch_bounds__(256) void stem_pool_kernel(const uint4* __restrict__ z, const bf16_t* __restrict__ w,
+// IMG: the patch is built from the fp32 NCHW image itself (the space-to-depth transform of
+// vqa_image_to_s2d16 applied while staging: Z[u][v][(2p+q)*3+c] = bf16(img[c][2u+p-1][2v+q-1]), 0
+// outside the image, channels 12..15 zero), so the s2d image is neither written nor read
+template <bool IMG>
+__global__ __launch_bounds__(256) void stem_pool_kernel(const void* __restrict__ src, const bf16_t* __restrict__ w,
                                                         const float* __restrict__ bias, bf16_t* __restrict__ y,
                                                         int hz, int oh, int ph, int ntiles) {
+  const uint4* z = reinterpret_cast<const uint4*>(src);
+  const float* img = reinterpret_cast<const float*>(src);
+  const int H = oh * 2;                          // image height = width (IMG)
   __shared__ __attribute__((aligned(16))) char patch[FPR * FPC * 32];
   __shared__ __attribute__((aligned(16))) char stem[5 * 32 * FSTR];
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
@@ -181,39 +188,68 @@ __global__ __launch_bounds__(256) void stem_pool_kernel(const uint4* __restrict_
   const int hi = lo + q8 + (xcd < r8 ? 1 : 0);
   const int wstride = (gridDim.x - xcd + 7) >> 3;
 
-  // this thread's patch pieces of a tile, into registers (zero outside the image)
-  auto load = [&](int tile, uint4 (&v)[2]) {
-    const int img = tile / per_img, rem = tile - img * per_img;
+  // this thread's patch pieces of a tile, into registers (zero outside the image):
+  // Z: 16-B pieces of the s2d image; IMG: one image column of one plane, every other row
+  // (thread t < 240: column cc = t % 40, plane c, row parity par) -> 12 bf16, i.e. one s2d
+  // channel of one patch column over the 12 patch rows
+  const int icc = tid % (2 * FPC), ic = (tid / (2 * FPC)) % 3, ipar = tid / (6 * FPC);
+  const int ich = (2 * ipar + (icc & 1)) * 3 + ic;
+  const int ioff = fpatch_off(0, icc >> 1, ich >> 3) + (ich & 7) * 2;
+  auto load = [&](int tile, uint4 (&v)[2], float (&f)[IMG ? FPR : 1]) {
+    const int im = tile / per_img, rem = tile - im * per_img;
     const int iy0 = 2 * ((rem / tx_n) * PY) - 2, ix0 = 2 * ((rem % tx_n) * PX) - 2;
-    const uint4* zi = z + (long)img * hz * hz * 2;
+    if constexpr (IMG) {
+      const int C = 2 * ix0 - 1 + icc, R0 = 2 * iy0 - 1 + ipar;
+      const float* ii = img + ((long)im * 3 + ic) * H * H + C;
+      const bool colok = tid < 12 * FPC && C >= 0 && C < H;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int u = tid + 256 * k;
-      v[k] = make_uint4(0u, 0u, 0u, 0u);
-      if (u < FPIECES) {
-        const int pr = u / (FPC * 2), rr = u - pr * (FPC * 2), pc = rr >> 1, h = rr & 1;
-        const int iy = iy0 + pr, ix = ix0 + pc;
-        if (iy >= 0 && iy < hz && ix >= 0 && ix < hz) v[k] = zi[((long)iy * hz + ix) * 2 + h];
+      for (int j = 0; j < FPR; ++j) {            // raw: converted at the LDS store, so the
+        const int R = R0 + 2 * j;                // loads stay in flight across the compute
+        f[j] = (colok && R >= 0 && R < H) ? ii[(long)R * H] : 0.f;
+      }
+    } else {
+      const uint4* zi = z + (long)im * hz * hz * 2;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int u = tid + 256 * k;
+        v[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (u < FPIECES) {
+          const int pr = u / (FPC * 2), rr = u - pr * (FPC * 2), pc = rr >> 1, h = rr & 1;
+          const int iy = iy0 + pr, ix = ix0 + pc;
+          if (iy >= 0 && iy < hz && ix >= 0 && ix < hz) v[k] = zi[((long)iy * hz + ix) * 2 + h];
+        }
       }
     }
   };
+  if constexpr (IMG) {                           // s2d channels 12..15 are zero: written once
+    if (tid < FPR * FPC)
+      *reinterpret_cast<uint2*>(patch + fpatch_off(tid / FPC, tid % FPC, 1) + 8) = make_uint2(0u, 0u);
+  }
   uint4 pv[2];
+  float pf[IMG ? FPR : 1];
   int tile = lo + (blockIdx.x >> 3);
-  if (tile < hi) load(tile, pv);
+  if (tile < hi) load(tile, pv, pf);
   for (; tile < hi; tile += wstride) {
     const int img = tile / per_img, rem = tile - img * per_img;
     const int py0 = (rem / tx_n) * PY, px0 = (rem % tx_n) * PX;
     __syncthreads();                             // the previous tile's patch / stem reads are done
+    if constexpr (IMG) {
+      if (tid < 12 * FPC) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int u = tid + 256 * k;
-      if (u < FPIECES) {
-        const int pr = u / (FPC * 2), rr = u - pr * (FPC * 2), pc = rr >> 1, h = rr & 1;
-        *reinterpret_cast<uint4*>(patch + fpatch_off(pr, pc, h)) = pv[k];
+        for (int j = 0; j < FPR; ++j) *reinterpret_cast<bf16_t*>(patch + ioff + j * FPC * 32) = f2bf(pf[j]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int u = tid + 256 * k;
+        if (u < FPIECES) {
+          const int pr = u / (FPC * 2), rr = u - pr * (FPC * 2), pc = rr >> 1, h = rr & 1;
+          *reinterpret_cast<uint4*>(patch + fpatch_off(pr, pc, h)) = pv[k];
+        }
       }
     }
     __syncthreads();
-    if (tile + wstride < hi) load(tile + wstride, pv);   // in flight while this tile computes
+    if (tile + wstride < hi) load(tile + wstride, pv, pf);   // in flight while this tile computes
 
     f32x16_t acc[3];
 #pragma unroll
@@ -311,7 +347,21 @@ extern "C" int vqa_stem_pool_s2d(const void* z, const void* w, const float* bias
               "vqa_stem_pool_s2d: 16-B aligned buffers needed");
   const int ntiles = n * (ph / PY) * (ph / PX);
   const int grid = std::min(ntiles, 2 * STEM_CUS) / 8 * 8 > 0 ? std::min(ntiles, 2 * STEM_CUS) / 8 * 8 : ntiles;
-  hipLaunchKernelGGL(stem_pool_kernel, dim3(grid), dim3(256), 0, s, (const uint4*)z, (const bf16_t*)w, bias,
-                     (bf16_t*)y, hz, oh, ph, ntiles);
+  hipLaunchKernelGGL(stem_pool_kernel<false>, dim3(grid), dim3(256), 0, s, z, (const bf16_t*)w, bias, (bf16_t*)y,
+                     hz, oh, ph, ntiles);
   return vqa::check_launch("vqa_stem_pool_s2d");
+}
+
+extern "C" int vqa_stem_pool_img(const float* img, const void* w, const float* bias, void* y, int n, int h,
+                                 hipStream_t s) {
+  VQA_REQUIRE(img && w && bias && y && n > 0, "vqa_stem_pool_img: null argument");
+  const int oh = h / 2, ph = oh / 2;
+  VQA_REQUIRE(h % 4 == 0 && ph % PY == 0 && ph % PX == 0, "vqa_stem_pool_img: h a multiple of 32 needed");
+  VQA_REQUIRE(((uintptr_t)w & 15) == 0 && ((uintptr_t)bias & 15) == 0 && ((uintptr_t)y & 15) == 0,
+              "vqa_stem_pool_img: 16-B aligned weights, bias and output needed");
+  const int ntiles = n * (ph / PY) * (ph / PX);
+  const int grid = std::min(ntiles, 2 * STEM_CUS) / 8 * 8 > 0 ? std::min(ntiles, 2 * STEM_CUS) / 8 * 8 : ntiles;
+  hipLaunchKernelGGL(stem_pool_kernel<true>, dim3(grid), dim3(256), 0, s, img, (const bf16_t*)w, bias, (bf16_t*)y,
+                     oh + 1, oh, ph, ntiles);
+  return vqa::check_launch("vqa_stem_pool_img");
 }

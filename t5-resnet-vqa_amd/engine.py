@@ -351,11 +351,20 @@ class VQAEngine:
         # stem: conv7x7/2 + BN + ReLU, then maxpool 3x3/2
         # (as a 4x4 stride-1 conv over the space-to-depth image: K 256 instead of 7*7*8 = 392)
         w16, b32 = conv_w("conv1", "bn1", s2d=True)
-        self.res_calls.append(ops.Call("vqa_image_to_s2d16", self.IMG.data_ptr(), self.IMG8.data_ptr(), B, H, H,
-                                       keep=(self.IMG, self.IMG8)))
         g = ops.conv_geom(B, hz, hz, 16, h1, h1, 4, 4, 1, 1)
-        stem = os.environ.get("VQA_STEM", "pool")           # pool | patch | gemm (A/B switches)
-        if stem == "pool" and h1 % 16 == 0 and hz == h1 + 1 and h2 == h1 // 2:
+        stem = os.environ.get("VQA_STEM", "img")            # img | pool | patch | gemm (A/B switches)
+        if stem == "img" and H % 32 == 0 and hz == h1 + 1 and h2 == h1 // 2:
+            # space-to-depth + stem + maxpool in one pass (csrc/stem.hip): patches staged from the
+            # fp32 image, only the pooled map written; bit-identical to the three-kernel form below
+            self.res_calls.append(ops.Call("vqa_stem_pool_img", self.IMG.data_ptr(), w16.data_ptr(), b32.data_ptr(),
+                                           bufs[1].data_ptr(), B, H, keep=(self.IMG, w16, b32, bufs[1])))
+            stem = None
+        else:
+            self.res_calls.append(ops.Call("vqa_image_to_s2d16", self.IMG.data_ptr(), self.IMG8.data_ptr(), B, H, H,
+                                           keep=(self.IMG, self.IMG8)))
+        if stem is None:
+            pass
+        elif stem in ("img", "pool") and h1 % 16 == 0 and hz == h1 + 1 and h2 == h1 // 2:
             # stem + maxpool in one pass from LDS input patches (csrc/stem.hip): only the pooled
             # map is written; bit-identical to the implicit GEMM + vqa_maxpool3x3s2_nhwc below
             self.res_calls.append(ops.Call("vqa_stem_pool_s2d", self.IMG8.data_ptr(), w16.data_ptr(), b32.data_ptr(),

@@ -177,6 +177,7 @@ register("vqa_maxpool3x3s2_nhwc", P, P, c_int, c_int, c_int, c_int, c_int, c_int
 register("vqa_subsample_nhwc", P, c_int, c_int, c_int, c_int, c_int, P, c_ll)
 register("vqa_stem_s2d_conv", P, P, P, P, c_int, c_int, c_int)
 register("vqa_stem_pool_s2d", P, P, P, P, c_int, c_int, c_int)
+register("vqa_stem_pool_img", P, P, P, P, c_int, c_int)
 register("vqa_colsum", P, c_int, c_int, c_int, c_ll, P, c_float, P)
 register("vqa_embedding_fwd", P, P, P, c_int, c_int, c_int, P)
 register("vqa_embedding_bwd", P, P, P, c_int, c_int, c_int, P)

@@ -54,6 +54,9 @@ def test_byte_model_of_argument_calls():
     # stem + pool at B = 64, 224^2: the s2d image, weights, bias and the pooled map only
     want = 64 * 113 * 113 * 32 + 64 * 256 * 2 + 256 + 64 * 56 * 56 * 128
     assert bench.call_bytes(C("vqa_stem_pool_s2d", 0, 0, 0, 0, 64, 113, 112)) == want
+    # the same from the fp32 image: the image instead of the s2d image
+    want = 64 * 3 * 224 * 224 * 4 + 64 * 256 * 2 + 256 + 64 * 56 * 56 * 128
+    assert bench.call_bytes(C("vqa_stem_pool_img", 0, 0, 0, 0, 64, 224)) == want
     # stride-2 subsample of a 56x56x256 map: read and write the 28x28 samples
     assert bench.call_bytes(C("vqa_subsample_nhwc", 0, 64, 56, 56, 256, 2, 0, 384)) == 2 * 64 * 28 * 28 * 256 * 2
     assert bench.call_bytes(C("vqa_maxpool3x3s2_nhwc", 0, 0, 2, 21, 21, 64, 11, 11)) == (2 * 21 * 21 + 2 * 11 * 11) * 128

@@ -569,3 +569,22 @@ def test_stem_pool_equals_stem_then_maxpool(k, n, oh):
     run(k, "vqa_stem_pool_s2d", z, w, b, y, n, hz, oh)
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("n,h", [(2, 224), (3, 64), (1, 32), (1, 384)])
+def test_stem_pool_from_the_image_equals_s2d_then_stem_pool(k, n, h):
+    """vqa_stem_pool_img (space-to-depth staged from the fp32 image inside the stem kernel) against
+    vqa_image_to_s2d16 followed by vqa_stem_pool_s2d: bit for bit.  The weights are random in the
+    s2d channels 12..15 too, so the kernel's zeroed channels are checked."""
+    hz, oh = h // 2 + 1, h // 2
+    img = rnd((n, 3, h, h), 57)
+    w = rnd((64, 4, 4, 16), 58, scale=0.1, dtype=torch.bfloat16)
+    b = rnd(64, 59)
+    z = torch.empty(n, hz, hz, 16, device="cuda", dtype=torch.bfloat16)
+    run(k, "vqa_image_to_s2d16", img, z, n, h, h)
+    ref = torch.empty(n, h // 4, h // 4, 64, device="cuda", dtype=torch.bfloat16)
+    run(k, "vqa_stem_pool_s2d", z, w, b, ref, n, hz, oh)
+    y = torch.full_like(ref, 7.0)
+    run(k, "vqa_stem_pool_img", img, w, b, y, n, h)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
