@@ -28,8 +28,11 @@ def torch_cuda():
     return torch
 
 
-def census(graph_handle):
-    hip = ctypes.CDLL("libamdhip64.so")
+def census(graph_handle, pkg):
+    # the runtime torch already runs: a CDLL by file name can map /opt/rocm's copy beside it, a
+    # second HIP runtime in the process (its graph calls on the first one's objects; the replay
+    # that followed segfaulted on the host in two suite runs)
+    hip = pkg.lib.hip_runtime()
     n = ctypes.c_size_t(0)
     assert hip.hipGraphGetNodes(ctypes.c_void_p(graph_handle), None, ctypes.byref(n)) == 0
     nodes = (ctypes.c_void_p * n.value)()
@@ -63,7 +66,7 @@ def test_step_graph_is_kernel_only(torch_cuda, pkg, pipeline):
     eng, _ = _engine(pkg, torch, pipeline)
     eng.capture(keep_graph=True)
     (g,) = eng.graph
-    c = census(g.raw_cuda_graph())
+    c = census(g.raw_cuda_graph(), pkg)
     assert set(c) == {"kernel"}, c
     n_calls = len(eng.fwd_calls) + len(eng.bwd_calls) + len(eng.opt_calls) + len(eng.adam_segs)
     assert c["kernel"] >= n_calls, (c, n_calls)
