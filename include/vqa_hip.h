@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VQA_ABI_VERSION 17
+#define VQA_ABI_VERSION 18
 #define VQA_OK 0
 #define VQA_ERR_INVALID 1000
 
@@ -398,10 +398,21 @@ int vqa_xattn1_bwd(const void* dctx, long long ldd, float* dv32, void* dv16, lon
 int vqa_head_fwd(const float* x, const float* wp, const float* bp, const float* wc, const float* bc,
                  const long long* targets, float* att, float* pooled, float* logp, float* nll, float* loss,
                  int batch, int seq, int d, int answers, hipStream_t stream);
+/* Backward.  row_total NULL: the NLL mean's divisor is this batch's valid-row count.  Data
+ * parallel (ABI 18): row_total -> the valid-row count summed over the ranks (vqa_count_targets,
+ * all-reduced) and row_scale = the world size; the divisor is then row_total[0] / row_scale, so
+ * the ranks' gradients summed and scaled by 1/world are the global batch's mean however the rows
+ * are split (a rank with no valid row gives zero), and loss[0] is rewritten as
+ * sum(nll) * row_scale / row_total[0] (its mean over the ranks is the global batch's loss).
+ * nll / loss are read / written only when row_total is set.  Replaces the DP form of
+ * loss.backward() on a contiguously split global batch (NLLLoss mean, resnet_vqa_model.py:159). */
 int vqa_head_bwd(const float* x, const float* att, const float* pooled, const float* logp, const long long* targets,
                  const float* wp, const float* wc, float* dx32, void* dx16, float* dwp, float* dbp, float* dwc,
-                 float* dbc, float* ws, int batch, int seq, int d, int answers, hipStream_t stream);
+                 float* dbc, float* ws, int batch, int seq, int d, int answers, const float* nll, float* loss,
+                 const float* row_total, float row_scale, hipStream_t stream);
 int vqa_head_workspace_floats(int batch, int seq, int d, int answers);
+/* out[0] = (float) the number of targets >= 0 among targets[0..batch) (batch <= 1024). */
+int vqa_count_targets(const long long* targets, int batch, float* out, hipStream_t stream);
 
 /* ------------------------------------------------------------- optimiser ---
  * clip_grad_norm_(1.0) + AdamW(amsgrad) + linear warmup/decay schedule

@@ -222,7 +222,9 @@ template <bool CHUNKED>                               // false: A <= 192, one ch
 __global__ __launch_bounds__(256) void head_dpooled_kernel(const float* __restrict__ lp,
                                                            const long long* __restrict__ tgt,
                                                            const float* __restrict__ wc, float* __restrict__ dl_out,
-                                                           float* __restrict__ dpooled, int B, int D, int A) {
+                                                           float* __restrict__ dpooled, int B, int D, int A,
+                                                           const float* __restrict__ nll, float* __restrict__ loss,
+                                                           const float* __restrict__ row_total, float row_scale) {
   constexpr int AP = 4 * DP_AQ;                       // padded answer row in LDS
   __shared__ __attribute__((aligned(16))) float dl[16][AP];
   __shared__ float red[4][16][64];
@@ -231,9 +233,24 @@ __global__ __launch_bounds__(256) void head_dpooled_kernel(const float* __restri
   constexpr int FI = 16 * AP / 256;                   // fill elements per thread (all loads first)
   // the NLL mean's divisor: rows with a target >= 0 (ignore_index rows get no gradient); a full
   // batch gives 1 / B exactly as the host-computed factor did
-  int nvalid = 0;
-  for (int b0 = 0; b0 < B; b0 += 256) nvalid += __syncthreads_count(b0 + tid < B && tgt[min(b0 + tid, B - 1)] >= 0);
-  const float inv_b = 1.0f / (float)nvalid;
+  // Data parallel (row_total set): the divisor is the valid-row count summed over the ranks,
+  // row_total[0], over row_scale = the world size, so that the ranks' gradients, summed and
+  // scaled by 1/world in the update, are the global batch's NLL mean whatever each rank's rows
+  // (a rank with no valid row contributes zero).  The rank's loss is rewritten the same way:
+  // sum(nll) * world / total, whose mean over the ranks is the global batch's loss.
+  float inv_b;
+  if (row_total) {
+    inv_b = row_scale / row_total[0];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
+      float s = 0.f;                                    // the forward's fixed order (head_lse)
+      for (int b = 0; b < B; ++b) s += nll[b];
+      loss[0] = (s * row_scale) / row_total[0];
+    }
+  } else {
+    int nvalid = 0;
+    for (int b0 = 0; b0 < B; b0 += 256) nvalid += __syncthreads_count(b0 + tid < B && tgt[min(b0 + tid, B - 1)] >= 0);
+    inv_b = 1.0f / (float)nvalid;
+  }
   float acc[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc[q] = 0.f;
@@ -484,9 +501,12 @@ extern "C" int vqa_head_fwd(const float* x, const float* wp, const float* bp, co
 extern "C" int vqa_head_bwd(const float* x, const float* att, const float* pooled, const float* logp,
                             const long long* targets, const float* wp, const float* wc, float* dx32, void* dx16,
                             float* dwp, float* dbp, float* dwc, float* dbc, float* ws, int batch, int seq, int d,
-                            int answers, hipStream_t s) {
+                            int answers, const float* nll, float* loss, const float* row_total, float row_scale,
+                            hipStream_t s) {
   VQA_REQUIRE(x && att && pooled && logp && targets && wp && wc && dx32 && dwp && dbp && dwc && dbc && ws,
               "vqa_head_bwd: null argument");
+  VQA_REQUIRE(!row_total || (nll && loss && row_scale > 0.f),
+              "vqa_head_bwd: a global row total needs nll, loss and row_scale > 0");
   VQA_REQUIRE(seq >= 1 && seq <= 64 && d >= 4 && d <= 1024 && d % 4 == 0 && answers >= 1 && answers <= MAXA &&
                   batch >= 1 && batch <= 1024,
               "vqa_head_bwd: shape out of range (1<=L<=64, 4<=D<=1024, D%4==0, 1<=A<=1024, 1<=B<=1024)");
@@ -496,9 +516,11 @@ extern "C" int vqa_head_bwd(const float* x, const float* att, const float* poole
   float* part = dpool + batch * d;
   const dim3 dg(vqa::cdiv(d, 64), vqa::cdiv(batch, 16));
   if (answers <= 4 * DP_AQ)
-    hipLaunchKernelGGL(head_dpooled_kernel<false>, dg, dim3(256), 0, s, logp, targets, wc, dl, dpool, batch, d, answers);
+    hipLaunchKernelGGL(head_dpooled_kernel<false>, dg, dim3(256), 0, s, logp, targets, wc, dl, dpool, batch, d, answers,
+                       nll, loss, row_total, row_scale);
   else
-    hipLaunchKernelGGL(head_dpooled_kernel<true>, dg, dim3(256), 0, s, logp, targets, wc, dl, dpool, batch, d, answers);
+    hipLaunchKernelGGL(head_dpooled_kernel<true>, dg, dim3(256), 0, s, logp, targets, wc, dl, dpool, batch, d, answers,
+                       nll, loss, row_total, row_scale);
   int rc = vqa::check_launch("vqa_head_bwd/dpooled");
   if (rc) return rc;
   rc = with_lmax(seq, [&](auto lm) {
@@ -514,4 +536,22 @@ extern "C" int vqa_head_bwd(const float* x, const float* att, const float* poole
   hipLaunchKernelGGL(head_wgrad_kernel, dim3(nca * ncd + ncd), dim3(256), 0, s, dl, pooled, part, pbp, dwc, dbc, dwp, dbp,
                      batch, answers, d);
   return vqa::check_launch("vqa_head_bwd/wgrad");
+}
+
+// Valid rows of a batch (targets >= 0, i.e. not ignore_index) as a float, one workgroup: the
+// data-parallel step all-reduces it into vqa_head_bwd's row_total before the backward.
+namespace {
+__global__ __launch_bounds__(256) void count_targets_kernel(const long long* __restrict__ tgt, int B,
+                                                            float* __restrict__ out) {
+  const int tid = threadIdx.x;
+  int n = 0;
+  for (int b0 = 0; b0 < B; b0 += 256) n += __syncthreads_count(b0 + tid < B && tgt[min(b0 + tid, B - 1)] >= 0);
+  if (tid == 0) out[0] = (float)n;
+}
+}  // namespace
+
+extern "C" int vqa_count_targets(const long long* targets, int batch, float* out, hipStream_t s) {
+  VQA_REQUIRE(targets && out && batch >= 1 && batch <= 1024, "vqa_count_targets: null argument or batch out of 1..1024");
+  hipLaunchKernelGGL(count_targets_kernel, dim3(1), dim3(256), 0, s, targets, batch, out);
+  return vqa::check_launch("vqa_count_targets");
 }

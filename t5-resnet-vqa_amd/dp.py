@@ -225,6 +225,9 @@ class DataParallelStep:
         self.shard = bool(shard_optimizer)
         e = engine
         e.set_grad_scale(1.0 / self.world)
+        # the NLL mean over the global batch (ranks may hold unequal rows, or none): the head
+        # backward divides by the all-reduced valid-row count over world (engine.use_global_rows)
+        e.use_global_rows(self.world)
         emb = e.lay["t5.embed"]
         self.buckets = plan_buckets(e.ready_marks, emb.offset, bucket_mb << 20)
         calls = e.bwd_calls[:-1]                            # all but the local embedding scatter
@@ -519,6 +522,7 @@ class DataParallelStep:
     def capture(self):
         e = self.eng
         e.flush_optimizer()              # the warm-up's backward must not overwrite a pending update's G
+        e.ROWTOT.fill_(float(e.B * self.world))             # a finite divisor for the warm-up's head backward
         s = torch.cuda.Stream(e.dev)
         s.wait_stream(torch.cuda.current_stream(e.dev))
         saved_rng = e.RNG.clone()
@@ -561,14 +565,29 @@ class DataParallelStep:
         if self._res_a:
             _after(main, e._rstream)
 
+    def _exchange_row_total(self):
+        """This rank's valid-row count (vqa_count_targets, on the step's stream), summed over the
+        ranks on the comm stream; the head backward (first backward stage) reads the sum.  Issued
+        before the forward, waited on after it: the tiny collective runs while the forward does."""
+        e = self.eng
+        main = torch.cuda.current_stream(e.dev)
+        e.count_call(L.stream_handle(main))
+        _after(self._comm, main)
+        with torch.cuda.stream(self._comm):
+            return allreduce_buckets(e.ROWTOT, [(None, 0, 1)], self.group)
+
     def step(self):
         e = self.eng
+        rows = self._exchange_row_total()
         if e.pipeline:                                      # F4 <- F4N: this batch's features (last step's ResNet)
             e.copy_f4(L.stream_handle(torch.cuda.current_stream(e.dev)))
         if self.graphs is not None:
             self.graphs["fwd"].replay()
         else:
             self._fwd()
+        for w in rows:                                      # long done: the forward ran meanwhile
+            w.wait()
+        _after(torch.cuda.current_stream(e.dev), self._comm)   # gloo: the staged copy ran on comm
         tev = self._backward_exchange()
         if self.shard:
             self._sharded_optimizer()

@@ -144,23 +144,29 @@ def _h2d(dst, src):
 IGNORE_INDEX = -100          # nn.NLLLoss's default ignore_index: the head skips rows with a target < 0
 
 
-def batch_rows(batch, key, planned):
+def batch_rows(batch, key, planned, allow_empty=False):
     """Rows of a collate batch (the reference's loaders have no drop_last, so an epoch's last
-    batch is short: faster_rcnn_vqa_trainer.py:172-197); 1 <= rows <= the planned batch."""
+    batch is short: faster_rcnn_vqa_trainer.py:172-197); 1 <= rows <= the planned batch (0 rows
+    only for a data-parallel rank whose share of the global batch is empty: allow_empty)."""
     n = int(torch.as_tensor(batch[key]).shape[0])
-    if not 1 <= n <= planned:
-        raise ValueError(f"{key}: batch of {n} rows; this engine is planned for 1..{planned} rows")
+    if not (0 if allow_empty else 1) <= n <= planned:
+        lo = 0 if allow_empty else 1
+        raise ValueError(f"{key}: batch of {n} rows; this engine is planned for {lo}..{planned} rows")
     return n
 
 
-def load_rows(dst, src, n, fill=None):
+def load_rows(dst, src, n, fill=None, empty_fill=0):
     """dst[:n] <- src (n rows); the planned rows past n are padding: copies of rows 0..n-1
     (real samples, so every activation stays finite) or `fill` (targets: IGNORE_INDEX, so the
     padded rows add nothing to the loss or to any gradient -- the NLL mean runs over the n
-    real rows)."""
+    real rows).  n = 0 (an empty data-parallel rank): every row is `fill`, else `empty_fill`
+    (finite inputs whose targets are all ignored: the rank's gradient is exactly zero)."""
     if src is None:
         return
     B = dst.shape[0]
+    if n == 0:
+        dst.fill_(fill if fill is not None else empty_fill)
+        return
     _h2d(dst[:n] if n < B else dst, src)
     if n == B:
         return
@@ -259,6 +265,9 @@ class VQAEngine:
         self._wside = torch.cuda.Stream(self.dev)
         self._rstream = torch.cuda.Stream(self.dev)
         self.res_external = False        # set_res_cumask: the ResNet launched eagerly beside the graph
+        self.allow_empty_rows = False     # use_global_rows (DP): a rank may get 0 rows
+        self._img_rows_next = None        # pipelined: rows of the images whose features the next batch uses
+        self.count_call = None
         self._scratch = None             # split-K workspace used while autotuning
 
     @classmethod
@@ -331,13 +340,14 @@ class VQAEngine:
                 out = planes * 4 if bottleneck else planes
                 ho = (hh + 2 - 3) // stride + 1
                 maxel = max(maxel, B * hh * hh * planes, B * ho * ho * out)
+                if bottleneck and bi == 0:            # the fused conv3 + downsample's [conv2 | x] rows
+                    maxel = max(maxel, B * ho * ho * (planes + cin))
                 plan.append((li, bi, stride, hh, ho, cin, planes, out))
                 hh, cin = ho, out
         self.fh, self.fc = hh, cin                    # layer4 spatial size / channels
         self.V_TOK = B * hh * hh
         self.IMG = self._t((B, 3, H, H))
         hz = H // 2 + 1                               # space-to-depth stem image (vqa_image_to_s2d16)
-        self.IMG8 = self._t((B, hz, hz, 16), BF16)
         bufs = [self._t(maxel, BF16) for _ in range(5)]
         self.res_bufs = bufs
         self.F4 = self._t((B, hh, hh, cin), BF16)
@@ -353,7 +363,10 @@ class VQAEngine:
         w16, b32 = conv_w("conv1", "bn1", s2d=True)
         g = ops.conv_geom(B, hz, hz, 16, h1, h1, 4, 4, 1, 1)
         stem = os.environ.get("VQA_STEM", "img")            # img | pool | patch | gemm (A/B switches)
-        if stem == "img" and H % 32 == 0 and hz == h1 + 1 and h2 == h1 // 2:
+        fused_img = stem == "img" and H % 32 == 0 and hz == h1 + 1 and h2 == h1 // 2
+        # the space-to-depth image only exists for the forms that read it (B x 113 x 113 x 16 bf16)
+        self.IMG8 = None if fused_img else self._t((B, hz, hz, 16), BF16)
+        if fused_img:
             # space-to-depth + stem + maxpool in one pass (csrc/stem.hip): patches staged from the
             # fp32 image, only the pooled map written; bit-identical to the three-kernel form below
             self.res_calls.append(ops.Call("vqa_stem_pool_img", self.IMG.data_ptr(), w16.data_ptr(), b32.data_ptr(),
@@ -405,6 +418,7 @@ class VQAEngine:
                 wcat = torch.cat([w3.reshape(out, planes), wd.reshape(out, ci)], dim=1).contiguous()
                 bcat = b3 + bd
                 self._res_keep += [wcat, bcat]
+                assert B * ho * ho * kc <= ds.numel(), "fused downsample: the [conv2 | x] rows exceed the buffer"
                 self._gemm(self.res_calls, ds, wcat, B * ho * ho, out, kc, lda=kc, ldb=kc, c16=y, ldc16=out,
                            bias=bcat, relu=True)
                 if y is not self.F4N:
@@ -504,6 +518,7 @@ class VQAEngine:
         # head
         self.ATT, self.POOLED = t((B, Lq)), t((B, D))
         self.LOGP, self.NLL, self.LOSS = t((B, self.A)), t(B), t(1)
+        self.ROWTOT = t(1, zero=True)     # DP: valid rows summed over the ranks (use_global_rows)
         # backward temporaries (reused layer to layer)
         mx = max(T, V)
         self.dY = [t((T, D)), t((T, D))]
@@ -870,7 +885,8 @@ class VQAEngine:
         last = self.sga[-1]["OUT"]
         self._call(b, "vqa_head_bwd", last, self.ATT, self.POOLED, self.LOGP, self.TGT, self.p32["pool_w"],
                    self.p32["cls_w"], self.dY[(NB - 1) & 1], None, self.g32["pool_w"], self.g32["pool_b"],
-                   self.g32["cls_w"], self.g32["cls_b"], self.WS_HEAD, B, Lq, D, self.A)
+                   self.g32["cls_w"], self.g32["cls_b"], self.WS_HEAD, B, Lq, D, self.A, self.NLL, self.LOSS,
+                   None, 1.0)
         # ready marks: (number of backward calls issued, end of the gradient prefix now final).
         # The flat layout is in backward-completion order, so finished gradients always form
         # a prefix of G32: DP all-reduces bucket [prev_end, end) as soon as it is final.
@@ -1257,22 +1273,59 @@ class VQAEngine:
         Pipelined engines take the batch's text and targets, and `next_images` = the image
         tensors of the batch that the FOLLOWING step trains on (this batch's images went
         in one step earlier, or through prime())."""
-        n = self.rows = batch_rows(batch, "question_input_ids", self.B)
+        ae = self.allow_empty_rows
+        n = batch_rows(batch, "question_input_ids", self.B, ae)
         if self.pipeline:
+            # this batch's images went in one step earlier (or through prime()): their row count
+            # must be the text's, else the rows past the shorter one would pair other samples'
+            # features with real targets
+            if self._img_rows_next is not None and self._img_rows_next != n:
+                raise ValueError(f"pipelined engine: this batch has {n} question rows but its images "
+                                 f"(loaded one step earlier) had {self._img_rows_next}")
             if next_images is not None:
-                load_rows(self.IMG, next_images, batch_rows({"image_tensors": next_images}, "image_tensors", self.B))
+                ni = batch_rows({"image_tensors": next_images}, "image_tensors", self.B, ae)
+                load_rows(self.IMG, next_images, ni)
+                self._img_rows_next = ni
+            else:
+                self._img_rows_next = None
         else:
             load_rows(self.IMG, batch["image_tensors"], n)
+        self.rows = n
         load_rows(self.IDS, batch["question_input_ids"], n)
-        load_rows(self.MASK, batch["question_attention_masks"], n)
+        load_rows(self.MASK, batch["question_attention_masks"], n, empty_fill=1)
         load_rows(self.TGT, batch.get("annotation_ids"), n, fill=IGNORE_INDEX)
 
     def prime(self, images):
         """Pipelined engines: compute the layer4 features of the first batch's images, so
         that the first train_step has them (later steps produce their successor's)."""
         assert self.pipeline, "prime() is for pipelined engines"
-        load_rows(self.IMG, images, batch_rows({"image_tensors": images}, "image_tensors", self.B))
+        ni = batch_rows({"image_tensors": images}, "image_tensors", self.B, self.allow_empty_rows)
+        load_rows(self.IMG, images, ni)
+        self._img_rows_next = ni
         self._run(self.res_calls)
+
+    def use_global_rows(self, world):
+        """Data parallel (dp.DataParallelStep): the head backward divides by the valid-row count
+        summed over the `world` ranks (ROWTOT, which the DP step fills each step: count_call, then
+        an all-reduce) over `world` instead of by the rank's own count, and rewrites LOSS as the
+        rank's share (vqa_head_bwd, ABI 18), so the summed, 1/world-scaled gradients are the
+        global batch's NLL mean however the global batch is split -- unequal rows per rank, or a
+        rank with none (allowed from here on: its gradient is zero).  The reference's mean is
+        over the whole batch (resnet_vqa_model.py:159, loaders without drop_last,
+        trainer/faster_rcnn_vqa_trainer.py:172-197)."""
+        i = next(k for k, c in enumerate(self.bwd_calls) if c.name == "vqa_head_bwd")
+        old = self.bwd_calls[i]
+        if self.count_call is not None:
+            assert old.args[-1] == float(world), "use_global_rows: already set for another world size"
+            return
+        new = ops.Call("vqa_head_bwd", *old.args[:-2], ops.addr(self.ROWTOT), float(world),
+                       keep=tuple(old.keep) + (self.ROWTOT,))
+        new.side = old.side
+        self.bwd_calls[i] = new
+        self.count_call = ops.Call("vqa_count_targets", ops.addr(self.TGT), self.B, ops.addr(self.ROWTOT),
+                                   keep=(self.TGT, self.ROWTOT))
+        self.allow_empty_rows = True
+        self.graph = None
 
     def forward(self):
         if self.defer_opt:                              # the previous step's update, then the forward
@@ -1481,9 +1534,33 @@ class VQAEngine:
             rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(len(words)), arr)
         if rc != 0:
             raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-        self._rstream_handle = s                      # lives as long as the engine's process
+        self.reset_res_cumask()                       # one masked stream at a time
+        self._rstream_plain = self._rstream           # restored by reset_res_cumask
+        self._rstream_handle = s
         self._rstream = torch.cuda.ExternalStream(s.value, device=self.dev)
         self.res_external = True
+
+    def reset_res_cumask(self, destroy=True):
+        """End the set_res_cumask experiment: the ResNet goes back to the engine's own stream and
+        into the captured step (re-capture needed: the graph is dropped).  destroy=False keeps the
+        masked stream alive and returns it (tools/queue_probe.py times the step while it exists);
+        the caller then owns the handle (hipStreamDestroy)."""
+        h = getattr(self, "_rstream_handle", None)
+        if h is None:
+            return None
+        torch.cuda.synchronize(self.dev)
+        masked = self._rstream
+        self._rstream = self._rstream_plain
+        self._rstream_handle = None
+        if self.res_external:
+            self.res_external = False
+            self.graph = None
+        if destroy:
+            rc = L.hip_runtime().hipStreamDestroy(h)
+            if rc != 0:
+                raise RuntimeError(f"hipStreamDestroy failed ({rc})")
+            return None
+        return masked, h
 
     def _res_external_step(self):
         main = torch.cuda.current_stream(self.dev)

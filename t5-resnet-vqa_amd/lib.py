@@ -192,7 +192,8 @@ register("vqa_copy", P, P, c_ll)
 register("vqa_tap_shift", P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int)
 register("vqa_quant_rows_fp8", P, c_int, c_ll, c_int, c_int, P, c_ll, P)
 register("vqa_head_fwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
-register("vqa_head_bwd", P, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
+register("vqa_head_bwd", P, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, c_float)
+register("vqa_count_targets", P, c_int, P)
 register("vqa_grad_sqnorm", P, c_ll, P, c_int)
 register("vqa_vit_patchify", P, P, c_int, c_int, c_int, c_int)
 register("vqa_gather_rows", P, c_ll, P, c_ll, c_ll, P, c_ll, c_int, c_int, c_int)

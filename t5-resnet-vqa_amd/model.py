@@ -153,8 +153,9 @@ class ResnetVQAModel:
     # ------------------------------------------------------------------ forward
     def _check_batch(self, question_input_ids, image_tensors):
         n = int(question_input_ids.shape[0])
-        if not 1 <= n <= self.batch_size:
-            raise ValueError(f"batch of {n} rows: the model is planned for 1..{self.batch_size} rows")
+        lo = 0 if self.engine.allow_empty_rows else 1         # 0: an empty data-parallel rank
+        if not lo <= n <= self.batch_size:
+            raise ValueError(f"batch of {n} rows: the model is planned for {lo}..{self.batch_size} rows")
         want_q = (n, self.seq_len)
         want_i = (n, 3, self.image_size, self.image_size)
         if tuple(question_input_ids.shape) != want_q:

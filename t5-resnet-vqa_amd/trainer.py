@@ -71,6 +71,10 @@ class VQATrainer:
             # DP layout: T5 weight gradients in groups that let the buckets become final (and be
             # all-reduced) while the backward runs; rebuilt before the optimizer is configured
             model._build(model.state_dict(), t5_dw_group=groups)
+        if self.data_parallel:
+            # the NLL mean over the GLOBAL batch: unequal rows per rank, or none on a rank
+            # (engine.use_global_rows; the DP step all-reduces the valid-row count each step)
+            model.engine.use_global_rows(torch.distributed.get_world_size(process_group))
         self.num_training_steps = int(num_training_steps)
         warm = lr_scheduler_kwargs.get("num_warmup_steps", -1)
         warm = self.num_training_steps // 10 if warm == -1 else int(warm)

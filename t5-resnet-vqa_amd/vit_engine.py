@@ -356,7 +356,7 @@ class VitVQAEngine:
         self._call(b, "vqa_embedding_zero_rows", self.IDS_PREV, self.IDS_ALL, T + TD, z, D, S.T5_VOCAB)
         self._call(b, "vqa_head_bwd", self.ANS32, self.ATT, self.POOLED, self.LOGP, self.TGT, self.DUMMY_PW,
                    self.p32["cls_w"], self.dANS32, None, self.DUMMY_GPW, self.DUMMY_GPB, self.g32["cls_w"],
-                   self.g32["cls_b"], self.WS_HEAD, B, 1, D, self.A)
+                   self.g32["cls_b"], self.WS_HEAD, B, 1, D, self.A, None, None, None, 1.0)
         # the answer rows move with the batch's decoder masks: clear last step's rows first
         self._call(b, "vqa_zero", self.dDEC32, TD * D * 4)
         self._call(b, "vqa_scatter_rows", self.dANS32, D, self.LASTIDX, 0, 0, self.dDEC32, D, B, D, 4)

@@ -9,7 +9,9 @@ picked up from the initialised process group) instead of the engine directly; `t
 the same with a short last batch (3 rows per rank, padded to the planned 4); `shard`: the
 engine step with the sharded optimizer (reduce-scatter, AdamW on the own chunks, all-gather);
 `c5`: the engine step at BASELINE configs[4] widths (T5-large, 6 SGA blocks, fp8 forward GEMMs,
-T5 weight-gradient groups (8, 8, 6, 2))."""
+T5 weight-gradient groups (8, 8, 6, 2)); `rows<R0>.<R1>...`: unequal rows per rank (rank r takes
+the next R_r samples of each sum(R)-row global batch; R_r = 0: an empty rank), the engine planned
+for B = 4 rows with the global-batch NLL mean (engine.use_global_rows)."""
 import os
 import sys
 
@@ -37,9 +39,16 @@ def main():
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0, **({"num_attention_blocks": 6, "language_model": "t5-large"}
                                                               if c5 else {}))
     rows = short_rows(B, steps) if mode == "trainer_short" else [B] * (steps + 1)
-    gb = [pkg.synthetic.make_batch(world * rows[i], L, H, seed=40 + i) for i in range(steps + 1)]
-    mine = [{k: (None if v is None else v[rank * rows[i]:(rank + 1) * rows[i]]) for k, v in nb.items()}
-            for i, nb in enumerate(gb)]
+    if mode.startswith("rows"):                         # unequal rows: rank r's slice of each global batch
+        per = [int(x) for x in mode[4:].split(".")]
+        assert len(per) == world
+        lo, hi = sum(per[:rank]), sum(per[:rank + 1])
+        gb = [pkg.synthetic.make_batch(sum(per), L, H, seed=40 + i) for i in range(steps + 1)]
+        mine = [{k: (None if v is None else v[lo:hi]) for k, v in nb.items()} for nb in gb]
+    else:
+        gb = [pkg.synthetic.make_batch(world * rows[i], L, H, seed=40 + i) for i in range(steps + 1)]
+        mine = [{k: (None if v is None else v[rank * rows[i]:(rank + 1) * rows[i]]) for k, v in nb.items()}
+                for i, nb in enumerate(gb)]
     dev = [{k: torch.as_tensor(v).cuda() for k, v in nb.items() if v is not None} for nb in mine]
     if mode in ("trainer", "trainer_short"):
         tr = trainer_run(pkg, sd, B, L, H, dev, steps, graph)
@@ -51,6 +60,8 @@ def main():
     eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.0,
                                seed=rank, pipeline=pipe, t5_dw_group=groups, device="cuda:0", **ekw)
     assert not c5 or (eng.t5_dw_groups == [8, 8, 6, 2] and eng.fp8)
+    if mode.startswith("rows"):
+        eng.use_global_rows(world)                      # before the first load: a rank may hold 0 rows
     if pipe:
         eng.prime(dev[0]["image_tensors"])
         eng.F4.copy_(eng.F4N)

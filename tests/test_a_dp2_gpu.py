@@ -83,6 +83,46 @@ def test_dp_two_ranks_match_global_batch(gpu, pkg, tmp_path, parity_report, pipe
     assert upd_err <= 5e-2, upd_err
 
 
+@pytest.mark.parametrize("per,pipe", [((4, 1), False), ((4, 0), True), ((1, 3), True)])
+def test_dp_unequal_rows_match_global_batch(gpu, pkg, tmp_path, parity_report, per, pipe):
+    """Ranks holding unequal shares of the global batch (a contiguous split of a batch that does
+    not divide evenly; (4, 0): rank 1 holds none).  The head divides by the all-reduced valid-row
+    count over the world size (engine.use_global_rows, vqa_head_bwd ABI 18), so the summed,
+    1/world-scaled gradients are the global batch's NLL mean (resnet_vqa_model.py:159), and each
+    rank's loss is its share, whose mean over the ranks is the global loss.  Against one engine on
+    the sum(per)-row global batch: ranks bitwise in lockstep, loss at step 0 within 1e-5."""
+    world, steps = 2, 3
+    res = _ranks(tmp_path, world, steps, pipe, True, mode="rows" + ".".join(map(str, per)))
+    for r in res[1:]:
+        assert np.array_equal(r["p32"], res[0]["p32"]), "DP ranks diverged"
+        assert np.array_equal(r["norms"], res[0]["norms"]), "clip norms differ across ranks"
+    if 0 in per:
+        assert res[per.index(0)]["losses"].tolist() == [0.0] * steps, "an empty rank's loss share is 0"
+    import torch
+    B, L, H, n = 4, 32, 64, sum(per)
+    sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
+    ref = pkg.engine.VQAEngine(sd, batch=world * B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.0)
+    gloss, gnorm = [], []
+    for i in range(steps):
+        ref.load_batch(pkg.synthetic.make_batch(n, L, H, seed=40 + i))      # n < 2B rows: padded
+        ref.train_step()
+        torch.cuda.synchronize()
+        gloss.append(float(ref.LOSS.item()))
+        gnorm.append(ref.last_grad_norm())
+    ref.flush_optimizer()
+    p_ref = ref.P32.cpu().numpy()
+    dloss = np.abs(np.mean([r["losses"] for r in res], axis=0) - gloss) / np.abs(gloss)
+    dnorm = np.abs(res[0]["norms"] - gnorm) / np.array(gnorm)
+    p0 = ref.lay.pack(sd)
+    upd_err = float(np.linalg.norm(res[0]["p32"].astype(np.float64) - p_ref) /
+                    np.linalg.norm(p_ref.astype(np.float64) - p0))
+    parity_report["dp2_rows" + "_".join(map(str, per))] = {"loss_rel": dloss.tolist(), "grad_norm_rel": dnorm.tolist(),
+                                                          "update_rel_l2": upd_err}
+    assert dloss[0] <= 1e-5 and dnorm[0] <= 1e-4, (dloss, dnorm)
+    assert (dloss <= 2e-3).all() and (dnorm <= 2e-2).all(), (dloss, dnorm)
+    assert upd_err <= 5e-2, upd_err
+
+
 @pytest.mark.parametrize("mode", ["trainer", "trainer_short"])
 def test_trainer_data_parallel_two_ranks(gpu, pkg, tmp_path, parity_report, mode):
     """`VQATrainer` picks up the initialised process group (world 2) and drives

@@ -51,3 +51,23 @@ def test_short_batch_rows_are_padded_with_real_rows_and_ignored_targets(pkg):
     for bad in (0, 8):
         with pytest.raises(ValueError):
             E.batch_rows({"q": torch.zeros(bad, 2)}, "q", 7)
+
+
+def test_empty_data_parallel_rank_rows(pkg):
+    """A data-parallel rank whose share of the global batch is empty (engine.use_global_rows):
+    batch_rows accepts 0 rows only with allow_empty, and load_rows fills every row -- targets with
+    ignore_index (the rank's gradient is exactly zero), inputs with a finite constant (masks 1)."""
+    import torch
+    E = pkg.engine
+    assert E.batch_rows({"q": torch.zeros(0, 2)}, "q", 7, allow_empty=True) == 0
+    with pytest.raises(ValueError):
+        E.batch_rows({"q": torch.zeros(8, 2)}, "q", 7, allow_empty=True)
+    img = torch.full((4, 3), float("nan"))
+    E.load_rows(img, torch.zeros(0, 3), 0)
+    assert torch.equal(img, torch.zeros(4, 3))
+    mask = torch.zeros(4, 5, dtype=torch.int64)
+    E.load_rows(mask, torch.zeros(0, 5, dtype=torch.int64), 0, empty_fill=1)
+    assert bool((mask == 1).all())
+    tgt = torch.zeros(4, dtype=torch.int64)
+    E.load_rows(tgt, torch.zeros(0, dtype=torch.int64), 0, fill=E.IGNORE_INDEX)
+    assert tgt.tolist() == [-100] * 4

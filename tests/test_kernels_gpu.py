@@ -273,10 +273,56 @@ def test_head_fwd_bwd(k, B, L, A, D, ign):
     dwp, dbp, dwc, dbc = torch.empty_like(wp), torch.empty(1, device="cuda"), torch.empty_like(wc), \
         torch.empty_like(bc)
     ws = torch.empty(k.lib.load().vqa_head_workspace_floats(B, L, D, A), device="cuda")
-    run(k, "vqa_head_bwd", x, att, pooled, logp, tgt, wp, wc, dx, None, dwp, dbp, dwc, dbc, ws, B, L, D, A)
+    run(k, "vqa_head_bwd", x, att, pooled, logp, tgt, wp, wc, dx, None, dwp, dbp, dwc, dbc, ws, B, L, D, A,
+        None, None, None, 1.0)
     torch.cuda.synchronize()
     for got, ref in ((dx, xr.grad), (dwp, wpr.grad), (dbp, bpr.grad), (dwc, wcr.grad), (dbc, bcr.grad)):
         torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,ign,others,world", [(8, 0, 8, 2), (8, 3, 1, 2), (8, 8, 5, 2), (64, 10, 150, 3),
+                                               (300, 40, 0, 1)])
+def test_head_bwd_global_rows(k, B, ign, others, world):
+    """Data-parallel divisor (ABI 18): vqa_count_targets counts this rank's valid rows; with
+    row_total = that count + `others` (the other ranks' rows) and row_scale = world, dlogits are
+    (softmax - onehot) * world / total and the loss is sum(nll) * world / total -- summed over
+    the ranks and scaled by 1/world, the global batch's mean.  ign = B: a rank with no valid row
+    (zero gradient, loss 0)."""
+    L, A, D = 16, 170, 768
+    x = rnd((B, L, D), 30)
+    wp, bp = 0.03 * rnd(D, 31), 0.1 * rnd(1, 32)
+    wc, bc = 0.03 * rnd((A, D), 33), 0.1 * rnd(A, 34)
+    tgt = torch.randint(0, A, (B,), device="cuda")
+    if ign:
+        tgt[B - ign:] = -100
+    cnt = torch.full((1,), -1.0, device="cuda")
+    run(k, "vqa_count_targets", tgt, B, cnt)
+    torch.cuda.synchronize()
+    assert cnt.item() == float(B - ign)
+    total = cnt + others
+    att, pooled, logp = torch.empty(B, L, device="cuda"), torch.empty(B, D, device="cuda"), \
+        torch.empty(B, A, device="cuda")
+    nll, loss = torch.empty(B, device="cuda"), torch.empty(1, device="cuda")
+    run(k, "vqa_head_fwd", x, wp, bp, wc, bc, tgt, att, pooled, logp, nll, loss, B, L, D, A)
+    xr, wpr, bpr, wcr, bcr = (t.clone().requires_grad_(True) for t in (x, wp, bp, wc, bc))
+    a = torch.softmax(xr @ wpr[:, None] + bpr, dim=1)
+    pr = torch.bmm(a.transpose(1, 2), xr).squeeze(1)
+    lp = F.log_softmax(pr @ wcr.T + bcr, -1)
+    ls = F.nll_loss(lp, tgt, reduction="sum") * world / total.item()
+    ls.backward()
+    dx = torch.empty_like(x)
+    dwp, dbp, dwc, dbc = torch.empty_like(wp), torch.empty(1, device="cuda"), torch.empty_like(wc), \
+        torch.empty_like(bc)
+    ws = torch.empty(k.lib.load().vqa_head_workspace_floats(B, L, D, A), device="cuda")
+    run(k, "vqa_head_bwd", x, att, pooled, logp, tgt, wp, wc, dx, None, dwp, dbp, dwc, dbc, ws, B, L, D, A,
+        nll, loss, total, float(world))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(loss[0], ls.detach(), rtol=1e-5, atol=1e-6)
+    for got, ref in ((dx, xr.grad), (dwp, wpr.grad), (dbp, bpr.grad), (dwc, wcr.grad), (dbc, bcr.grad)):
+        if ign == B:
+            assert not got.any()
+        else:
+            torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("T,pad", [(300, 0), (2048, 900), (1, 0), (8192, 5000), (16384, 7000), (40000, 16000)])
@@ -588,3 +634,31 @@ def test_stem_pool_from_the_image_equals_s2d_then_stem_pool(k, n, h):
     run(k, "vqa_stem_pool_img", img, w, b, y, n, h)
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_stem_pool_benched_shape_many_tiles_per_workgroup(k, n):
+    """The benched stem shape (224², B = 64: 6,272 tiles over the persistent grid, ~12 per
+    workgroup, so the register prefetch of the next tile's patch runs many times per workgroup;
+    ADVICE r05): vqa_stem_pool_img and vqa_stem_pool_s2d against vqa_image_to_s2d16 + the
+    implicit-GEMM stem + vqa_maxpool3x3s2_nhwc, bit for bit."""
+    ops = k.ops
+    h = 224
+    hz, oh, ph = h // 2 + 1, h // 2, h // 4
+    img = rnd((n, 3, h, h), 60)
+    w = rnd((64, 4, 4, 16), 61, scale=0.1, dtype=torch.bfloat16)
+    b = rnd(64, 62)
+    z = torch.empty(n, hz, hz, 16, device="cuda", dtype=torch.bfloat16)
+    run(k, "vqa_image_to_s2d16", img, z, n, h, h)
+    s = torch.empty(n, oh, oh, 64, device="cuda", dtype=torch.bfloat16)
+    g = ops.conv_geom(n, hz, hz, 16, oh, oh, 4, 4, 1, 1)
+    ops.run(ops.gemm_desc(z, w, n * oh * oh, 64, 256, lda=256, ldb=256, ga=g, c16=s, ldc16=64, bias=b, relu=True))
+    ref = torch.empty(n, ph, ph, 64, device="cuda", dtype=torch.bfloat16)
+    run(k, "vqa_maxpool3x3s2_nhwc", s, ref, n, oh, oh, 64, ph, ph)
+    y1 = torch.full_like(ref, 5.0)
+    run(k, "vqa_stem_pool_s2d", z, w, b, y1, n, hz, oh)
+    y2 = torch.full_like(ref, 7.0)
+    run(k, "vqa_stem_pool_img", img, w, b, y2, n, h)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, ref)
+    assert torch.equal(y2, ref)

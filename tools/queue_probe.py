@@ -66,8 +66,12 @@ for k in range(1, 9):
     touch(s)
     keep.append(s)
     rows.append({"extra_streams": k, "step_ms": replay_ms()})
+graph = eng.graph
 eng.set_res_cumask(bench.cumask_words("all", torch.cuda.get_device_properties(dev).multi_processor_count))
-eng.res_external = False                               # the stream exists and was used once; the step is unchanged
-touch(eng._rstream)
+masked, handle = eng.reset_res_cumask(destroy=False)  # the engine's own ResNet stream again; the
+eng.graph = graph                                      # masked one exists and is used once, the step unchanged
+touch(masked)
 rows.append({"extra_streams": "8 + one CU-masked (own queue)", "step_ms": replay_ms()})
+torch.cuda.synchronize()
+pkg.lib.hip_runtime().hipStreamDestroy(handle)
 print(json.dumps({"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "rows": rows}))
