@@ -21,6 +21,8 @@ parameters after every step.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -89,6 +91,26 @@ def _wait_only(w):
     return w.wait_only() if hasattr(w, "wait_only") else w.wait()
 
 
+# RCCL collectives are issued with async_op=False from the comm stream: torch's ProcessGroupNCCL then
+# launches them on the CURRENT stream (the comm stream, whose hardware queue the step chooses, DESIGN
+# §5) instead of its own pooled stream, and the host does not block (no blocking-wait mode)
+COMM_ON_STREAM = True
+
+
+class _OnStream:
+    """Collectives already enqueued on the current (comm) stream: wait() makes the waiting stream
+    wait for an event recorded right after them (wait_only is the same: nothing follows)."""
+    def __init__(self):
+        self.ev = torch.cuda.Event()
+        self.ev.record(torch.cuda.current_stream())
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+        return True
+
+    wait_only = wait
+
+
 class _Done:
     """A completed collective (host-staged gloo path): wait() is a no-op."""
     def wait(self):
@@ -144,6 +166,10 @@ def allreduce_buckets(flat, buckets, group=None):
             dist.all_reduce(h, group=group)
             flat[a:b].copy_(h)
         return [_Done() for _ in buckets]
+    if COMM_ON_STREAM and flat.is_cuda:
+        for _, a, b in buckets:
+            dist.all_reduce(flat[a:b], group=group, async_op=False)
+        return [_OnStream()]
     return [dist.all_reduce(flat[a:b], group=group, async_op=True) for _, a, b in buckets]
 
 
@@ -162,6 +188,10 @@ def gather_rows(ids, rows, out_ids, out_rows, group=None):
         w1 = dist.all_gather(list(out_ids.chunk(w)), ids.reshape(-1), group=group, async_op=True)
         w2 = dist.all_gather(list(out_rows.chunk(w)), rows, group=group, async_op=True)
         return [w1, w2]
+    if COMM_ON_STREAM:
+        dist.all_gather_into_tensor(out_ids, ids.reshape(-1), group=group, async_op=False)
+        dist.all_gather_into_tensor(out_rows, rows, group=group, async_op=False)
+        return [_OnStream()]
     w1 = dist.all_gather_into_tensor(out_ids, ids.reshape(-1), group=group, async_op=True)
     w2 = dist.all_gather_into_tensor(out_rows, rows, group=group, async_op=True)
     return [w1, w2]
@@ -329,8 +359,13 @@ class DataParallelStep:
                 # into a separate buffer (no reliance on RCCL's in-place aliasing rule), then
                 # copied into the own chunk on the NCCL work's completion (the wait below)
                 out = self.RS_OUT[self.rs_off[bk_index]:self.rs_off[bk_index] + c]
-                works.append(_Then(dist.reduce_scatter_tensor(out, full, group=self.group, async_op=True),
-                                   lambda out=out, mine=mine: mine.copy_(out)))
+                if COMM_ON_STREAM:                          # on the comm stream, the copy right behind it
+                    dist.reduce_scatter_tensor(out, full, group=self.group, async_op=False)
+                    mine.copy_(out)
+                    works.append(_OnStream())
+                else:
+                    works.append(_Then(dist.reduce_scatter_tensor(out, full, group=self.group, async_op=True),
+                                       lambda out=out, mine=mine: mine.copy_(out)))
         if b > a + N * c:
             works += allreduce_buckets(e.G32, [(None, a + N * c, b)], self.group)
         return [_All(works)]
@@ -425,7 +460,11 @@ class DataParallelStep:
         # its hardware queue
         self.finish_calls = self.tail + [self.emb_call] + ([] if self.shard else list(e.opt_calls))
         # (high-priority streams -- hardware queues of their own -- measured 2.5x slower, r04)
-        self._comm = torch.cuda.Stream(e.dev)               # issues the collectives behind the stage events
+        # issues the collectives behind the stage events (VQA_DP_COMM, an A/B switch: "own" a stream of
+        # its own; "side" / "wside" the engine's capture-only fork streams, whose hardware queue the
+        # replayed graphs do not use -- the graphs run on their execs' internal parallel streams)
+        comm = os.environ.get("VQA_DP_COMM", "wside")
+        self._comm = {"own": None, "side": e._side, "wside": e._wside}[comm] or torch.cuda.Stream(e.dev)
         self._tstream = torch.cuda.Stream(e.dev)            # timing mode: collective completions
 
     def stage_plan(self):

@@ -126,7 +126,10 @@ def test_dp_exchange_never_queues_stage_work_behind_a_collective(pg, pkg, monkey
     world-1 DP step: every collective is issued on the comm stream (never on the step's stream,
     whose packets the stage graphs follow), every wait on a collective is issued on the step's
     stream and only after the LAST stage graph has been replayed (a wait packet holds back every
-    later packet of its hardware queue), and the finish graph comes after those waits."""
+    later packet of its hardware queue), and the finish graph comes after those waits.  The one
+    exception is the valid-row count (engine.use_global_rows): issued before the forward graph,
+    waited on between the forward and the first stage (the head backward reads it) -- the tiny
+    collective has had the whole forward to finish."""
     dpm = pkg.dp
     B, L, H = 4, 32, 96
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
@@ -163,11 +166,20 @@ def test_dp_exchange_never_queues_stage_work_behind_a_collective(pg, pkg, monkey
         return _W(real_ag(*a, **kw))
     monkeypatch.setattr(dist, "all_reduce", all_reduce)
     monkeypatch.setattr(dist, "all_gather_into_tensor", all_gather_into_tensor)
+    real_osw = dpm._OnStream.wait
+
+    def on_stream_wait(self):                        # collectives enqueued on the comm stream (COMM_ON_STREAM)
+        log.append(("wait", torch.cuda.current_stream() == main))
+        return real_osw(self)
+    monkeypatch.setattr(dpm._OnStream, "wait", on_stream_wait)
     for name, g in step.graphs.items():
         monkeypatch.setattr(g, "replay", (lambda n, r: (lambda: (log.append(("graph", n)), r())[1]))(name, g.replay))
     e.load_batch(nb, next_images=nb["image_tensors"])
     step.step()
     torch.cuda.synchronize()
+    # the valid-row count: its collective first (before the forward graph), its wait right after it
+    assert log[0] == ("collective", False) and log[1] == ("graph", "fwd") and log[2] == ("wait", True), log
+    log = log[1:2] + log[3:]
     kinds = [k for k, _ in log]
     assert "collective" in kinds and "wait" in kinds, log
     assert all(not on_main for k, on_main in log if k == "collective"), log   # collectives: comm stream

@@ -9,11 +9,12 @@ vanishes, profiles/r04_dp_ab.txt).
   chain        the chain only (what --res-cumask captures)
   chain_stub   the chain with a 1-element torch kernel forked first on the ResNet stream, joined at the end
   chain_res1   the chain with the ResNet's first call only (the stem) forked first
-  chain_x      the chain issued on a fresh stream forked from the capture stream (the launch
-               stream then carries only the fork and the join)
+  chain_x      the chain issued on a fresh stream forked from the capture stream after a 1-element
+               kernel (the launch stream then carries only that kernel, the fork and the join)
   tiny_first   a 1-element kernel on the capture stream, then the chain
-  python tools/chain_probe.py [variant ...]
+  [PRE=streams:K|cumask|prio] [POST=plain,all,hi:64,...] python tools/chain_probe.py [variant ...]
 """
+import ctypes
 import json
 import os
 import sys
@@ -89,6 +90,7 @@ _x = torch.cuda.Stream(dev)
 
 
 def v_chain_x():
+    tiny.add_(1)              # a node on the capture stream first (a fork from an empty capture crashed capture_end)
     j = forked(chain, _x)
     torch.cuda.current_stream(dev).wait_event(j)
 
@@ -119,6 +121,27 @@ for st in (torch.cuda.current_stream(dev), eng._rstream, _x):      # torch's add
         tiny.add_(1)
 torch.cuda.synchronize()
 
+# PRE: perturb the process's streams / hardware queues BEFORE any capture (a graph exec's
+# internal parallel streams are bound to hardware queues when it is instantiated)
+#   streams:K   K more torch streams, each used once (round-robin over the GPU_MAX_HW_QUEUES queues)
+#   cumask      one CU-masked stream (all CUs; a hardware queue of its own), used once
+#   prio        one high-priority torch stream (a queue of its own), used once
+_pre = os.environ.get("PRE", "")
+_held = []
+if _pre.startswith("streams:"):
+    for _ in range(int(_pre.split(":")[1])):
+        _held.append(torch.cuda.Stream(dev))
+elif _pre == "cumask":
+    eng.set_res_cumask(bench.cumask_words("all", torch.cuda.get_device_properties(dev).multi_processor_count))
+    _held.append(eng._rstream)
+    eng.res_external = False                         # the ResNet branch stays in the captured graph bodies
+elif _pre == "prio":
+    _held.append(torch.cuda.Stream(dev, priority=-1))
+for st in _held:
+    with torch.cuda.stream(st):
+        tiny.add_(1)
+torch.cuda.synchronize()
+
 
 def timed(g, n=10):
     main = torch.cuda.current_stream(dev)
@@ -136,11 +159,64 @@ def timed(g, n=10):
     return round(a.elapsed_time(b) / n, 3), round(t_issue * 1e3 / n, 3)
 
 
-graphs = {v: capture(BODY[v]) for v in variants}
-out = {"env": {k: v for k, v in os.environ.items() if k.startswith(("DEBUG_", "HIP_", "AMD_", "GPU_", "ROC_"))}}
+graphs = {}
+for v in variants:
+    print("capture", v, file=sys.stderr, flush=True)
+    graphs[v] = capture(BODY[v])
+# POST=SPEC[,SPEC...]: AFTER the graphs are instantiated, for each cumask spec (bench.py --res-cumask
+# syntax; "plain" = an ordinary pooled stream) create that stream and time the pipelined step as
+# "chain graph on the launch stream || the next batch's ResNet launched eagerly on that stream"
+# (F4 <- F4N first, joined at the end), plus the chain and full graphs again beside it.
+_post = [x for x in os.environ.get("POST", "").split(",") if x]
+_rs = {}
+for spec in _post:
+    if spec == "plain":
+        _rs[spec] = torch.cuda.Stream(dev)
+    else:
+        import ctypes
+        words = bench.cumask_words(spec, torch.cuda.get_device_properties(dev).multi_processor_count)
+        h = ctypes.c_void_p()
+        arr = (ctypes.c_uint32 * len(words))(*words)
+        rc = pkg.lib.hip_runtime().hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), arr)
+        assert rc == 0, rc
+        _rs[spec] = torch.cuda.ExternalStream(h.value, device=dev)
+    with torch.cuda.stream(_rs[spec]):
+        tiny.add_(1)
+torch.cuda.synchronize()
+
+
+class _Overlap:
+    """replay(): the chain graph beside the ResNet on stream `rs` (eager launches)."""
+    def __init__(self, g, rs):
+        self.g, self.rs = g, rs
+
+    def replay(self):
+        main = torch.cuda.current_stream(dev)
+        eng.copy_f4(pkg.lib.stream_handle(main))
+        f = torch.cuda.Event()
+        f.record(main)
+        self.g.replay()
+        self.rs.wait_event(f)
+        h = pkg.lib.stream_handle(self.rs)
+        for c in eng.res_calls:
+            c(h)
+        j = torch.cuda.Event()
+        j.record(self.rs)
+        main.wait_event(j)
+
+
+if _post and "chain" in graphs:
+    for spec, rs in _rs.items():
+        graphs["chain||res@" + spec] = _Overlap(graphs["chain"], rs)
+    variants = list(graphs)
+out = {"env": {k: v for k, v in os.environ.items() if k.startswith(("DEBUG_", "HIP_", "AMD_", "GPU_", "ROC_", "PRE", "POST"))}}
 for rep in range(2):                              # interleaved twice
     for v in variants:
         ms, host = timed(graphs[v])
         out.setdefault(v, []).append(ms)
         out.setdefault(v + "_host_ms", []).append(host)
 print(json.dumps(out), flush=True)
+torch.cuda.synchronize()
+for spec, rs in _rs.items():                      # the CU-masked streams are ours to destroy
+    if spec != "plain":
+        pkg.lib.hip_runtime().hipStreamDestroy(ctypes.c_void_p(rs.cuda_stream))
