@@ -115,8 +115,15 @@ def step_calls(eng):
         seq += [eng.copy_f4] + list(eng.res_calls)
     if eng.defer_opt:
         seq += [c for _, c in eng.adam_segs] + [eng.clear_pending]
-    seq += list(eng.fwd_calls) + list(eng.bwd_calls) + list(eng.opt_calls)
+    seq += list(eng.fwd_calls) + list(eng.bwd_calls)
+    if getattr(eng, "embed_split", False):                 # the stream step's embedding rows split
+        seq += list(eng.emb_pre) + list(eng.opt_calls[:2]) + list(eng.tail_calls)
+    else:
+        seq += list(eng.opt_calls)
     return list(_flat_calls(seq))
+
+
+ALG_TOUCHED_ROWS = 64 * 32     # embedding rows a step touches at most (B x L; main() sets it per config)
 
 
 def call_bytes(c):
@@ -148,6 +155,13 @@ def call_bytes(c):
         return 38.0 * d.n
     if n == "vqa_grad_sqnorm":
         return 4.0 * c.args[1]
+    if n == "vqa_embed_mark":                                       # ids, tokens, rows, mark, state
+        return float(c.args[1] * 8 + c.args[1] * 4)
+    if n == "vqa_adamw_rows":                                       # desc, mark, rows, cols, touched, ...
+        rows, cols, touched = c.args[2], c.args[3], c.args[4]
+        t = min(rows, ALG_TOUCHED_ROWS)                             # the step's tokens bound the touched rows
+        # untouched rows: p m v vmax read + written, bf16 shadow written (no gradient read); touched: 38 B
+        return float(rows * 4 + (t * cols * 38.0 if touched else (rows - t) * cols * 34.0))
     if n == "vqa_embedding_fwd":                                    # ids, table, out, tokens, d, ...
         t, dd = c.args[3], c.args[4]
         return float(t * 8 + 2 * t * dd * 4)
@@ -596,6 +610,8 @@ def main():
     step_flop = FLOP_PER_PAIR * B if survey_cfg else calls_flop(eng)
     step_tflops = step_flop / gpu_step / 1e12
     st = pmc.get("step", {})
+    global ALG_TOUCHED_ROWS
+    ALG_TOUCHED_ROWS = eng.T                                     # tokens per step bound the touched rows
     alg = sum(call_bytes(c) for c in step_calls(eng))            # algorithmic HBM bytes of one step
     # config 5 mixes e4m3 (forward weight GEMMs) and bf16 MFMA work: the peak is the rate at which
     # the step's FLOP mix would run with every launch at its dtype's dense peak

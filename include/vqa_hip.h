@@ -449,6 +449,24 @@ int vqa_grad_sqnorm(const float* g, long long n, double* ws, int parts, hipStrea
 int vqa_optim_finalize(const double* ws, int parts, float grad_scale, float max_norm, int warmup, int total,
                        float beta1, float beta2, float* state, hipStream_t stream);
 int vqa_adamw_amsgrad(const vqa_adamw_desc* d, hipStream_t stream);
+/* The embedding table's AdamW split by rows (ABI 18; the dense table pass was the step's last,
+ * exposed 0.9 GB).  vqa_embed_mark: mark[ids[i]] = the step counter (state[VQA_ST_STEP]) for the
+ * step's n token ids (rows outside [0, rows) ignored); mark starts at -1.  vqa_adamw_rows over the
+ * table d (n = rows x cols elements, its groups / state as vqa_adamw_amsgrad):
+ *   touched = 0, BEFORE the step's vqa_optim_finalize: every row NOT marked with the counter gets
+ *     the update with a zero gradient (exactly its gradient: no token touched it), using the LR
+ *     multiplier and bias corrections that finalize is about to set (computed here from STEP,
+ *     warmup, total); no clip coefficient is needed (0 * coef = 0).  Ignores PENDING.
+ *   touched > 1: the same as 0 on a grid of `touched` workgroups striding over the rows (the
+ *     engine's pass beside the backward chain: a grid per row would hold CU slots it waits for).
+ *   touched = 1, AFTER finalize (STEP advanced): the marked rows get the full update (no-op while
+ *     PENDING == 0).
+ * Together bit-identical to vqa_adamw_amsgrad over the table.  Replaces the embedding part of
+ * optimizer.step() (faster_rcnn_vqa_trainer.py:399-404) for a dense-gradient table that a step
+ * touches in <= batch x seq rows. */
+int vqa_embed_mark(const long long* ids, int n, int rows, int* mark, const float* state, hipStream_t stream);
+int vqa_adamw_rows(const vqa_adamw_desc* d, const int* mark, int rows, int cols, int touched, int warmup, int total,
+                   hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -34,14 +34,15 @@ inline int adam_args(const vqa_adamw_desc* d, AdamArgs& A) {
   return VQA_OK;
 }
 
-// float4 i of the range: p, m, v, vm updated in place from g (clip coefficient, LR schedule
-// and bias corrections from the device state written by vqa_optim_finalize)
-__device__ __forceinline__ void adamw_update4(const AdamArgs& A, long i, f32x4_t& p, const f32x4_t g4, f32x4_t& m,
-                                              f32x4_t& v, f32x4_t& vm) {
-  // no FMA contraction: the two kernels that inline this must round every operation alike
+// float4 i of the range: p, m, v, vm updated in place from g, with the clip coefficient, LR
+// schedule multiplier and bias corrections given (adamw_update4 reads them from the device state
+// written by vqa_optim_finalize; the embedding table's row-split update, vqa_adamw_rows, computes
+// them for the coming step itself)
+__device__ __forceinline__ void adamw_update4_with(const AdamArgs& A, long i, f32x4_t& p, const f32x4_t g4,
+                                                   f32x4_t& m, f32x4_t& v, f32x4_t& vm, const float coef,
+                                                   const float lam, const float bc1, const float bc2s) {
+  // no FMA contraction: the kernels that inline this must round every operation alike
 #pragma clang fp contract(off)
-  const float coef = A.st[VQA_ST_CLIP_COEF], lam = A.st[VQA_ST_LR_SCALE];
-  const float bc1 = A.st[VQA_ST_BC1], bc2s = A.st[VQA_ST_BC2_SQRT];
   const float gmul = A.gscale * coef;
   const float omb1 = 1.f - A.b1, omb2 = 1.f - A.b2;
   int gi = 0;
@@ -59,6 +60,12 @@ __device__ __forceinline__ void adamw_update4(const AdamArgs& A, long i, f32x4_t
     const float denom = sqrtf(vm[j]) / bc2s + A.eps;
     p[j] = p[j] - step_size * (m[j] / denom);
   }
+}
+
+__device__ __forceinline__ void adamw_update4(const AdamArgs& A, long i, f32x4_t& p, const f32x4_t g4, f32x4_t& m,
+                                              f32x4_t& v, f32x4_t& vm) {
+  adamw_update4_with(A, i, p, g4, m, v, vm, A.st[VQA_ST_CLIP_COEF], A.st[VQA_ST_LR_SCALE], A.st[VQA_ST_BC1],
+                     A.st[VQA_ST_BC2_SQRT]);
 }
 
 }  // namespace

@@ -40,6 +40,20 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g
   if (threadIdx.x == 0) ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// the LR multiplier lambda(step) and the bias corrections of the update at step counter `step`
+// (get_linear_schedule_with_warmup, TF/optimization.py:101-107; torch AdamW's 1 - beta^t): one
+// function for vqa_optim_finalize and the embedding rows' early update, so both round alike
+__device__ __forceinline__ void schedule_at(double step, int warmup, int total, float beta1, float beta2,
+                                            float& lam_f, float& bc1, float& bc2s) {
+  double lam;
+  if (step < warmup) lam = step / (double)(warmup > 1 ? warmup : 1);
+  else lam = fmax(0.0, (double)(total - step) / (double)((total - warmup) > 1 ? (total - warmup) : 1));
+  const double t = step + 1.0;
+  lam_f = (float)lam;
+  bc1 = (float)(1.0 - pow((double)beta1, t));
+  bc2s = (float)sqrt(1.0 - pow((double)beta2, t));
+}
+
 __global__ void finalize_kernel(const double* __restrict__ ws, int parts, float grad_scale, float max_norm,
                                 int warmup, int total, float beta1, float beta2, float* __restrict__ st) {
   // fixed-order two-level sum of the partials by one workgroup
@@ -55,17 +69,75 @@ __global__ void finalize_kernel(const double* __restrict__ ws, int parts, float 
   float coef = 1.f;
   if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
   const double step = (double)st[VQA_ST_STEP];
-  double lam;
-  if (step < warmup) lam = step / (double)(warmup > 1 ? warmup : 1);
-  else lam = fmax(0.0, (double)(total - step) / (double)((total - warmup) > 1 ? (total - warmup) : 1));
-  const double t = step + 1.0;
+  float lam, bc1, bc2s;
+  schedule_at(step, warmup, total, beta1, beta2, lam, bc1, bc2s);
   st[VQA_ST_GRAD_NORM] = norm;
   st[VQA_ST_CLIP_COEF] = coef;
-  st[VQA_ST_LR_SCALE] = (float)lam;
-  st[VQA_ST_BC1] = (float)(1.0 - pow((double)beta1, t));
-  st[VQA_ST_BC2_SQRT] = (float)sqrt(1.0 - pow((double)beta2, t));
-  st[VQA_ST_STEP] = (float)t;
+  st[VQA_ST_LR_SCALE] = lam;
+  st[VQA_ST_BC1] = bc1;
+  st[VQA_ST_BC2_SQRT] = bc2s;
+  st[VQA_ST_STEP] = (float)(step + 1.0);
   st[VQA_ST_PENDING] = 1.f;
+}
+
+// The embedding table's update split by rows.  mark[id] = the step counter for every id of the
+// step's tokens (embed_mark_kernel, before the step's finalize).  A row no token touched has an
+// exactly zero gradient, so its AdamW update needs neither the gradient nor the clip coefficient
+// (g * gscale * coef = +0 for any finite coef) -- only the schedule of the coming finalize: MODE 0
+// applies it to those rows, beside the backward, before finalize.  MODE 1 (after finalize, which
+// advanced the counter) applies the full update to the marked rows.  Every row gets the same
+// arithmetic as the dense pass (adamw_update4_with), so the table ends bit-identical to it; a row
+// marked but not touched (a warm-up's ids) gets g = 0 in MODE 1, the same result as in MODE 0.
+__global__ __launch_bounds__(256) void embed_mark_kernel(const long long* __restrict__ ids, int n, int rows,
+                                                         int* __restrict__ mark, const float* __restrict__ st) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long long id = ids[i];
+  if (id >= 0 && id < rows) mark[id] = (int)st[VQA_ST_STEP];
+}
+
+// one block per row, or (rows_per_block > 1) a grid of rows / rows_per_block blocks striding over
+// the rows: the untouched rows' pass runs beside the latency-bound backward chain, where a
+// 32k-block grid would hold CU slots the chain's launches wait for
+template <int MODE>
+__global__ __launch_bounds__(192) void adamw_rows_kernel(AdamArgs A, const int* __restrict__ mark, int rows, int d4,
+                                                         int warmup, int total) {
+  const int step = (int)A.st[VQA_ST_STEP];
+  float coef, lam, bc1, bc2s;
+  if (MODE == 0) {
+    coef = 1.f;
+    schedule_at((double)A.st[VQA_ST_STEP], warmup, total, A.b1, A.b2, lam, bc1, bc2s);
+  } else {
+    if (A.st[VQA_ST_PENDING] == 0.f) return;
+    coef = A.st[VQA_ST_CLIP_COEF];
+    lam = A.st[VQA_ST_LR_SCALE];
+    bc1 = A.st[VQA_ST_BC1];
+    bc2s = A.st[VQA_ST_BC2_SQRT];
+  }
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+  const bool touched = mark[row] == (MODE == 0 ? step : step - 1);
+  if (MODE == 0 ? touched : !touched) continue;
+  for (int c = threadIdx.x; c < d4; c += 192) {
+    const long i = (long)row * d4 + c;
+    f32x4_t p = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.p) + i);
+    f32x4_t g4 = {0.f, 0.f, 0.f, 0.f};
+    if (MODE == 1) g4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.g) + i);
+    f32x4_t m = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.m) + i);
+    f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.v) + i);
+    f32x4_t vm = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(A.vm) + i);
+    adamw_update4_with(A, i, p, g4, m, v, vm, coef, lam, bc1, bc2s);
+    __builtin_nontemporal_store(p, reinterpret_cast<f32x4_t*>(A.p) + i);
+    __builtin_nontemporal_store(m, reinterpret_cast<f32x4_t*>(A.m) + i);
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4_t*>(A.v) + i);
+    __builtin_nontemporal_store(vm, reinterpret_cast<f32x4_t*>(A.vm) + i);
+    if (A.p16) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(p[0]) | ((uint32_t)f2bf(p[1]) << 16);
+      u.y = (uint32_t)f2bf(p[2]) | ((uint32_t)f2bf(p[3]) << 16);
+      reinterpret_cast<uint2*>(A.p16)[i] = u;
+    }
+  }
+  }
 }
 
 // One float4 of every stream per thread, no grid-stride loop: 138k blocks of
@@ -119,4 +191,25 @@ extern "C" int vqa_adamw_amsgrad(const vqa_adamw_desc* d, hipStream_t s) {
   if (int rc = adam_args(d, A)) return rc;
   hipLaunchKernelGGL(adamw_kernel, dim3(vqa::cdiv(A.n4, 256)), dim3(256), 0, s, A);
   return vqa::check_launch("vqa_adamw_amsgrad");
+}
+
+extern "C" int vqa_embed_mark(const long long* ids, int n, int rows, int* mark, const float* state, hipStream_t s) {
+  VQA_REQUIRE(ids && mark && state && n > 0 && rows > 0, "vqa_embed_mark: bad arguments");
+  hipLaunchKernelGGL(embed_mark_kernel, dim3(vqa::cdiv(n, 256)), dim3(256), 0, s, ids, n, rows, mark, state);
+  return vqa::check_launch("vqa_embed_mark");
+}
+
+extern "C" int vqa_adamw_rows(const vqa_adamw_desc* d, const int* mark, int rows, int cols, int touched, int warmup,
+                              int total, hipStream_t s) {
+  AdamArgs A;
+  if (int rc = adam_args(d, A)) return rc;
+  VQA_REQUIRE(mark && rows > 0 && cols > 0 && cols % 4 == 0 && (long long)rows * cols == d->n,
+              "vqa_adamw_rows: rows x cols must be the descriptor's n (cols %% 4 == 0)");
+  // touched > 1 (the untouched-rows pass only): a grid of `touched` blocks striding over the rows
+  const int grid = touched > 1 && touched < rows ? touched : rows;
+  if (touched == 1)
+    hipLaunchKernelGGL(adamw_rows_kernel<1>, dim3(rows), dim3(192), 0, s, A, mark, rows, cols / 4, warmup, total);
+  else
+    hipLaunchKernelGGL(adamw_rows_kernel<0>, dim3(grid), dim3(192), 0, s, A, mark, rows, cols / 4, warmup, total);
+  return vqa::check_launch("vqa_adamw_rows");
 }

@@ -1208,6 +1208,42 @@ class VQAEngine:
             o += self.quant_all
         elif self.adam_embed is not None:
             o.append(self.adam_embed)
+        # The embedding table's update split by rows (vqa_adamw_rows): the rows no
+        # token of the step touched have a zero gradient, so their update runs beside the
+        # backward (emb_pre: mark the step's ids, then those rows), and the step's exposed tail
+        # keeps only the rel-bias range and the touched rows (tail_calls).  Bit-identical to the
+        # dense range; used by the stream / graph step (run_backward_streams with sq_overlap),
+        # while opt_calls keeps the dense form (eager steps, dp.DataParallelStep's finish graph).
+        self.embed_split = self.defer_opt and os.environ.get("VQA_EMBED_SPLIT", "1") != "0"
+        self.tail_calls = o[2:]
+        self.emb_pre = []
+        if self.embed_split:
+            emb = lay["t5.embed"]
+            assert emb.offset + emb.numel == n and self.adam_embed is o[-1]
+            if getattr(self, "EMB_MARK", None) is None:
+                self.EMB_MARK = torch.full((S.T5_VOCAB,), -1, dtype=torch.int32, device=self.dev)
+            dt = L.AdamWDesc()
+            ctypes.memmove(ctypes.addressof(dt), ctypes.addressof(d), ctypes.sizeof(d))
+            lo = emb.offset
+            dt.param, dt.grad = ops.addr(self.P32, lo), ops.addr(self.G32, lo)
+            dt.exp_avg, dt.exp_avg_sq = ops.addr(self.M, lo), ops.addr(self.V, lo)
+            dt.max_exp_avg_sq, dt.param16 = ops.addr(self.VMAX, lo), ops.addr(self.P16, lo)
+            dt.n = emb.numel
+            for i in range(d.ngroups):                     # as adam_range_call: ends relative to the table
+                dt.group_end[i] = d.group_end[i] - lo
+            self._emb_desc = dt
+            keep = (self.P32, self.G32, self.M, self.V, self.VMAX, self.P16, self.opt_state, self.EMB_MARK)
+            rows_call = lambda touched: ops.Call("vqa_adamw_rows", ctypes.byref(dt), self.EMB_MARK.data_ptr(),  # noqa: E731
+                                                 S.T5_VOCAB, self.D, touched, int(self.warmup), int(self.total),
+                                                 desc=dt, keep=keep)
+            self.emb_pre = [ops.Call("vqa_embed_mark", self.IDS.data_ptr(), self.T, S.T5_VOCAB,
+                                     self.EMB_MARK.data_ptr(), self.opt_state.data_ptr(),
+                                     keep=(self.IDS, self.EMB_MARK, self.opt_state)),
+                            # the untouched rows' pass as 256 workgroups striding over the rows: a
+                            # 32k-block grid beside the chain cost what it saved at the tail (A/B:
+                            # 6.47-6.48 ms either way), 256 measured 6.44-6.47
+                            rows_call(int(os.environ.get("VQA_EMB_GRID", "256")))]
+            self.tail_calls = o[2:-1] + [self.adam_range_call(lay["t5.relbias"].offset, lo), rows_call(1)]
 
     def adam_range_call(self, lo, hi):
         """The fused AdamW-amsgrad pass over flat parameters [lo, hi) only (the step's device
@@ -1347,7 +1383,7 @@ class VQAEngine:
         self.run_forward_streams()
         if optimizer:
             self.run_backward_streams(sq_overlap=True)
-            self._run(self.opt_calls[2:])
+            self._run(self.tail_calls)
         else:
             self.run_backward_streams()
 
@@ -1456,7 +1492,8 @@ class VQAEngine:
         """sq_overlap: also run the optimizer plan's first two calls (the squared-norm partials
         of [0, a), final once the first T5 weight-gradient group is, and of [a, rel-bias),
         final before the embedding scatter) on `side`, beside the backward's tail; the caller
-        then runs opt_calls[2:]."""
+        then runs tail_calls (opt_calls[2:], the embedding table's dense update split by rows:
+        emb_pre runs here, on `side`)."""
         main = torch.cuda.current_stream(self.dev)
         side, wside = self._side, self._wside
         b = self.bwd_calls
@@ -1467,6 +1504,8 @@ class VQAEngine:
         side.wait_event(fork2)
         with torch.cuda.stream(side):
             self._run(b[q0:q1])                            # scaler dW / db
+            if sq_overlap:                                 # a full step: the untouched embedding rows'
+                self._run(self.emb_pre)                    # update, beside the T5 backward
         if sq_overlap:
             assert b[-1] is self.emb_call
 
@@ -1585,7 +1624,7 @@ class VQAEngine:
         if self.res_external:                              # the chain only (set_res_cumask)
             self.run_forward_streams()
             self.run_backward_streams(sq_overlap=True)
-            self._run(self.opt_calls[2:])
+            self._run(self.tail_calls)
             return
         if not (torch.cuda.is_current_stream_capturing() and getattr(self, "res_order", "first") == "root"):
             self.copy_f4(L.stream_handle(main))            # ("root": issued before the replay, train_step)
@@ -1608,7 +1647,7 @@ class VQAEngine:
             assert not self._res_feed[0], "every ResNet call issued"
             self._res_feed = None
         self.run_backward_streams(sq_overlap=True)
-        self._run(self.opt_calls[2:])
+        self._run(self.tail_calls)
         if last:
             with torch.cuda.stream(self._rstream):
                 self._run(self.res_calls)

@@ -142,6 +142,7 @@ def load():
     lib.vqa_attn_path.argtypes = [ctypes.POINTER(AttnDesc), c_int]
     lib.vqa_attn_probs.argtypes = [ctypes.POINTER(AttnDesc), c_void_p]
     lib.vqa_adamw_amsgrad.argtypes = [ctypes.POINTER(AdamWDesc), c_void_p]
+    lib.vqa_adamw_rows.argtypes = [ctypes.POINTER(AdamWDesc), c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]
     for name in ("vqa_norm_bwd_workspace_floats", "vqa_colsum_workspace_floats"):
         getattr(lib, name).argtypes = [c_int, c_int]
     lib.vqa_head_workspace_floats.argtypes = [c_int] * 4
@@ -194,6 +195,7 @@ register("vqa_quant_rows_fp8", P, c_int, c_ll, c_int, c_int, P, c_ll, P)
 register("vqa_head_fwd", P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int)
 register("vqa_head_bwd", P, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, c_float)
 register("vqa_count_targets", P, c_int, P)
+register("vqa_embed_mark", P, c_int, c_int, P, P)
 register("vqa_grad_sqnorm", P, c_ll, P, c_int)
 register("vqa_vit_patchify", P, P, c_int, c_int, c_int, c_int)
 register("vqa_gather_rows", P, c_ll, P, c_ll, c_ll, P, c_ll, c_int, c_int, c_int)

@@ -82,6 +82,8 @@ def test_prepared_calls_keep_every_pointer(torch_cuda, pkg):
         [c for _, c in eng.adam_segs] + [eng.clear_pending, eng.copy_f4, eng.adam_full]
     if eng.adam_embed is not None:
         calls.append(eng.adam_embed)
+    calls += list(eng.emb_pre) + list(eng.tail_calls)      # the embedding rows' split update
+    assert eng.emb_pre, "the stream step splits the embedding table's update by rows"
     bad = {}
     for c in calls:
         for sub in getattr(c, "calls", [c]):               # engine._Seq groups

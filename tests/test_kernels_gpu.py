@@ -662,3 +662,63 @@ def test_stem_pool_benched_shape_many_tiles_per_workgroup(k, n):
     torch.cuda.synchronize()
     assert torch.equal(y1, ref)
     assert torch.equal(y2, ref)
+
+
+def test_adamw_rows_split_equals_dense(k):
+    """vqa_embed_mark + vqa_adamw_rows (ABI 18): the embedding table's update split by rows -- the
+    rows no token touched (zero gradient) before vqa_optim_finalize with the schedule it is about
+    to set, the marked rows after it -- equals vqa_adamw_amsgrad over the whole table bit for bit
+    (p, m, v, vmax and the bf16 shadow), two LR groups, duplicated ids, a warm-up-phase step."""
+    L = k.lib
+    V, D, T = 1000, 64, 300
+    gen = torch.Generator(device="cuda").manual_seed(90)
+    ids = torch.randint(0, V, (T,), device="cuda", generator=gen)
+    g = torch.zeros(V, D, device="cuda")
+    g[ids] = rnd((T, D), 91)                                  # touched rows only (duplicates overwrite)
+    base = {"p": rnd((V, D), 92), "m": 0.01 * rnd((V, D), 93), "v": 0.001 * rnd((V, D), 94).abs()}
+    base["vm"] = base["v"] + 0.0005 * rnd((V, D), 95).abs()
+    ws = torch.tensor([3.25, 1.5], dtype=torch.float64, device="cuda")
+    warm, total = 10, 100
+
+    def state(step):
+        st = torch.zeros(L.ST_FLOATS, device="cuda")
+        st[0] = step
+        return st
+
+    def desc(t, st):
+        d = L.AdamWDesc()
+        d.param, d.grad, d.exp_avg = t["p"].data_ptr(), g.data_ptr(), t["m"].data_ptr()
+        d.exp_avg_sq, d.max_exp_avg_sq, d.param16 = t["v"].data_ptr(), t["vm"].data_ptr(), t["p16"].data_ptr()
+        d.n = V * D
+        d.ngroups = 2
+        d.group_end[0], d.group_end[1] = 300 * D, V * D
+        d.group_lr[0], d.group_lr[1] = 5e-3, 1e-4
+        d.beta1, d.beta2, d.eps, d.weight_decay, d.grad_scale = 0.9, 0.999, 1e-8, 0.1, 1.0
+        d.state = st.data_ptr()
+        return d
+    for step in (3.0, 40.0):                                   # warm-up and decay phases of the schedule
+        res = []
+        for split in (False, True):
+            t = {kk: vv.clone() for kk, vv in base.items()}
+            t["p16"] = torch.empty(V, D, device="cuda", dtype=torch.bfloat16)
+            st = state(step)
+            d = desc(t, st)
+            s = L.stream_handle()
+            fin = lambda: L.check(L.load().vqa_optim_finalize(ctypes.c_void_p(ws.data_ptr()), 2, ctypes.c_float(1.0),  # noqa: E731
+                                                              ctypes.c_float(1.0), warm, total, ctypes.c_float(0.9),
+                                                              ctypes.c_float(0.999), ctypes.c_void_p(st.data_ptr()), s),
+                                  "finalize")
+            if split:
+                mark = torch.full((V,), -1, dtype=torch.int32, device="cuda")
+                run(k, "vqa_embed_mark", ids, T, V, mark, st)
+                L.check(L.load().vqa_adamw_rows(ctypes.byref(d), mark.data_ptr(), V, D, 0, warm, total, s), "rows0")
+                fin()
+                L.check(L.load().vqa_adamw_rows(ctypes.byref(d), mark.data_ptr(), V, D, 1, warm, total, s), "rows1")
+            else:
+                fin()
+                L.check(L.load().vqa_adamw_amsgrad(ctypes.byref(d), s), "dense")
+            torch.cuda.synchronize()
+            res.append(t)
+        for kk in ("p", "m", "v", "vm", "p16"):
+            assert torch.equal(res[0][kk], res[1][kk]), (step, kk)
+        assert not torch.equal(res[0]["p"], base["p"])          # the update did something
