@@ -197,6 +197,25 @@ def gather_rows(ids, rows, out_ids, out_rows, group=None):
     return [w1, w2]
 
 
+def gather_tensor(x, out, group=None):
+    """All-gather one tensor per rank into `out` (rank-major): the step's token ids at its start,
+    the (id-ordered) embedding-gradient rows after the backward.  gloo: staged through host memory."""
+    import torch.distributed as dist
+    w = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo":
+        if x.is_cuda:
+            h = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_gather(list(h.chunk(w)), x.reshape(-1, *out.shape[1:]).cpu(), group=group)
+            out.copy_(h)
+            return [_Done()]
+        dist.all_gather(list(out.chunk(w)), x.reshape(-1, *out.shape[1:]), group=group)
+        return [_Done()]
+    if COMM_ON_STREAM:
+        dist.all_gather_into_tensor(out, x.reshape(-1, *out.shape[1:]), group=group, async_op=False)
+        return [_OnStream()]
+    return [dist.all_gather_into_tensor(out, x.reshape(-1, *out.shape[1:]), group=group, async_op=True)]
+
+
 # share of the next batch's frozen-ResNet calls forked beside the forward graph (pipelined
 # engines; the rest go beside the first backward stage), DataParallelStep(res_split=...)
 RES_SPLIT = 1.0
@@ -264,13 +283,17 @@ class DataParallelStep:
         assert e.bwd_calls[-1] is e.emb_call
         T, D = e.T, e.D
         dev = e.dev
+        # every rank's token ids, gathered at the start of the step (with the valid-row count): the
+        # embedding rows the step touches on ANY rank are known before the backward, so the table's
+        # untouched rows are updated beside it (engine.emb_pre) and only the gradient rows (GDH)
+        # are gathered after the backward.  The rows to re-zero are the previous step's gathered
+        # ids (every rank's rows were written): GIDS_PREV, then GIDS_PREV <- GIDS.
         self.GIDS = torch.zeros(self.world * T, dtype=torch.int64, device=dev)
-        # the rows to re-zero are the previous step's GATHERED ids (every rank's rows were written);
-        # GIDS still holds them when the backward starts (the gather runs after the first segment)
+        self.GIDS_PREV = torch.zeros(self.world * T, dtype=torch.int64, device=dev)
         assert calls[0] is e.zero_calls[0]
         g = e.g32["t5.embed"]
-        calls = [ops.Call("vqa_embedding_zero_rows", self.GIDS.data_ptr(), None, self.world * T, g.data_ptr(), D,
-                          S.T5_VOCAB, keep=(self.GIDS, g))] + calls[1:]
+        calls = [ops.Call("vqa_embedding_zero_rows", self.GIDS_PREV.data_ptr(), self.GIDS.data_ptr(), self.world * T,
+                          g.data_ptr(), D, S.T5_VOCAB, keep=(self.GIDS_PREV, self.GIDS, g))] + calls[1:]
         self.segments, prev = [], 0
         for ci, _, _ in self.buckets:
             self.segments.append(calls[prev:ci])
@@ -458,7 +481,35 @@ class DataParallelStep:
         # behind the early buckets' collectives: at world 1 they did not overlap anything (trace), and at
         # N > 1 that stream's wait on a running collective would hold back whatever stage kernels share
         # its hardware queue
-        self.finish_calls = self.tail + [self.emb_call] + ([] if self.shard else list(e.opt_calls))
+        # the embedding table's update split by rows (engine.emb_pre; bit-identical to the dense
+        # range): the rows no rank touched beside the first stage (marks from the gathered ids),
+        # the rel-bias range and the touched rows in the finish graph.  The squared-norm partials of
+        # [0, a) (engine._sq_split) run on the comm stream right behind the all-reduce that completes
+        # that prefix, so the finish keeps only the later partials.
+        self.emb_pre = []
+        self._sq0_stage = None
+        opt = list(e.opt_calls)
+        if not self.shard:
+            if e.embed_split:
+                self.emb_pre = [ops.Call("vqa_embed_mark", self.GIDS.data_ptr(), self.world * e.T, S.T5_VOCAB,
+                                         e.EMB_MARK.data_ptr(), e.opt_state.data_ptr(),
+                                         keep=(self.GIDS, e.EMB_MARK, e.opt_state)), e.emb_pre[1]]
+                self.stages[0]["ops"].insert(0, ("emb", self.emb_pre))
+                opt = opt[:2] + list(e.tail_calls)
+            a = e._sq_split[1] if e._sq_split is not None else None
+            if a is not None:
+                done = 0
+                for j, st in enumerate(self.stages):
+                    if st["final"]:
+                        done = max(done, max(self.buckets[k][2] for k in st["final"]))
+                    if done >= a and st["final"]:
+                        self._sq0_stage = j
+                        break
+            if self._sq0_stage is not None:
+                assert opt[0].name == "vqa_grad_sqnorm"
+                self._sq0_call = opt[0]
+                opt = opt[1:]
+        self.finish_calls = self.tail + [self.emb_call] + ([] if self.shard else opt)
         # (high-priority streams -- hardware queues of their own -- measured 2.5x slower, r04)
         # issues the collectives behind the stage events (VQA_DP_COMM, an A/B switch: "own" a stream of
         # its own; "side" / "wside" the engine's capture-only fork streams, whose hardware queue the
@@ -470,7 +521,8 @@ class DataParallelStep:
     def stage_plan(self):
         """Per stage: its calls in order as ("chain" | "dw_fork", count), and the buckets final
         after it."""
-        return [{"ops": [({"main": "chain", "fork": "dw_fork", "res": "resnet_fork"}[kd], len(c)) for kd, c in st["ops"]],
+        return [{"ops": [({"main": "chain", "fork": "dw_fork", "res": "resnet_fork", "emb": "embedding_rows_fork"}[kd],
+                          len(c)) for kd, c in st["ops"]],
                  "final_buckets": st["final"]} for st in self.stages]
 
     def _run_stage(self, st):
@@ -483,8 +535,8 @@ class DataParallelStep:
         for kind, calls in st["ops"]:
             if kind == "main":
                 self._run(calls)
-            else:                                           # "fork": pending dW; "res": the next batch's ResNet
-                side = e._wside if kind == "fork" else e._rstream
+            else:     # "fork": pending dW; "res": the next batch's ResNet; "emb": the untouched embedding rows
+                side = {"fork": e._wside, "res": e._rstream, "emb": e._side}[kind]
                 _after(side, main)
                 with torch.cuda.stream(side):
                     self._run(calls)
@@ -527,7 +579,7 @@ class DataParallelStep:
             _after(comm, main)
             with torch.cuda.stream(comm):
                 if j == self.rows_stage:
-                    works["rows"] = gather_rows(e.IDS, e.dH32, self.GIDS, self.GDH, self.group)
+                    works["rows"] = gather_tensor(e.dH32, self.GDH, self.group)
                     mark_done("rows", works["rows"])
                 if self.shard:
                     for k in st["final"]:
@@ -540,6 +592,8 @@ class DataParallelStep:
                     for k in ks:
                         works[k] = ws if k == ks[-1] else []
                         mark_done(k, ws)
+                    if j == self._sq0_stage and (COMM_ON_STREAM or _staged(e.G32, self.group)):
+                        self._sq0_call(L.stream_handle(comm))     # behind the all-reduce of [0, a)
         if tm is not None:
             tm["wait"] = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             tm["wait"][0].record(main)
@@ -604,20 +658,24 @@ class DataParallelStep:
         if self._res_a:
             _after(main, e._rstream)
 
-    def _exchange_row_total(self):
-        """This rank's valid-row count (vqa_count_targets, on the step's stream), summed over the
-        ranks on the comm stream; the head backward (first backward stage) reads the sum.  Issued
-        before the forward, waited on after it: the tiny collective runs while the forward does."""
+    def _exchange_step_start(self):
+        """The step's opening exchange, on the comm stream: this rank's valid-row count
+        (vqa_count_targets, on the step's stream) summed over the ranks -- the head backward (first
+        backward stage) divides by it -- and every rank's token ids gathered into GIDS (the
+        embedding rows the step touches anywhere: the untouched rows' update in the first stage,
+        the re-zeroing and the scatter).  Issued before the forward, waited on after it: the two
+        small collectives run while the forward does."""
         e = self.eng
         main = torch.cuda.current_stream(e.dev)
         e.count_call(L.stream_handle(main))
         _after(self._comm, main)
         with torch.cuda.stream(self._comm):
-            return allreduce_buckets(e.ROWTOT, [(None, 0, 1)], self.group)
+            ws = allreduce_buckets(e.ROWTOT, [(None, 0, 1)], self.group)
+            return ws + gather_tensor(e.IDS, self.GIDS, self.group)
 
     def step(self):
         e = self.eng
-        rows = self._exchange_row_total()
+        rows = self._exchange_step_start()
         if e.pipeline:                                      # F4 <- F4N: this batch's features (last step's ResNet)
             e.copy_f4(L.stream_handle(torch.cuda.current_stream(e.dev)))
         if self.graphs is not None:

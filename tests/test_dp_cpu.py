@@ -92,6 +92,11 @@ def _allreduce_worker(rank, world, port, pkg_dir):
     for r in range(world):
         assert torch.equal(gi[r * T:(r + 1) * T], torch.tensor([5, 7, 5, 0, 0, 9]) + r)
         assert torch.equal(gr[r * T:(r + 1) * T], torch.arange(T * D, dtype=torch.float32).reshape(T, D) + 100 * r)
+    # the step's opening id gather and the later row gather as separate collectives (r06)
+    gi2, gr2 = torch.zeros(world * T, dtype=torch.int64), torch.zeros(world * T, D)
+    for w in dp.gather_tensor(ids.reshape(2, 3), gi2) + dp.gather_tensor(rows, gr2):
+        w.wait()
+    assert torch.equal(gi2, gi) and torch.equal(gr2, gr)
     # gathered scatter == all-reduce of the per-rank dense scatters (what the reference computes)
     dense = torch.zeros(20, D).index_add_(0, ids, rows)
     dist.all_reduce(dense)

@@ -127,9 +127,10 @@ def test_dp_exchange_never_queues_stage_work_behind_a_collective(pg, pkg, monkey
     whose packets the stage graphs follow), every wait on a collective is issued on the step's
     stream and only after the LAST stage graph has been replayed (a wait packet holds back every
     later packet of its hardware queue), and the finish graph comes after those waits.  The one
-    exception is the valid-row count (engine.use_global_rows): issued before the forward graph,
-    waited on between the forward and the first stage (the head backward reads it) -- the tiny
-    collective has had the whole forward to finish."""
+    exception is the step's opening exchange -- the valid-row count (engine.use_global_rows) and
+    the token-id gather: issued before the forward graph, waited on between the forward and the
+    first stage (the head backward reads the count, the first stage the ids) -- two small
+    collectives that have had the whole forward to finish."""
     dpm = pkg.dp
     B, L, H = 4, 32, 96
     sd = pkg.synthetic.make_state_dict("resnet50", seed=0)
@@ -177,9 +178,10 @@ def test_dp_exchange_never_queues_stage_work_behind_a_collective(pg, pkg, monkey
     e.load_batch(nb, next_images=nb["image_tensors"])
     step.step()
     torch.cuda.synchronize()
-    # the valid-row count: its collective first (before the forward graph), its wait right after it
-    assert log[0] == ("collective", False) and log[1] == ("graph", "fwd") and log[2] == ("wait", True), log
-    log = log[1:2] + log[3:]
+    # the opening exchange -- the valid-row count and the token-id gather -- first (before the
+    # forward graph), its waits right after it
+    assert log[:5] == [("collective", False)] * 2 + [("graph", "fwd")] + [("wait", True)] * 2, log
+    log = log[2:3] + log[5:]
     kinds = [k for k, _ in log]
     assert "collective" in kinds and "wait" in kinds, log
     assert all(not on_main for k, on_main in log if k == "collective"), log   # collectives: comm stream
