@@ -354,6 +354,10 @@ __device__ __forceinline__ float epi_act(float v, int a) {
 template <int BM, int BN, int STAGES, int NWM, int NWN, bool EXT = false, int BKT = BK>
 __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&acc)[BM / NWM / 32][BN / NWN / 32],
                                               const int z, const int m0, const int n0, const int mlim, char* smem) {
+  // no FMA contraction: every tile config and epilogue path (operands prefetched or loaded in the
+  // sweep, vectorised or scalar) must round each element the same way -- the config is a speed
+  // choice only (tests/test_gemm_gpu.py::test_all_tile_configs_bitwise_identical)
+#pragma clang fp contract(off)
   constexpr int NW = NWM * NWN, NT = 64 * NW;
   constexpr int WM = BM / NWM, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
   constexpr int ST_BYTES = (BM + BN) * BKT * 2;
@@ -392,11 +396,42 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
     float* img = reinterpret_cast<float*>(smem);
     constexpr int TPR = BN / 8;                         // threads per row
     constexpr int RPP = NT / TPR;                       // rows per sweep
+    constexpr int NSW = (HALF + RPP - 1) / RPP;         // row sweeps per pass
+    // Operand prefetch: the residual (fp32 or bf16) -- or, without one, the old C of a beta
+    // epilogue -- and the ReLU mask of every sweep of a pass are loaded BEFORE the pass's LDS
+    // staging, so their HBM round trips overlap each other and the staging.  In the sweep loop
+    // each sweep's stores precede the next sweep's loads (a C store may alias later operand rows,
+    // so the compiler keeps that order): one dependent round trip per sweep, ~4 us per 128 x 64
+    // tile of the ResNet's residual 1x1 convolutions (r05 stamps).  Same operands, same
+    // arithmetic: the bits do not change.  Up to 4 sweeps (the register budget).
+    constexpr bool PF = NSW <= 4;
+    const int pfk = R32 ? 1 : (R16 ? 2 : (beta ? 3 : 0));   // what pre[] holds
+    f32x4_t pre[PF ? NSW : 1][2];                      // native vectors: register-resident (float4
+    i32x4_t mpre[PF ? NSW : 1];                         // structs would live in scratch)
     // __syncthreads (waits for this wave's LDS ops, then barriers); no LDS-DMA is in flight now
     __syncthreads();                                    // every wave is done with the ring
 #pragma unroll
     for (int pass = 0; pass < NWM * GPW; ++pass) {
       const int pw = pass / GPW, pg = pass % GPW;
+      if constexpr (PF) {
+        const int c = (tid % TPR) * 8, col = n0 + c;
+#pragma unroll
+        for (int sw = 0; sw < NSW; ++sw) {
+          const int r = sw * RPP + tid / TPR, row = m0 + pw * WM + pg * HALF + r;
+          if ((HALF % RPP != 0 && r >= HALF) || (NT % TPR != 0 && tid >= RPP * TPR) || row >= mlim || col >= P.n)
+            continue;
+          if (pfk == 1) {
+            pre[sw][0] = *reinterpret_cast<const f32x4_t*>(R32 + (long)row * P.ldres + col);
+            pre[sw][1] = *reinterpret_cast<const f32x4_t*>(R32 + (long)row * P.ldres + col + 4);
+          } else if (pfk == 2) {
+            pre[sw][0] = __builtin_bit_cast(f32x4_t, *reinterpret_cast<const i32x4_t*>(R16 + (long)row * P.ldres + col));
+          } else if (pfk == 3) {
+            pre[sw][0] = *reinterpret_cast<const f32x4_t*>(C32 + (long)row * P.ldc32 + col);
+            pre[sw][1] = *reinterpret_cast<const f32x4_t*>(C32 + (long)row * P.ldc32 + col + 4);
+          }
+          if (MK) mpre[sw] = *reinterpret_cast<const i32x4_t*>(MK + (long)row * P.ldmask + col);
+        }
+      }
       if (wm == pw) {
 #pragma unroll
         for (int ii = 0; ii < G; ++ii)
@@ -414,8 +449,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
       __syncthreads();                                  // the fragment writes have landed
       const int c = (tid % TPR) * 8, col = n0 + c;
 #pragma unroll
-      for (int r0 = 0; r0 < HALF; r0 += RPP) {
-        const int r = r0 + tid / TPR, row = m0 + pw * WM + pg * HALF + r;
+      for (int sw = 0; sw < NSW; ++sw) {
+        const int r = sw * RPP + tid / TPR, row = m0 + pw * WM + pg * HALF + r;
         if (HALF % RPP != 0 && r >= HALF) continue;
         if (NT % TPR != 0 && tid >= RPP * TPR) continue;   // BN = 192: 24 threads per row, 10 rows per sweep
         if (row >= mlim || col >= P.n) continue;
@@ -426,8 +461,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
 #pragma unroll
         for (int t = 0; t < 8; ++t) kf[t] = 1.f;
         if (MK) {
-          const uint4 m4 = *reinterpret_cast<const uint4*>(MK + (long)row * P.ldmask + col);
-          const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
+          const i32x4_t m4 = PF ? mpre[PF ? sw : 0] : *reinterpret_cast<const i32x4_t*>(MK + (long)row * P.ldmask + col);
+          const uint32_t mw[4] = {(uint32_t)m4[0], (uint32_t)m4[1], (uint32_t)m4[2], (uint32_t)m4[3]};
 #pragma unroll
           for (int t = 0; t < 8; ++t)
             if (!(bf2f((t & 1) ? (mw[t >> 1] >> 16) : (mw[t >> 1] & 0xffff)) > 0.f)) kf[t] = 0.f;
@@ -447,14 +482,16 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
 #pragma unroll
         for (int t = 0; t < 8; ++t) v[t] *= kf[t];
         if (R32) {
-          const float4 a0 = *reinterpret_cast<const float4*>(R32 + (long)row * P.ldres + col);
-          const float4 a1 = *reinterpret_cast<const float4*>(R32 + (long)row * P.ldres + col + 4);
-          v[0] += a0.x; v[1] += a0.y; v[2] += a0.z; v[3] += a0.w;
-          v[4] += a1.x; v[5] += a1.y; v[6] += a1.z; v[7] += a1.w;
+          const bool pr = PF && pfk == 1;
+          const f32x4_t a0 = pr ? pre[PF ? sw : 0][0] : *reinterpret_cast<const f32x4_t*>(R32 + (long)row * P.ldres + col);
+          const f32x4_t a1 = pr ? pre[PF ? sw : 0][1] : *reinterpret_cast<const f32x4_t*>(R32 + (long)row * P.ldres + col + 4);
+          v[0] += a0[0]; v[1] += a0[1]; v[2] += a0[2]; v[3] += a0[3];
+          v[4] += a1[0]; v[5] += a1[1]; v[6] += a1[2]; v[7] += a1[3];
         }
         if (R16) {
-          const uint4 q = *reinterpret_cast<const uint4*>(R16 + (long)row * P.ldres + col);
-          const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+          const i32x4_t q = (PF && pfk == 2) ? __builtin_bit_cast(i32x4_t, pre[PF ? sw : 0][0])
+                               : *reinterpret_cast<const i32x4_t*>(R16 + (long)row * P.ldres + col);
+          const uint32_t qw[4] = {(uint32_t)q[0], (uint32_t)q[1], (uint32_t)q[2], (uint32_t)q[3]};
 #pragma unroll
           for (int t = 0; t < 8; ++t) v[t] += bf2f((t & 1) ? (qw[t >> 1] >> 16) : (qw[t >> 1] & 0xffff));
         }
@@ -466,7 +503,9 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
           float4* cp = reinterpret_cast<float4*>(C32 + (long)row * P.ldc32 + col);
           float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
           if (beta) {
-            const float4 c0 = cp[0], c1 = cp[1];
+            const bool pc = PF && pfk == 3;                 // prefetched old C (no residual)
+            const f32x4_t c0 = pc ? pre[PF ? sw : 0][0] : *reinterpret_cast<const f32x4_t*>(cp),
+                          c1 = pc ? pre[PF ? sw : 0][1] : *reinterpret_cast<const f32x4_t*>(cp + 1);
             o0.x += P.beta * c0.x; o0.y += P.beta * c0.y; o0.z += P.beta * c0.z; o0.w += P.beta * c0.w;
             o1.x += P.beta * c1.x; o1.y += P.beta * c1.y; o1.z += P.beta * c1.z; o1.w += P.beta * c1.w;
           }
