@@ -34,8 +34,8 @@ FLOP_PER_PAIR = 30.95e9        # fwd+bwd algorithmic FLOPs
 MFMA_PEAK_TFLOPS = 2517.0      # bf16 dense: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md)
 FP8_PEAK_TFLOPS = 5034.0       # e4m3 dense, block-scaled MFMA (2x the bf16 rate per clock, MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
-PMC_FILE = "r05_pmc.json"               # rocprofv3 PMC summary this bench quotes (tools/pmc_step.py)
-PMC_FILE_C5 = "r05_pmc_c5.json"         # the same passes over the config-5 step (bench.py --config5)
+PMC_FILE = "r06_pmc.json"               # rocprofv3 PMC summary this bench quotes (tools/pmc_step.py)
+PMC_FILE_C5 = "r06_pmc_c5.json"         # the same passes over the config-5 step (bench.py --config5)
 DIGEST_SUFFIXES = (".py", ".hip", ".h", ".inl", ".json", "Makefile")
 
 
