@@ -160,8 +160,10 @@ def call_bytes(c):
     if n == "vqa_adamw_rows":                                       # desc, mark, rows, cols, touched, ...
         rows, cols, touched = c.args[2], c.args[3], c.args[4]
         t = min(rows, ALG_TOUCHED_ROWS)                             # the step's tokens bound the touched rows
-        # untouched rows: p m v vmax read + written, bf16 shadow written (no gradient read); touched: 38 B
-        return float(rows * 4 + (t * cols * 38.0 if touched else (rows - t) * cols * 34.0))
+        # touched == 1: the marked rows after finalize, 38 B each; 0 or > 1 (the grid size of the pass
+        # beside the backward): the untouched rows, p m v vmax read + written and the bf16 shadow
+        # written, no gradient read
+        return float(rows * 4 + (t * cols * 38.0 if touched == 1 else (rows - t) * cols * 34.0))
     if n == "vqa_embedding_fwd":                                    # ids, table, out, tokens, d, ...
         t, dd = c.args[3], c.args[4]
         return float(t * 8 + 2 * t * dd * 4)

@@ -60,3 +60,11 @@ def test_byte_model_of_argument_calls():
     # stride-2 subsample of a 56x56x256 map: read and write the 28x28 samples
     assert bench.call_bytes(C("vqa_subsample_nhwc", 0, 64, 56, 56, 256, 2, 0, 384)) == 2 * 64 * 28 * 28 * 256 * 2
     assert bench.call_bytes(C("vqa_maxpool3x3s2_nhwc", 0, 0, 2, 21, 21, 64, 11, 11)) == (2 * 21 * 21 + 2 * 11 * 11) * 128
+    # the embedding table's row-split AdamW (ABI 18): `touched` 1 = the marked rows after finalize
+    # (38 B each); 0 or a grid size > 1 = the untouched rows beside the backward (34 B: no gradient)
+    rows, cols = 32128, 768
+    t = min(rows, bench.ALG_TOUCHED_ROWS)
+    assert bench.call_bytes(C("vqa_adamw_rows", 0, 0, rows, cols, 1, 0, 0)) == rows * 4 + t * cols * 38
+    for touched in (0, 256):
+        assert bench.call_bytes(C("vqa_adamw_rows", 0, 0, rows, cols, touched, 0, 0)) == \
+            rows * 4 + (rows - t) * cols * 34
