@@ -9,7 +9,8 @@ picked up from the initialised process group) instead of the engine directly; `t
 the same with a short last batch (3 rows per rank, padded to the planned 4); `shard`: the
 engine step with the sharded optimizer (reduce-scatter, AdamW on the own chunks, all-gather);
 `c5`: the engine step at BASELINE configs[4] widths (T5-large, 6 SGA blocks, fp8 forward GEMMs,
-T5 weight-gradient groups (8, 8, 6, 2)); `rows<R0>.<R1>...`: unequal rows per rank (rank r takes
+T5 weight-gradient groups (8, 8, 6, 2)); `c5full`: the same at the benched shape (B = 64 per rank,
+384^2, 24 MB buckets); `rows<R0>.<R1>...`: unequal rows per rank (rank r takes
 the next R_r samples of each sum(R)-row global batch; R_r = 0: an empty rank), the engine planned
 for B = 4 rows with the global-batch NLL mean (engine.use_global_rows)."""
 import os
@@ -31,8 +32,9 @@ def main():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     mode = sys.argv[8] if len(sys.argv) > 8 else "engine"
-    c5 = mode == "c5"
-    B, L, H = 4, 32, 64
+    c5 = mode in ("c5", "c5full")
+    # c5full: the benched config-5 shape itself (B = 64 per rank, 384^2; tools/c5_dp2_parity.py)
+    B, L, H = (64, 32, 384) if mode == "c5full" else (4, 32, 64)
     # c5: BASELINE configs[4] widths -- T5-large (24 layers, d 1024), 6 SGA blocks at 1024, e4m3
     # forward weight GEMMs, the DP weight-gradient groups dp.dp_t5_dw_groups(24) = (8, 8, 6, 2)
     ekw = dict(language_model="t5-large", num_blocks=6, fp8=True) if c5 else {}
@@ -69,7 +71,8 @@ def main():
     else:
         eng.load_batch(dev[0])
     shard = mode == "shard"
-    step = pkg.dp.DataParallelStep(eng, bucket_mb=8, use_graph=graph, shard_optimizer=shard)
+    step = pkg.dp.DataParallelStep(eng, bucket_mb=24 if mode == "c5full" else 8, use_graph=graph,
+                                   shard_optimizer=shard)
     if pipe:
         eng.prime(dev[0]["image_tensors"])
     losses, norms = [], []
