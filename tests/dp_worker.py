@@ -9,8 +9,8 @@ picked up from the initialised process group) instead of the engine directly; `t
 the same with a short last batch (3 rows per rank, padded to the planned 4); `shard`: the
 engine step with the sharded optimizer (reduce-scatter, AdamW on the own chunks, all-gather);
 `c5`: the engine step at BASELINE configs[4] widths (T5-large, 6 SGA blocks, fp8 forward GEMMs,
-T5 weight-gradient groups (8, 8, 6, 2)); `c5full`: the same at the benched shape (B = 64 per rank,
-384^2, 24 MB buckets); `rows<R0>.<R1>...`: unequal rows per rank (rank r takes
+T5 weight-gradient groups (8, 8, 6, 2)); `c5full` / `c2full`: config 5 / config 2 at the benched shape
+(B = 64 per rank, 384^2 / 224^2, 24 MB buckets, tools/dp_full_parity.py); `rows<R0>.<R1>...`: unequal rows per rank (rank r takes
 the next R_r samples of each sum(R)-row global batch; R_r = 0: an empty rank), the engine planned
 for B = 4 rows with the global-batch NLL mean (engine.use_global_rows)."""
 import os
@@ -33,8 +33,10 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     mode = sys.argv[8] if len(sys.argv) > 8 else "engine"
     c5 = mode in ("c5", "c5full")
-    # c5full: the benched config-5 shape itself (B = 64 per rank, 384^2; tools/c5_dp2_parity.py)
-    B, L, H = (64, 32, 384) if mode == "c5full" else (4, 32, 64)
+    full = mode in ("c2full", "c5full")
+    # c2full / c5full: the benched config-2 / config-5 shape itself (B = 64 per rank, 224^2 / 384^2,
+    # 24 MB buckets, the DP weight-gradient groups bench.py uses; tools/dp_full_parity.py)
+    B, L, H = (64, 32, 384) if mode == "c5full" else (64, 32, 224) if mode == "c2full" else (4, 32, 64)
     # c5: BASELINE configs[4] widths -- T5-large (24 layers, d 1024), 6 SGA blocks at 1024, e4m3
     # forward weight GEMMs, the DP weight-gradient groups dp.dp_t5_dw_groups(24) = (8, 8, 6, 2)
     ekw = dict(language_model="t5-large", num_blocks=6, fp8=True) if c5 else {}
@@ -58,7 +60,7 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
         return
-    groups = pkg.dp.dp_t5_dw_groups(24) if c5 else (4, 4, 3, 1)
+    groups = pkg.dp.dp_t5_dw_groups(24) if c5 else pkg.dp.dp_t5_dw_groups(12) if full else (4, 4, 3, 1)
     eng = pkg.engine.VQAEngine(sd, batch=B, seq_len=L, image_size=H, warmup=1, total=20, dropout=0.0,
                                seed=rank, pipeline=pipe, t5_dw_group=groups, device="cuda:0", **ekw)
     assert not c5 or (eng.t5_dw_groups == [8, 8, 6, 2] and eng.fp8)
@@ -71,7 +73,7 @@ def main():
     else:
         eng.load_batch(dev[0])
     shard = mode == "shard"
-    step = pkg.dp.DataParallelStep(eng, bucket_mb=24 if mode == "c5full" else 8, use_graph=graph,
+    step = pkg.dp.DataParallelStep(eng, bucket_mb=24 if full else 8, use_graph=graph,
                                    shard_optimizer=shard)
     if pipe:
         eng.prime(dev[0]["image_tensors"])
