@@ -140,8 +140,9 @@ typedef struct vqa_gemm_desc {
  * 13..16 64x192 / 128x192 (k-contiguous B only); 17..20 the LDS-patch convolution;
  * 21 64x64/2, 22 64x128/2, 23 128x64/2 with 128-deep k-tiles (no implicit im2col, no split-K);
  * 24 64x128/2 with 8 waves (2x4) and 128-deep k-tiles; 25 the LDS-patch convolution's 128x128 tile
- * with 8 waves (4x2) */
-#define VQA_GEMM_CONFIGS 25
+ * with 8 waves (4x2); 26 64x128, 27 128x64, 28 64x64 for k <= 64 only (one k-tile in a single-stage
+ * ring: more workgroups per CU; no implicit im2col) */
+#define VQA_GEMM_CONFIGS 28
 #define VQA_GEMM_PATCH_FIRST 17    /* configs 17..20 and VQA_GEMM_PATCH_WIDE: a_conv = 2 only */
 #define VQA_GEMM_PATCH_LAST 20
 #define VQA_GEMM_PATCH_WIDE 25

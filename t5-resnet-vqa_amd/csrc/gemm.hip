@@ -60,7 +60,8 @@ __global__ __launch_bounds__(256) void gemm_pair_kernel(GemmParams P1, GemmParam
 //         16 = 128x192 (3) -- 4 waves, k-contiguous B only;
 //         17..20 = the LDS-patch 3x3 convolution (a_conv = 2, conv_patch.inl): 128x64, 128x128,
 //         64x64, 64x128; 21..23 = 64x64 / 64x128 / 128x64 with 128-deep k-tiles (4 waves);
-//         24 = 64x128 with 128-deep k-tiles on 8 waves (2x4).
+//         24 = 64x128 with 128-deep k-tiles on 8 waves (2x4); 26 / 27 / 28 = 64x128 / 128x64 /
+//         64x64 for k <= 64 (one k-tile, single-stage ring: 4 / 4 / 5 workgroups per CU).
 // Every config accumulates each output element in the same K order (BK = 64
 // k-tiles, 16-deep MFMA steps), so the choice changes speed, never the bits.
 // Auto (measured on MI355X, tools/callprof.py): fewer stages = less LDS = more
@@ -115,6 +116,15 @@ int dispatch_tile(GemmParams& P, int batch, int config, hipStream_t s) {
       } else {
         return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: tile config %d takes no implicit-im2col operand", config);
       }
+    case 26: case 27: case 28:
+      // one k-tile in a single-stage ring (gemm_k1_kernel): k <= 64, plain operands
+      if constexpr (!GA && !GB) {
+        if (config == 26) return launch_k1<64, 128, 4, AKC, BKC, GA, GB>(P, batch, s);
+        if (config == 27) return launch_k1<128, 64, 4, AKC, BKC, GA, GB>(P, batch, s);
+        return launch_k1<64, 64, 5, AKC, BKC, GA, GB>(P, batch, s);
+      } else {
+        return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: tile config %d takes no implicit-im2col operand", config);
+      }
     default: return launch<64, 64, 4, 2, 2, AKC, BKC, GA, GB>(P, batch, s);
   }
 }
@@ -128,7 +138,7 @@ void tile_of(int config, int& bm, int& bn) {
                                                  {128, 256}, {256, 256}, {256, 128}, {64, 192}, {128, 192},
                                                  {64, 192},  {128, 192}, {128, 64}, {128, 128}, {64, 64},
                                                  {64, 128},  {64, 64},   {64, 128}, {128, 64}, {64, 128},
-                                                 {128, 128}};
+                                                 {128, 128}, {64, 128},  {128, 64}, {64, 64}};
   bm = T[config][0];
   bn = T[config][1];
 }

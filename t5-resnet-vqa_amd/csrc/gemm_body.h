@@ -254,6 +254,19 @@ __global__ __launch_bounds__(64 * NWM * NWN) void gemm_kernel(GemmParams P) {
   gemm_body<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB, false, BKT, F8>(P, blockIdx.x, smem);
 }
 
+// One k-tile (K <= 64: the frozen ResNet's 1x1 convolutions over 64 channels, tile configs 26-28):
+// the ring's second stage is never filled (the prologue issues k-tile 0 into stage 0 and the loop
+// issues nothing more), so the workgroup allocates ONE stage and the register target follows the
+// LDS: 64x128 / 128x64 in 24 KB at 4 workgroups per CU (the two-stage kernels: 48 KB and 140
+// VGPRs, 3 per CU), 64x64 in 16 KB at 5.  Same body, same k order: the bits do not change.
+template <int BM, int BN, int W, bool AKC, bool BKC, bool GA, bool GB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void gemm_k1_kernel(GemmParams P) {
+  // the epilogue parks one 32-row fragment group per pass (TM = 1 or 2 here): it must fit one stage
+  static_assert(32 * (BN + 4) * 4 <= TileCfg<BM, BN, 1>::LDS, "epilogue image must fit the single stage");
+  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<BM, BN, 1>::LDS];
+  gemm_body<BM, BN, 2, 2, 2, AKC, BKC, GA, GB>(P, blockIdx.x, smem);
+}
+
 // split-K workspace: a fixed 64 KiB counter block first (so any sequence of calls
 // sharing a workspace only ever finds zeros there), then the slabs
 constexpr long long SPLITK_CNT_BYTES = 65536;
@@ -280,6 +293,17 @@ int launch(GemmParams& P, int batch, hipStream_t s) {
   dim3 grid(P.tiles_m * P.tiles_n * (P.splitk > 1 ? P.splitk : 1), 1, batch);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, STAGES, NWM, NWN, AKC, BKC, GA, GB, BKT, F8>), grid, dim3(64 * NWM * NWN), 0,
                      s, P);
+  return vqa::check_launch("vqa_gemm");
+}
+
+template <int BM, int BN, int W, bool AKC, bool BKC, bool GA, bool GB>
+int launch_k1(GemmParams& P, int batch, hipStream_t s) {
+  if (P.k > BK || P.splitk > 1)
+    return vqa::fail(VQA_ERR_INVALID, "vqa_gemm: tile configs 26-28 take one k-tile (k <= %d), no split-K", BK);
+  P.tiles_m = vqa::cdiv(P.m, BM);
+  P.tiles_n = vqa::cdiv(P.n, BN);
+  dim3 grid(P.tiles_m * P.tiles_n, 1, batch);
+  hipLaunchKernelGGL((gemm_k1_kernel<BM, BN, W, AKC, BKC, GA, GB>), grid, dim3(256), 0, s, P);
   return vqa::check_launch("vqa_gemm");
 }
 

@@ -1829,10 +1829,12 @@ class VQAEngine:
                     tiles = -(-d.m // bm) * -(-d.n // bn) * max(1, d.batch)
                     if cfg in L.GEMM_BK128 and (d.a_conv or d.b_conv):
                         continue                           # 128-deep k-tiles: plain operands only
+                    if cfg in L.GEMM_K64_ONLY and (d.k > 64 or d.a_conv or d.b_conv):
+                        continue                           # one k-tile, plain operands only
                     for sk in SPLITS:
                         # split only grids that leave CUs idle, with >= 2 k-tiles per slice
                         if sk > 1 and (tiles >= 512 or nk < 2 * sk or tiles > 16384 or d.a_conv == 2
-                                       or cfg in L.GEMM_BK128):
+                                       or cfg in L.GEMM_BK128 or cfg in L.GEMM_K64_ONLY):
                             continue
                         d.config = cfg
                         ops.set_splitk(d, sk)

@@ -82,10 +82,12 @@ GEMM_TILES = {1: (128, 128, 3), 2: (128, 64, 4), 3: (64, 64, 4), 4: (64, 64, 2),
               7: (64, 128, 2), 8: (128, 128, 2), 9: (256, 128, 2), 10: (128, 256, 2), 11: (256, 256, 2),
               12: (256, 128, 3), 13: (64, 192, 2), 14: (128, 192, 2), 15: (64, 192, 3), 16: (128, 192, 3),
               17: (128, 64, 2), 18: (128, 128, 2), 19: (64, 64, 2), 20: (64, 128, 2),
-              21: (64, 64, 2), 22: (64, 128, 2), 23: (128, 64, 2), 24: (64, 128, 2), 25: (128, 128, 3)}
+              21: (64, 64, 2), 22: (64, 128, 2), 23: (128, 64, 2), 24: (64, 128, 2), 25: (128, 128, 3),
+              26: (64, 128, 1), 27: (128, 64, 1), 28: (64, 64, 1)}
 GEMM_PATCH_ONLY = (17, 18, 19, 20, 25)   # the LDS-patch 3x3 convolution (a_conv = 2) and nothing else
 GEMM_KC_B_ONLY = (13, 14, 15, 16)        # tile configs that need a k-contiguous B operand (b_trans = 0)
 GEMM_BK128 = (21, 22, 23, 24)            # 128-deep k-tiles: no implicit im2col operand, no split-K
+GEMM_K64_ONLY = (26, 27, 28)             # one k-tile in a single-stage ring: k <= 64, no implicit im2col, no split-K
 GEMM_FP8 = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 21, 22, 23)   # tile configs with an e4m3 form (gemm_fp8.hip)
 GEMM_WAVES = {c: ((4, 2) if c in (9, 12, 25) else (2, 4) if c in (10, 11, 24) else (2, 2)) for c in GEMM_TILES}
 

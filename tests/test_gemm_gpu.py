@@ -206,6 +206,8 @@ def test_all_tile_configs_bitwise_identical(ops, pkg, layout):
             continue
         if cfg in pkg.lib.GEMM_BK128 and layout in ("conv", "convw"):     # no implicit-im2col operand
             continue
+        if cfg in pkg.lib.GEMM_K64_ONLY:                  # k <= 64 only: test_k64_configs_bitwise_identical
+            continue
         out = torch.empty(M, N, device="cuda")
         d = mk(out)
         d.config = cfg
@@ -285,7 +287,7 @@ def test_splitk_matches_reference_and_is_config_invariant(ops, pkg, layout, spli
         scale = 0.5 * (A.abs() @ Bm.abs()).max().item()
     outs = []
     cfgs = [c for c in sorted(pkg.lib.GEMM_TILES) if (layout in ("AB", "conv") or c not in pkg.lib.GEMM_KC_B_ONLY)
-            and c not in pkg.lib.GEMM_PATCH_ONLY and c not in pkg.lib.GEMM_BK128]
+            and c not in pkg.lib.GEMM_PATCH_ONLY and c not in pkg.lib.GEMM_BK128 and c not in pkg.lib.GEMM_K64_ONLY]
     for cfg in cfgs:
         out = torch.full((M, N), float("nan"), device="cuda")
         d = mk(out)
@@ -302,6 +304,65 @@ def test_splitk_matches_reference_and_is_config_invariant(ops, pkg, layout, spli
     close(outs[0], ref, scale)
     for cfg, o in zip(cfgs[1:], outs[1:]):
         assert torch.equal(o, outs[0]), f"config {cfg} differs at splitk={splitk}"
+
+
+@pytest.mark.parametrize("layout", ["AB", "ABt", "AtB", "AtBt"])
+@pytest.mark.parametrize("K", [64, 40])
+def test_k64_configs_bitwise_identical(ops, pkg, layout, K):
+    """Tile configs 26-28 (one k-tile in a single-stage ring, k <= 64) against every other plain
+    config at the ResNet's 1x1-conv epilogues: bias + bf16 residual + ReLU into bf16 (the expand
+    convolutions) and bias + fp32 residual + dropout into fp32 -- bit for bit, M and N ragged."""
+    M, N = 1000, 264
+    at, bt = layout in ("AtBt", "AtB"), layout in ("ABt", "AtBt")
+    a = bf((K, M) if at else (M, K), seed=41)
+    b = bf((K, N) if bt else (N, K), seed=42)
+    bias = torch.randn(N, device="cuda")
+    res16 = bf((M, N), seed=43)
+    res32 = torch.randn(M, N, device="cuda")
+    rng = torch.tensor([1, 2, 1], dtype=torch.int32, device="cuda")
+    for form in ("expand", "dropout"):
+        outs, cfgs = [], []
+        for cfg in sorted(pkg.lib.GEMM_TILES):
+            if cfg in pkg.lib.GEMM_PATCH_ONLY or (cfg in pkg.lib.GEMM_KC_B_ONLY and bt):
+                continue
+            if form == "expand":
+                out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+                d = ops.gemm_desc(a, b, M, N, K, lda=M if at else K, ldb=N if bt else K, a_trans=at, b_trans=bt,
+                                  c16=out, ldc16=N, bias=bias, res16=res16, ldres=N, relu=True)
+            else:
+                out = torch.empty(M, N, device="cuda")
+                d = ops.gemm_desc(a, b, M, N, K, lda=M if at else K, ldb=N if bt else K, a_trans=at, b_trans=bt,
+                                  c32=out, ldc32=N, bias=bias, res32=res32, ldres=N)
+                d.drop = pkg.lib.Dropout(0.1, 3, rng.data_ptr())
+            d.config = cfg
+            ops.run(d)
+            outs.append(out)
+            cfgs.append(cfg)
+        torch.cuda.synchronize()
+        assert set(pkg.lib.GEMM_K64_ONLY) <= set(cfgs)
+        for cfg, o in zip(cfgs[1:], outs[1:]):
+            assert torch.equal(o, outs[0]), f"{form}: config {cfg} differs from config {cfgs[0]}"
+
+
+def test_k64_configs_refuse_deeper_k_and_conv(ops, pkg):
+    """Configs 26-28 hold one k-tile: k > 64 and the implicit-im2col operands are refused with an
+    error, not run wrongly."""
+    M, N, K = 128, 128, 128
+    a, b = bf((M, K), seed=5), bf((N, K), seed=6)
+    out = torch.empty(M, N, device="cuda")
+    x = bf((2, 7, 7, 64), seed=7)
+    wt = bf((64, 3, 3, 64), 0.05, seed=8)
+    g = ops.conv_geom(2, 7, 7, 64, 7, 7, 3, 3, 1, 1)
+    out2 = torch.empty(98, 64, device="cuda")
+    for cfg in pkg.lib.GEMM_K64_ONLY:
+        d = ops.gemm_desc(a, b, M, N, K, lda=K, ldb=K, c32=out, ldc32=N)
+        d.config = cfg
+        with pytest.raises(RuntimeError):
+            ops.run(d)
+        d = ops.gemm_desc(x, wt, 98, 64, 576, lda=576, ldb=576, c32=out2, ldc32=64, ga=g)
+        d.config = cfg
+        with pytest.raises(RuntimeError):
+            ops.run(d)
 
 
 def test_bk128_configs_refuse_split_k_and_conv(ops, pkg):
