@@ -6,6 +6,8 @@ bit for bit.  Multi-rank arithmetic is covered by tests/test_dp_cpu.py and
 tests/test_a_dp2_gpu.py (gloo)."""
 import os
 import socket
+import subprocess
+import sys
 
 import pytest
 import torch
@@ -13,9 +15,33 @@ import torch.distributed as dist
 
 pytestmark = pytest.mark.gpu
 
+# The world-1 RCCL group -- and the communicator's threads -- live only in a child process that runs
+# this module's cases: one r06 full-suite run segfaulted inside hipGraphLaunch of a plain engine
+# graph replayed in the same process as a live RCCL communicator (the next run of the same tree
+# passed; DESIGN §3.8, "Graph hygiene").  The parent process never initialises RCCL.
+_CHILD = os.environ.get("VQA_DP_CHILD") == "1"
+
+
+def test_dp_world1_cases_in_a_child_process():
+    if _CHILD:
+        pytest.skip("the child runs the cases themselves")
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-u", "-m", "pytest", os.path.abspath(__file__), "-m", "gpu", "-x", "-v",
+                        "-p", "no:cacheprovider", "--timeout", "300", "--timeout-method", "thread"],
+                       cwd=root, env={**os.environ, "VQA_DP_CHILD": "1"}, timeout=370, capture_output=True, text=True)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0, f"world-1 RCCL cases failed in the child (rc {r.returncode})"
+    import re
+    m = re.search(r"(\d+) passed", r.stdout)
+    assert m and int(m.group(1)) == 6 and "failed" not in r.stdout, "the child must run and pass all 6 cases"
+
 
 @pytest.fixture(scope="module")
 def pg(pkg):
+    if not _CHILD:
+        pytest.skip("runs in the child process (test_dp_world1_cases_in_a_child_process)")
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     s = socket.socket()
